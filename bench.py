@@ -1,0 +1,271 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X EC + checksum hot path (driver contract: one JSON line on rank 0).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|crc|e2e]
+
+Default workload = BASELINE.json configs[1]: rs-6-3-1024k encode of 4096 stripes, device-resident on one
+MI355X.  A "step" is one ozec_encode_batch over the whole 4096-stripe batch (24 GiB of data cells read,
+12 GiB of parity written).  For N > 1 (torchrun) every rank encodes its own 4096 stripes on its own GPU
+(stripes are independent: no collective on the data path, "scaling": "weak"); RCCL is used only for the
+start/stop barriers and the max-over-ranks reduction of the elapsed time.
+
+value      = data bytes of all ranks / max-over-ranks wall time of the K timed steps (GB = 1e9 B)
+roofline   = algorithmic bytes per launch (9 x 1 MiB per stripe x 4096) / mean kernel time measured with
+             HIP events on the launch stream, against 8.0 TB/s; traffic = rocprofv3 PMC bytes per launch
+             read from profiles/traffic_<workload>.json when it has been measured, else null
+cpu_baseline (rank 0, N = 1): the oracle/ C port of RSUtil.encodeData timed on this host's cores on a
+             bounded sample (threads share one coder, as RawErasureCoderBenchmark.java:201-206 does)
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+MIB = 1 << 20
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+SEED = 0x00EC5EED
+METRIC = "EC encode GB/s (data bytes) rs-6-3-1024k @1/8 GPUs + % HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "crc", "e2e"])
+    ap.add_argument("--stripes", type=int, default=0, help="override the stripe count (profiling only)")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------------------ workloads
+
+
+class Workload:
+    """Allocates device-resident inputs once; step() launches one batch on the current stream."""
+
+    def __init__(self, name, rank, stripes_override):
+        from ozone_amd import checksum as ck
+        from ozone_amd import rawcoder as rc
+        self.name = name
+        dev = torch.device("cuda", torch.cuda.current_device())
+        n = MIB
+        self.n = n
+        if name in ("c2", "c5", "e2e"):
+            k, p, S = 6, 3, stripes_override or (4096 if name != "e2e" else 1024)
+        elif name == "c3":
+            k, p, S = 10, 4, stripes_override or 2048
+        elif name == "c4":
+            k, p, S = 2, 1, stripes_override or 16 * 256
+        else:  # crc
+            k, p, S = 1, 0, stripes_override or 8192
+        self.k, self.p, self.S = k, p, S
+        self.bpc = 16384
+        self.nwin = n // self.bpc
+        self.crc_type = ck.ChecksumType.CRC32C
+        if name == "crc":
+            self.data = torch.empty((S, n), dtype=torch.uint8, device=dev)
+            rc.fill_splitmix64_cells(self.data, n, S, n, SEED, rank * 10_000_000)
+            self.crcs = torch.empty((S, self.nwin), dtype=torch.int32, device=dev)
+            self.data_bytes = S * n
+            self.alg_bytes = S * n + S * self.nwin * 4
+            self.kernel = "crc_windows_vec"
+            self.config = {"workload": "CRC32C per 16 KiB window, device-resident", "cells": S, "cell_bytes": n,
+                           "bytes_per_checksum": self.bpc}
+            self._step = lambda: ck.checksum_windows_batch(self.crc_type, self.data, n, S, n, self.bpc, self.crcs)
+            torch.cuda.synchronize()
+            return
+        units = k + p
+        if name == "e2e":
+            self.host_in = torch.empty((S, k, n), dtype=torch.uint8).pin_memory()
+            self.host_out = torch.empty((S, p, n), dtype=torch.uint8).pin_memory()
+            self.host_crc = torch.empty((S, units, self.nwin), dtype=torch.int32).pin_memory()
+            tmp = torch.empty((S, k, n), dtype=torch.uint8, device=dev)
+            rc.fill_splitmix64_cells(tmp, n, S * k, n, SEED, rank * 10_000_000)
+            self.host_in.copy_(tmp)
+            del tmp
+        # HBM layout: stripe-major, units contiguous: unit u of stripe s at s*(k+p)*n + u*n
+        self.units = torch.empty((S, units, n), dtype=torch.uint8, device=dev)
+        for u in range(k):
+            rc.fill_splitmix64_cells(self.units[:, u], units * n, S, n, SEED, rank * 10_000_000 + u * S)
+        enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, "rs" if name != "c4" else "xor"))
+        self.enc = enc
+        stride = units * n
+        if name == "c2":
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * units * n
+            self.kernel = "gf_code_vec<6,3>"
+            self.config = {"workload": "rs-6-3-1024k encode, 4096 stripes, device-resident (BASELINE configs[1])",
+                           "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
+                           "layout": "stripe-major [stripe][unit][cell] in HBM"}
+            self._step = lambda: enc.encode_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n)
+        elif name == "c3":
+            enc.encode_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n)
+            self.dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
+            self.erased = [0, 1, 2, 3]
+            present = [u for u in range(units) if u not in self.erased]
+            self.out = torch.empty((S, 4, n), dtype=torch.uint8, device=dev)
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * (k + len(self.erased)) * n
+            self.kernel = "gf_code_vec<10,4>"
+            self.config = {"workload": "rs-10-4-1024k decode, 2048 stripes, 4 erased {0,1,2,3}, device-resident",
+                           "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S}
+            self._step = lambda: self.dec.decode_batch(self.units, stride, n, present, self.erased, self.out, 4 * n,
+                                                       n, S, n)
+        elif name in ("c4", "c5"):
+            self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * units * n + S * units * self.nwin * 4
+            self.kernel = f"encode_crc_vec<{k},{p}>"
+            wl = ("xor-2-1-1024k + CRC32C/16 KiB, 16 block groups x 256 stripes" if name == "c4"
+                  else "rs-6-3-1024k encode + CRC32C/16 KiB, 4096 stripes")
+            self.config = {"workload": wl + ", fused, device-resident", "codec": "xor" if name == "c4" else "rs",
+                           "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
+                           "bytes_per_checksum": self.bpc}
+            self._step = lambda: enc.encode_crc_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n,
+                                                      self.crc_type, self.bpc, self.crcs)
+        else:  # e2e: pinned host -> HBM -> fused encode+CRC -> host, chunked over 2 streams
+            self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * units * n
+            self.kernel = "encode_crc_vec<6,3> (+H2D/D2H)"
+            self.config = {"workload": "rs-6-3-1024k + CRC32C end-to-end from pinned host buffers", "stripes": S}
+            self.streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+            self._step = self._e2e_step
+        torch.cuda.synchronize()
+
+    def _e2e_step(self):
+        k, p, n, S = self.k, self.p, self.n, self.S
+        stride = (k + p) * n
+        chunk = 64
+        for i, s0 in enumerate(range(0, S, chunk)):
+            st = self.streams[i % 2]
+            s1 = min(S, s0 + chunk)
+            with torch.cuda.stream(st):
+                self.units[s0:s1, :k].copy_(self.host_in[s0:s1], non_blocking=True)
+                self.enc.encode_crc_batch(self.units[s0:], stride, n, self.units[s0:, k:], stride, n, s1 - s0, n,
+                                          self.crc_type, self.bpc, self.crcs[s0:], stream=st)
+                self.host_out[s0:s1].copy_(self.units[s0:s1, k:], non_blocking=True)
+                self.host_crc[s0:s1].copy_(self.crcs[s0:s1], non_blocking=True)
+        for st in self.streams:
+            torch.cuda.current_stream().wait_stream(st)
+
+    def step(self):
+        self._step()
+
+
+# ------------------------------------------------------------------------------------------ CPU baseline
+
+
+def cpu_baseline(budget_s):
+    """oracle/ (C port of RSUtil.encodeData) on this host: T threads share one coder; bounded sample."""
+    import oracle
+    from synth import cells
+    threads = min(16, os.cpu_count() or 1)
+    k, p, n = 6, 3, MIB
+    data = cells(SEED, 900, k, n)
+    oracle.rs_encode(k, p, data)  # warm the tables
+    done = [0] * threads
+    stop = time.perf_counter() + budget_s
+
+    def worker(i):
+        while time.perf_counter() < stop:
+            oracle.rs_encode(k, p, data)
+            done[i] += 1
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    el = time.perf_counter() - t0
+    stripes = sum(done)
+    return {"value": round(stripes * k * n / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{stripes} rs-6-3-1024k stripes encoded by {threads} threads sharing one coder in "
+                      f"{el:.1f} s wall (oracle/ozec_oracle.c, C restatement of RSUtil.encodeData, gcc -O3)"}
+
+
+# ------------------------------------------------------------------------------------------ main
+
+
+def main():
+    args = parse()
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    wl = Workload(args.workload, rank, args.stripes)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        wl.step()
+    barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record()
+        wl.step()
+        b.record()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = wl.data_bytes * world * args.steps / elapsed / 1e9
+    achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    result = {
+        "metric": METRIC if args.workload == "c2" else f"{args.workload}: data GB/s",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 bytes generated in HBM)",
+        "config": dict(wl.config, parallelism=f"stripe-sharded x{world} (independent stripes, no collective)"),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                     "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4),
+                     "alg_bytes_per_launch": wl.alg_bytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu and args.workload in ("c2", "e2e"):
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+/*
+ * ozec.h -- C ABI of libozec.so, the MI355X (gfx950) erasure-coding + chunk-checksum engine.
+ *
+ * This is the drop-in boundary for Ozone's EC raw-coder and chunk-checksum hot path.  Every entry point
+ * takes plain pointers and sizes (no Java, Python or torch types) so a JNI shim, ctypes or any C caller can
+ * bind it.  Each block below cites the reference interface it replaces (paths relative to the reference
+ * checkout, EC/ = hadoop-hdds/erasurecode/src/main/java/org/apache/ozone/erasurecode/,
+ * CM/ = hadoop-hdds/common/src/main/java/org/apache/hadoop/ozone/common/).  INTEGRATION.md shows the JNI
+ * binding a maintainer would add on the Java side.
+ *
+ * Conventions
+ *   - Return codes: 0 = OK, negative = error (OZEC_E*). ozec_last_error() returns a thread-local message
+ *     mirroring the reference's exception text ("Not invertible", "... closed", "Invalid inputs length").
+ *   - "host" entry points take host pointers (any alignment, pageable or pinned) and are synchronous, like
+ *     RawErasureEncoder.encode (EC/rawcoder/RawErasureEncoder.java:66-97).  They stage through a
+ *     process-global, per-GPU pinned buffer pool.
+ *   - "_device" / "_batch" entry points take device pointers and an optional hipStream_t (NULL = the
+ *     library's stream for the current device) and are asynchronous on that stream.
+ *   - Outputs are fully overwritten (the reference zero-fills, then accumulates: CoderUtil.java:84-98).
+ *   - Inputs are never modified (TestRawCoderBase.java:180-220).
+ */
+#ifndef OZEC_H
+#define OZEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes --------------------------------------------------------------------------- */
+#define OZEC_OK 0
+#define OZEC_EINVAL (-1)          /* HadoopIllegalArgumentException / IllegalArgumentException          */
+#define OZEC_ENOTINVERTIBLE (-2)  /* RuntimeException("Not invertible"), GF256.java:214-217              */
+#define OZEC_EDEVICE (-3)         /* HIP runtime error / no device                                       */
+#define OZEC_ECLOSED (-4)         /* IOException("... closed") after release(), TestRawCoderBase.java:118-134 */
+#define OZEC_ENOMEM (-5)
+#define OZEC_EUNSUPPORTED (-6)    /* schema outside the compiled limits (k > OZEC_MAX_K, rows > OZEC_MAX_ROWS) */
+#define OZEC_EMISMATCH (-7)       /* OzoneChecksumException: checksum mismatch, ChecksumData.java:118-150 */
+
+/* ---- codecs and checksum types ------------------------------------------------------------ */
+#define OZEC_CODEC_RS 0           /* ECReplicationConfig.EcCodec.RS  (hdds/client/ECReplicationConfig.java:44) */
+#define OZEC_CODEC_XOR 1          /* ECReplicationConfig.EcCodec.XOR                                  */
+/* numeric values follow ChecksumType in DatanodeClientProtocol.proto:422-434 */
+#define OZEC_CHECKSUM_NONE 1
+#define OZEC_CHECKSUM_CRC32 2
+#define OZEC_CHECKSUM_CRC32C 3
+
+#define OZEC_MAX_K 64             /* data units handled by the GPU kernels      */
+#define OZEC_MAX_ROWS 16          /* parity rows / erased units per call        */
+
+typedef struct ozec_coder ozec_coder; /* opaque encoder or decoder handle */
+
+/* ---- library / device ------------------------------------------------------------------------ */
+const char *ozec_last_error(void);
+int ozec_version(void);
+/* number of visible GPUs; 0 when none (the factory then throws, so CodecUtil falls back to rs_java:
+ * CodecUtil.createRawEncoderWithFallback, EC/rawcoder/util/CodecUtil.java:55-82) */
+int ozec_device_count(void);
+/* select the GPU used by subsequently created coders and host calls on this thread */
+int ozec_set_device(int device);
+int ozec_synchronize(void);
+
+/* ---- coder lifecycle: RawErasureCoderFactory.createEncoder/createDecoder
+ *      (EC/rawcoder/RawErasureCoderFactory.java:29-56), RSRawEncoder/RSRawDecoder ctors
+ *      (EC/rawcoder/RSRawEncoder.java:39-58, RSRawDecoder.java:57-71), XORRawEncoder/Decoder ctors,
+ *      and the ISA-L bridge's initImpl (EC/rawcoder/NativeRSRawEncoder.java:39-51). ------------- */
+int ozec_encoder_create(int codec, int num_data, int num_parity, ozec_coder **out);
+int ozec_decoder_create(int codec, int num_data, int num_parity, ozec_coder **out);
+/* RawErasureEncoder.release / RawErasureDecoder.release: idempotent; later calls return OZEC_ECLOSED */
+int ozec_coder_release(ozec_coder *coder);
+/* free the handle itself (the Java object's cleaner / Python __del__) */
+void ozec_coder_free(ozec_coder *coder);
+int ozec_coder_info(const ozec_coder *coder, int *codec, int *num_data, int *num_parity, int *is_decoder);
+
+/* ---- encode: RawErasureEncoder.doEncode -> RSUtil.encodeData (EC/rawcoder/util/RSUtil.java:87-133),
+ *      XORRawEncoder.doEncode (EC/rawcoder/XORRawEncoder.java:39-85); the JNI counterpart of
+ *      hadoop's NativeRSRawEncoder.performEncodeImpl(inputs, inputOffsets, dataLen, outputs, outputOffsets)
+ *      called from AbstractNativeRawEncoder.doEncode (EC/rawcoder/AbstractNativeRawEncoder.java:49-73).
+ *      inputs[num_data], outputs[num_parity]: host pointers already advanced to position/offset. -------- */
+int ozec_encode(ozec_coder *enc, const uint8_t *const *inputs, uint8_t *const *outputs, size_t len);
+
+/* ---- decode: RawErasureDecoder.decode -> RSRawDecoder.doDecode (EC/rawcoder/RSRawDecoder.java:73-115),
+ *      XORRawDecoder.doDecode (EC/rawcoder/XORRawDecoder.java:40-86); JNI counterpart of
+ *      performDecodeImpl(inputs, inOffsets, dataLen, erased, outputs, outOffsets)
+ *      (EC/rawcoder/AbstractNativeRawDecoder.java:49-75).
+ *      inputs[num_data + num_parity]: NULL = erased or not read; the first num_data non-NULL inputs in
+ *      ascending index order are used (RSRawDecoder.java:79-82).  erased[i] <-> outputs[i]. ----------- */
+int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased, int num_erased,
+                uint8_t *const *outputs, size_t len);
+
+/* ---- device-resident forms (same semantics, device pointers, async on `stream`) ---------------------- */
+int ozec_encode_device(ozec_coder *enc, const uint8_t *const *d_inputs, uint8_t *const *d_outputs,
+                       size_t len, void *stream);
+int ozec_decode_device(ozec_coder *dec, const uint8_t *const *d_inputs, const int *erased,
+                       int num_erased, uint8_t *const *d_outputs, size_t len, void *stream);
+
+/* Batched stripes, the layout the datanode/bench keeps in HBM: unit u (0 <= u < k+p) of stripe s lives at
+ *   base + s * stripe_stride + u * unit_stride            (bytes; any strides, 16-B aligned is fast)
+ * encode reads units 0..k-1 of `d_in` and writes parity unit j to d_out + s*out_stripe_stride + j*out_unit_stride.
+ * This is the batch entry SURVEY.md §7 "One stripe per call" asks for; the per-stripe semantics are exactly
+ * RSUtil.encodeData's. */
+int ozec_encode_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride,
+                      int64_t in_unit_stride, uint8_t *d_out, int64_t out_stripe_stride,
+                      int64_t out_unit_stride, size_t num_stripes, size_t len, void *stream);
+/* decode a batch: `present` lists which of the k+p units are readable (ascending or not; the decoder uses
+ * the first num_data in ascending order, as the reference does); erased[i] is written to
+ * d_out + s*out_stripe_stride + i*out_unit_stride. */
+int ozec_decode_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_stripe_stride,
+                      int64_t in_unit_stride, const int *present, int num_present, const int *erased,
+                      int num_erased, uint8_t *d_out, int64_t out_stripe_stride,
+                      int64_t out_unit_stride, size_t num_stripes, size_t len, void *stream);
+
+/* Fused encode + per-window checksum (north_star: "fused with encode, so each cell is read from HBM only
+ * once").  crcs[s][u][w] (uint32, value of (int)getValue(), Checksum.java:59-70) for u in 0..k+p-1
+ * (data then parity) and w in 0..ceil(len/bpc)-1.  big_endian != 0 stores each CRC byte-swapped, i.e.
+ * exactly the 4 bytes Ints.toByteArray / Checksum.int2ByteString would produce. */
+int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride,
+                          int64_t in_unit_stride, uint8_t *d_out, int64_t out_stripe_stride,
+                          int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
+                          size_t bytes_per_checksum, uint32_t *d_crcs, int big_endian, void *stream);
+
+/* ---- chunk checksums: Checksum.computeChecksum(ByteBuffer / ChunkBuffer) (CM/Checksum.java:132-200) with
+ *      ChunkBufferImplWithByteBuffer.iterate(bytesPerChecksum) (CM/ChunkBufferImplWithByteBuffer.java:78-98)
+ *      and ChecksumByteBufferImpl/CrcIntTable per window (CM/ChecksumByteBuffer.java:51-121).
+ *      One uint32 per window: ceil(len / bpc) values (0 for len == 0). ---------------------------------- */
+int ozec_checksum_windows(int checksum_type, const uint8_t *data, size_t len, size_t bytes_per_checksum,
+                          uint32_t *out, int big_endian);
+int ozec_checksum_windows_device(int checksum_type, const uint8_t *d_data, size_t len,
+                                 size_t bytes_per_checksum, uint32_t *d_out, int big_endian, void *stream);
+/* many equally sized cells: cell c at d_base + c*cell_stride; out[c][w] */
+int ozec_checksum_windows_batch(int checksum_type, const uint8_t *d_base, int64_t cell_stride,
+                                size_t num_cells, size_t len, size_t bytes_per_checksum, uint32_t *d_out,
+                                int big_endian, void *stream);
+/* Checksum.verifyChecksum + ChecksumData.verifyChecksumDataMatches (CM/Checksum.java:241-297,
+ * CM/ChecksumData.java:118-150): recompute and compare against expected[start_index ...].  Returns 0 when all
+ * match, OZEC_EMISMATCH with *mismatch_index set to the first bad window otherwise. */
+int ozec_checksum_verify(int checksum_type, const uint8_t *data, size_t len, size_t bytes_per_checksum,
+                         const uint32_t *expected, size_t num_expected, size_t start_index,
+                         int64_t *mismatch_index);
+
+/* ---- streaming ChecksumByteBuffer (CM/ChecksumByteBuffer.java:32-44): update(ByteBuffer) / getValue /
+ *      reset over an opaque 32-bit state.  The GPU computes the raw CRC of the buffer and the host combines
+ *      it with the running state (x^(8n) mod P shift), so results equal the sequential CrcIntTable. ---- */
+uint32_t ozec_crc_reset(int checksum_type);
+int ozec_crc_update(int checksum_type, uint32_t *state, const uint8_t *data, size_t len);
+uint32_t ozec_crc_value(int checksum_type, uint32_t state); /* getValue() = ~state */
+
+/* ---- host-side coding math (no GPU needed; exported for parity tests and for a Java-side cache) -------- */
+/* RSUtil.genCauchyMatrix (EC/rawcoder/util/RSUtil.java:64-77): (k+p) x k, row-major */
+int ozec_rs_encode_matrix(int num_data, int num_parity, uint8_t *matrix);
+/* RSRawDecoder.generateDecodeMatrix (EC/rawcoder/RSRawDecoder.java:143-176) incl. its erased-order quirk */
+int ozec_rs_decode_matrix(int num_data, int num_parity, const int *valid_indexes, const int *erased,
+                          int num_erased, uint8_t *decode_matrix);
+/* GF256.gfInvertMatrix (EC/rawcoder/util/GF256.java:191-250); `in` is clobbered like the reference's */
+int ozec_gf_invert_matrix(uint8_t *in, uint8_t *out, int n);
+uint8_t ozec_gf_mul(uint8_t a, uint8_t b);
+/* ECReplicationConfig(String) parser (hdds/client/ECReplicationConfig.java:96-130): "rs-6-3-1024k" */
+int ozec_parse_replication(const char *s, int *codec, int *num_data, int *num_parity, int *chunk_size);
+/* crc(A||B) from crc(A), crc(B), |B| -- the combine primitive behind streaming update and stripe checksums */
+uint32_t ozec_crc_combine(int checksum_type, uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* ---- harness utilities ------------------------------------------------------------------------------- */
+/* fill n bytes with splitmix64 stream `stream_id` of `seed` (tests/golden/synth.py is the CPU twin) */
+int ozec_fill_splitmix64(uint8_t *d_dst, size_t n, uint64_t seed, uint64_t stream_id, void *stream);
+/* same, many cells: cell c (stream first_stream + c) at d_base + c*cell_stride */
+int ozec_fill_splitmix64_cells(uint8_t *d_base, int64_t cell_stride, size_t num_cells, size_t n,
+                               uint64_t seed, uint64_t first_stream, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OZEC_H */

@@ -1,0 +1,758 @@
+// extern "C" implementation of include/ozec.h.
+//
+// Runtime model (SURVEY.md §7 "Lifetime"): coders are cheap host handles holding only coding matrices and a
+// decode-matrix cache; all device state (stream, pinned staging pool, device scratch, CRC tables) is a
+// process-global, lazily created context per GPU, shared by every coder and safe to use from many threads.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <regex>
+#include <string>
+#include <vector>
+
+#include "../../include/ozec.h"
+#include "crc_host.hpp"
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+namespace {
+
+using ozec::CodeArgs;
+using ozec::CrcArgs;
+using ozec::CrcMath;
+using ozec::CrcType;
+
+thread_local std::string g_error;
+
+int fail(int code, const std::string &msg) {
+  g_error = msg;
+  return code;
+}
+
+#define OZEC_HIP(call)                                                                              \
+  do {                                                                                              \
+    hipError_t err_ = (call);                                                                       \
+    if (err_ != hipSuccess) return fail(OZEC_EDEVICE, std::string("HIP error: ") + hipGetErrorString(err_) + \
+                                                          " at " #call);                            \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// per-GPU context
+
+struct DevCtx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  std::mutex mu;  // guards the staging buffers below
+  uint8_t *pinned = nullptr;
+  size_t pinned_cap = 0;
+  uint8_t *dbuf = nullptr;
+  size_t dbuf_cap = 0;
+  uint32_t *crc_tables[2] = {nullptr, nullptr};
+
+  int reserve(size_t bytes) {
+    if (bytes > pinned_cap) {
+      if (pinned) (void)hipHostFree(pinned);
+      pinned = nullptr;
+      pinned_cap = 0;
+      size_t cap = std::max<size_t>(bytes, 1 << 20);
+      OZEC_HIP(hipHostMalloc(reinterpret_cast<void **>(&pinned), cap, hipHostMallocDefault));
+      pinned_cap = cap;
+    }
+    if (bytes > dbuf_cap) {
+      if (dbuf) (void)hipFree(dbuf);
+      dbuf = nullptr;
+      dbuf_cap = 0;
+      size_t cap = std::max<size_t>(bytes, 1 << 20);
+      OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&dbuf), cap));
+      dbuf_cap = cap;
+    }
+    return OZEC_OK;
+  }
+};
+
+std::mutex g_ctx_mu;
+std::vector<std::unique_ptr<DevCtx>> g_ctx;
+
+// current device of the calling thread, with its context created on first use
+int get_ctx(DevCtx **out) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(OZEC_EDEVICE, "no HIP device available");
+  int dev = 0;
+  OZEC_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  if (g_ctx.size() < static_cast<size_t>(n)) g_ctx.resize(n);
+  if (!g_ctx[dev]) {
+    auto c = std::make_unique<DevCtx>();
+    c->device = dev;
+    OZEC_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int t = 0; t < 2; ++t) {
+      const auto &blob = CrcMath::get(static_cast<CrcType>(t)).device_tables();
+      OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->crc_tables[t]), blob.size() * sizeof(uint32_t)));
+      OZEC_HIP(hipMemcpy(c->crc_tables[t], blob.data(), blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    g_ctx[dev] = std::move(c);
+  }
+  *out = g_ctx[dev].get();
+  return OZEC_OK;
+}
+
+hipStream_t pick_stream(DevCtx *ctx, void *stream) {
+  return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+constexpr size_t kStageAlign = 256;
+inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+int crc_type_of(int checksum_type, CrcType *t) {
+  if (checksum_type == OZEC_CHECKSUM_CRC32) *t = CrcType::kCrc32;
+  else if (checksum_type == OZEC_CHECKSUM_CRC32C) *t = CrcType::kCrc32c;
+  else return fail(OZEC_EINVAL, "unsupported checksum type " + std::to_string(checksum_type) +
+                                    " (GPU path covers CRC32=2 and CRC32C=3)");
+  return OZEC_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// coder handle
+
+struct ozec_coder {
+  int codec = OZEC_CODEC_RS;
+  int k = 0, p = 0;
+  bool decoder = false;
+  std::atomic<bool> closed{false};
+  std::vector<uint8_t> parity_rows;  // p x k (RS) -- RSRawEncoder's encodeMatrix rows k..k+p-1
+  // decode cache on (erased, valid) like RSRawDecoder.prepareDecoding (RSRawDecoder.java:103-115)
+  std::mutex cache_mu;
+  bool cache_set = false;
+  std::vector<int> cached_erased, cached_valid;
+  std::vector<uint8_t> cached_rows;
+};
+
+namespace {
+
+int check_open(const ozec_coder *c, const char *what) {
+  if (!c) return fail(OZEC_EINVAL, "null coder");
+  if (c->closed.load()) return fail(OZEC_ECLOSED, std::string(what) + " failed: the coder is closed");
+  return OZEC_OK;
+}
+
+// Build the rows x k job for a decode: resolves the units to read and the coefficient rows.
+// Mirrors DecodingState.checkParameters (DecodingState.java:35-51), ByteBufferDecodingState input checks
+// (ByteBufferDecodingState.java:103-130) and RSRawDecoder.prepareDecoding/processErasures.
+int plan_decode(ozec_coder *dec, const bool *present, const int *erased, int n_erased, std::vector<int> &read_units,
+                std::vector<uint8_t> &rows) {
+  const int n_all = dec->k + dec->p;
+  if (n_erased > dec->p) return fail(OZEC_EINVAL, "Too many erased, not recoverable");
+  if (n_erased < 0 || (n_erased > 0 && !erased)) return fail(OZEC_EINVAL, "erasedIndexes and outputs mismatch in length");
+  for (int i = 0; i < n_erased; ++i)
+    if (erased[i] < 0 || erased[i] >= n_all)
+      return fail(OZEC_EINVAL, "erased index " + std::to_string(erased[i]) + " out of range");
+  std::vector<int> valid;
+  for (int u = 0; u < n_all; ++u)
+    if (present[u]) valid.push_back(u);
+  if (static_cast<int>(valid.size()) < dec->k)
+    return fail(OZEC_EINVAL, "No enough valid inputs are provided (" + std::to_string(valid.size()) + " vs. " +
+                                 std::to_string(dec->k) + "), not recoverable");
+  if (dec->codec == OZEC_CODEC_XOR) {
+    // XORRawDecoder.doDecode (XORRawDecoder.java:40-86): XOR every slot except erasedIndexes[0]
+    if (n_erased == 0) {
+      rows.clear();
+      read_units.clear();
+      return OZEC_OK;
+    }
+    read_units.clear();
+    for (int u = 0; u < n_all; ++u) {
+      if (u == erased[0]) continue;
+      if (!present[u]) return fail(OZEC_EINVAL, "input " + std::to_string(u) + " is null (XOR decode reads every unit)");
+      read_units.push_back(u);
+    }
+    rows.assign(read_units.size() * static_cast<size_t>(n_erased), 1);
+    return OZEC_OK;
+  }
+  read_units.assign(valid.begin(), valid.begin() + dec->k);
+  std::lock_guard<std::mutex> lk(dec->cache_mu);
+  std::vector<int> er(erased, erased + n_erased);
+  if (!dec->cache_set || er != dec->cached_erased || valid != dec->cached_valid) {
+    std::vector<uint8_t> r;
+    if (!ozec::decode_matrix(dec->k, dec->p, read_units.data(), erased, n_erased, r))
+      return fail(OZEC_ENOTINVERTIBLE, "Not invertible");
+    dec->cached_erased = er;
+    dec->cached_valid = valid;
+    dec->cached_rows = r;
+    dec->cache_set = true;
+  }
+  rows = dec->cached_rows;
+  return OZEC_OK;
+}
+
+void fill_coef(CodeArgs &a, int rows, int k, const uint8_t *coef) {
+  a.k = k;
+  a.rows = rows;
+  std::memcpy(a.coef, coef, static_cast<size_t>(rows) * k);
+  a.all_ones = 1;
+  for (int i = 0; i < rows * k; ++i) a.all_ones &= coef[i] == 1;
+}
+
+int check_limits(int k, int rows) {
+  if (k > OZEC_MAX_K || rows > OZEC_MAX_ROWS)
+    return fail(OZEC_EUNSUPPORTED, "schema exceeds GPU kernel limits (k <= " + std::to_string(OZEC_MAX_K) +
+                                       ", rows <= " + std::to_string(OZEC_MAX_ROWS) + ")");
+  return OZEC_OK;
+}
+
+// parity rows of an encoder as coefficient rows (XOR: a single all-ones row)
+void encode_rows(const ozec_coder *enc, std::vector<uint8_t> &rows) {
+  if (enc->codec == OZEC_CODEC_XOR) rows.assign(static_cast<size_t>(enc->k), 1);
+  else rows = enc->parity_rows;
+}
+
+int out_rows(const ozec_coder *enc) { return enc->codec == OZEC_CODEC_XOR ? 1 : enc->p; }
+
+}  // namespace
+
+extern "C" {
+
+const char *ozec_last_error(void) { return g_error.c_str(); }
+
+int ozec_version(void) { return 1; }
+
+int ozec_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ozec_set_device(int device) {
+  OZEC_HIP(hipSetDevice(device));
+  return OZEC_OK;
+}
+
+int ozec_synchronize(void) {
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  OZEC_HIP(hipStreamSynchronize(ctx->stream));
+  return OZEC_OK;
+}
+
+static int coder_create(int codec, int k, int p, bool decoder, ozec_coder **out) {
+  if (!out) return fail(OZEC_EINVAL, "null output handle");
+  *out = nullptr;
+  if (codec != OZEC_CODEC_RS && codec != OZEC_CODEC_XOR) return fail(OZEC_EINVAL, "unknown codec");
+  if (k <= 0 || p <= 0)
+    return fail(OZEC_EINVAL, "Data and parity part in EC replication config supposed to be positive numbers");
+  // RSRawEncoder.java:42-45 / RSRawDecoder.java:61-64
+  if (codec == OZEC_CODEC_RS && k + p >= 256) return fail(OZEC_EINVAL, "Invalid numDataUnits and numParityUnits");
+  if (int rc = check_limits(k, codec == OZEC_CODEC_XOR ? 1 : p)) return rc;
+  // a GPU coder must not be constructible without a device, so CodecUtil falls back to rs_java
+  // (CodecUtil.createRawEncoderWithFallback, CodecUtil.java:62-78)
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  auto *c = new (std::nothrow) ozec_coder();
+  if (!c) return fail(OZEC_ENOMEM, "out of memory");
+  c->codec = codec;
+  c->k = k;
+  c->p = p;
+  c->decoder = decoder;
+  if (codec == OZEC_CODEC_RS) {
+    std::vector<uint8_t> m = ozec::cauchy_matrix(k, p);
+    c->parity_rows.assign(m.begin() + static_cast<size_t>(k) * k, m.end());
+  }
+  *out = c;
+  return OZEC_OK;
+}
+
+int ozec_encoder_create(int codec, int k, int p, ozec_coder **out) { return coder_create(codec, k, p, false, out); }
+int ozec_decoder_create(int codec, int k, int p, ozec_coder **out) { return coder_create(codec, k, p, true, out); }
+
+int ozec_coder_release(ozec_coder *c) {
+  if (!c) return fail(OZEC_EINVAL, "null coder");
+  c->closed.store(true);
+  return OZEC_OK;
+}
+
+void ozec_coder_free(ozec_coder *c) { delete c; }
+
+int ozec_coder_info(const ozec_coder *c, int *codec, int *k, int *p, int *is_decoder) {
+  if (!c) return fail(OZEC_EINVAL, "null coder");
+  if (codec) *codec = c->codec;
+  if (k) *k = c->k;
+  if (p) *p = c->p;
+  if (is_decoder) *is_decoder = c->decoder;
+  return OZEC_OK;
+}
+
+// ---- encode ------------------------------------------------------------------------------------
+
+int ozec_encode(ozec_coder *enc, const uint8_t *const *inputs, uint8_t *const *outputs, size_t len) {
+  if (int rc = check_open(enc, "encode")) return rc;
+  if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
+  if (!inputs || !outputs) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  const int k = enc->k, rows = out_rows(enc);
+  for (int j = 0; j < k; ++j)
+    if (!inputs[j]) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  for (int r = 0; r < rows; ++r)
+    if (!outputs[r]) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  if (len == 0) return OZEC_OK;  // RawErasureEncoder.java:73-75
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  const size_t lp = round_up(len, kStageAlign);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (int rc = ctx->reserve(lp * (k + rows))) return rc;
+  for (int j = 0; j < k; ++j) std::memcpy(ctx->pinned + j * lp, inputs[j], len);
+  OZEC_HIP(hipMemcpyAsync(ctx->dbuf, ctx->pinned, lp * k, hipMemcpyHostToDevice, ctx->stream));
+  CodeArgs a{};
+  a.in = ctx->dbuf;
+  a.out = ctx->dbuf + lp * k;
+  a.nstripes = 1;
+  a.len = static_cast<int64_t>(len);
+  std::vector<uint8_t> coef;
+  encode_rows(enc, coef);
+  fill_coef(a, rows, k, coef.data());
+  for (int j = 0; j < k; ++j) a.in_off[j] = static_cast<int64_t>(j * lp);
+  for (int r = 0; r < rows; ++r) a.out_off[r] = static_cast<int64_t>(r * lp);
+  OZEC_HIP(ozec::launch_code(a, ctx->stream));
+  OZEC_HIP(hipMemcpyAsync(ctx->pinned + lp * k, a.out, lp * rows, hipMemcpyDeviceToHost, ctx->stream));
+  OZEC_HIP(hipStreamSynchronize(ctx->stream));
+  for (int r = 0; r < rows; ++r) std::memcpy(outputs[r], ctx->pinned + lp * (k + r), len);
+  // XOR with p > 1: the reference zero-fills every output and writes only outputs[0] (XORRawEncoder.java:67-85)
+  for (int r = rows; r < enc->p; ++r)
+    if (outputs[r]) std::memset(outputs[r], 0, len);
+  return OZEC_OK;
+}
+
+int ozec_encode_device(ozec_coder *enc, const uint8_t *const *d_inputs, uint8_t *const *d_outputs, size_t len,
+                       void *stream) {
+  if (int rc = check_open(enc, "encode")) return rc;
+  if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
+  if (!d_inputs || !d_outputs) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  const int k = enc->k, rows = out_rows(enc);
+  for (int j = 0; j < k; ++j)
+    if (!d_inputs[j]) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  for (int r = 0; r < rows; ++r)
+    if (!d_outputs[r]) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  if (len == 0) return OZEC_OK;
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  CodeArgs a{};
+  a.nstripes = 1;
+  a.len = static_cast<int64_t>(len);
+  std::vector<uint8_t> coef;
+  encode_rows(enc, coef);
+  fill_coef(a, rows, k, coef.data());
+  for (int j = 0; j < k; ++j) a.in_off[j] = reinterpret_cast<intptr_t>(d_inputs[j]);
+  for (int r = 0; r < rows; ++r) a.out_off[r] = reinterpret_cast<intptr_t>(d_outputs[r]);
+  hipStream_t st = pick_stream(ctx, stream);
+  OZEC_HIP(ozec::launch_code(a, st));
+  for (int r = rows; r < enc->p; ++r)
+    if (d_outputs[r]) OZEC_HIP(hipMemsetAsync(d_outputs[r], 0, len, st));
+  return OZEC_OK;
+}
+
+int ozec_encode_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
+                      uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes,
+                      size_t len, void *stream) {
+  if (int rc = check_open(enc, "encode")) return rc;
+  if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
+  if (len == 0 || num_stripes == 0) return OZEC_OK;
+  if (!d_in || !d_out) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  const int k = enc->k, rows = out_rows(enc);
+  CodeArgs a{};
+  a.in = d_in;
+  a.out = d_out;
+  a.in_stripe_stride = in_stripe_stride;
+  a.out_stripe_stride = out_stripe_stride;
+  a.nstripes = static_cast<int64_t>(num_stripes);
+  a.len = static_cast<int64_t>(len);
+  std::vector<uint8_t> coef;
+  encode_rows(enc, coef);
+  fill_coef(a, rows, k, coef.data());
+  for (int j = 0; j < k; ++j) a.in_off[j] = j * in_unit_stride;
+  for (int r = 0; r < rows; ++r) a.out_off[r] = r * out_unit_stride;
+  hipStream_t st = pick_stream(ctx, stream);
+  OZEC_HIP(ozec::launch_code(a, st));
+  for (int r = rows; r < enc->p; ++r)
+    OZEC_HIP(hipMemset2DAsync(d_out + r * out_unit_stride, out_stripe_stride, 0, len, num_stripes, st));
+  return OZEC_OK;
+}
+
+// ---- decode ------------------------------------------------------------------------------------
+
+int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased, int n_erased,
+                uint8_t *const *outputs, size_t len) {
+  if (int rc = check_open(dec, "decode")) return rc;
+  if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
+  if (!inputs) return fail(OZEC_EINVAL, "Invalid inputs length");
+  const int n_all = dec->k + dec->p;
+  bool present[256];
+  bool any = false;
+  for (int u = 0; u < n_all; ++u) any |= (present[u] = inputs[u] != nullptr);
+  if (!any) return fail(OZEC_EINVAL, "Invalid inputs are found, all being null");
+  for (int i = 0; i < n_erased; ++i)
+    if (!outputs || !outputs[i]) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  std::vector<int> units;
+  std::vector<uint8_t> rows;
+  if (int rc = plan_decode(dec, present, erased, n_erased, units, rows)) return rc;
+  if (len == 0 || n_erased == 0) return OZEC_OK;
+  const int nin = static_cast<int>(units.size());
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  const size_t lp = round_up(len, kStageAlign);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (int rc = ctx->reserve(lp * (nin + n_erased))) return rc;
+  for (int j = 0; j < nin; ++j) std::memcpy(ctx->pinned + j * lp, inputs[units[j]], len);
+  OZEC_HIP(hipMemcpyAsync(ctx->dbuf, ctx->pinned, lp * nin, hipMemcpyHostToDevice, ctx->stream));
+  CodeArgs a{};
+  a.in = ctx->dbuf;
+  a.out = ctx->dbuf + lp * nin;
+  a.nstripes = 1;
+  a.len = static_cast<int64_t>(len);
+  if (dec->codec == OZEC_CODEC_XOR) fill_coef(a, 1, nin, rows.data());
+  else fill_coef(a, n_erased, nin, rows.data());
+  if (int rc = check_limits(a.k, a.rows)) return rc;
+  for (int j = 0; j < nin; ++j) a.in_off[j] = static_cast<int64_t>(j * lp);
+  for (int r = 0; r < a.rows; ++r) a.out_off[r] = static_cast<int64_t>(r * lp);
+  OZEC_HIP(ozec::launch_code(a, ctx->stream));
+  OZEC_HIP(hipMemcpyAsync(ctx->pinned + lp * nin, a.out, lp * a.rows, hipMemcpyDeviceToHost, ctx->stream));
+  OZEC_HIP(hipStreamSynchronize(ctx->stream));
+  for (int r = 0; r < n_erased; ++r) {
+    // XOR decode: only erasedIndexes[0] is recovered, further outputs stay zero-filled (XORRawDecoder.java:45-61)
+    if (r < a.rows) std::memcpy(outputs[r], ctx->pinned + lp * (nin + r), len);
+    else std::memset(outputs[r], 0, len);
+  }
+  return OZEC_OK;
+}
+
+int ozec_decode_device(ozec_coder *dec, const uint8_t *const *d_inputs, const int *erased, int n_erased,
+                       uint8_t *const *d_outputs, size_t len, void *stream) {
+  if (int rc = check_open(dec, "decode")) return rc;
+  if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
+  if (!d_inputs) return fail(OZEC_EINVAL, "Invalid inputs length");
+  const int n_all = dec->k + dec->p;
+  bool present[256];
+  bool any = false;
+  for (int u = 0; u < n_all; ++u) any |= (present[u] = d_inputs[u] != nullptr);
+  if (!any) return fail(OZEC_EINVAL, "Invalid inputs are found, all being null");
+  for (int i = 0; i < n_erased; ++i)
+    if (!d_outputs || !d_outputs[i]) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  std::vector<int> units;
+  std::vector<uint8_t> rows;
+  if (int rc = plan_decode(dec, present, erased, n_erased, units, rows)) return rc;
+  if (len == 0 || n_erased == 0) return OZEC_OK;
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  CodeArgs a{};
+  a.nstripes = 1;
+  a.len = static_cast<int64_t>(len);
+  const int nin = static_cast<int>(units.size());
+  if (dec->codec == OZEC_CODEC_XOR) fill_coef(a, 1, nin, rows.data());
+  else fill_coef(a, n_erased, nin, rows.data());
+  if (int rc = check_limits(a.k, a.rows)) return rc;
+  for (int j = 0; j < nin; ++j) a.in_off[j] = reinterpret_cast<intptr_t>(d_inputs[units[j]]);
+  for (int r = 0; r < a.rows; ++r) a.out_off[r] = reinterpret_cast<intptr_t>(d_outputs[r]);
+  OZEC_HIP(ozec::launch_code(a, st));
+  for (int r = a.rows; r < n_erased; ++r) OZEC_HIP(hipMemsetAsync(d_outputs[r], 0, len, st));
+  return OZEC_OK;
+}
+
+int ozec_decode_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
+                      const int *present_units, int num_present, const int *erased, int n_erased, uint8_t *d_out,
+                      int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes, size_t len,
+                      void *stream) {
+  if (int rc = check_open(dec, "decode")) return rc;
+  if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
+  const int n_all = dec->k + dec->p;
+  bool present[256] = {false};
+  for (int i = 0; i < num_present; ++i) {
+    if (present_units[i] < 0 || present_units[i] >= n_all) return fail(OZEC_EINVAL, "present unit out of range");
+    present[present_units[i]] = true;
+  }
+  std::vector<int> units;
+  std::vector<uint8_t> rows;
+  if (int rc = plan_decode(dec, present, erased, n_erased, units, rows)) return rc;
+  if (len == 0 || num_stripes == 0 || n_erased == 0) return OZEC_OK;
+  if (!d_in || !d_out) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  CodeArgs a{};
+  a.in = d_in;
+  a.out = d_out;
+  a.in_stripe_stride = in_stripe_stride;
+  a.out_stripe_stride = out_stripe_stride;
+  a.nstripes = static_cast<int64_t>(num_stripes);
+  a.len = static_cast<int64_t>(len);
+  const int nin = static_cast<int>(units.size());
+  if (dec->codec == OZEC_CODEC_XOR) fill_coef(a, 1, nin, rows.data());
+  else fill_coef(a, n_erased, nin, rows.data());
+  if (int rc = check_limits(a.k, a.rows)) return rc;
+  for (int j = 0; j < nin; ++j) a.in_off[j] = units[j] * in_unit_stride;
+  for (int r = 0; r < a.rows; ++r) a.out_off[r] = r * out_unit_stride;
+  OZEC_HIP(ozec::launch_code(a, st));
+  for (int r = a.rows; r < n_erased; ++r)
+    OZEC_HIP(hipMemset2DAsync(d_out + r * out_unit_stride, out_stripe_stride, 0, len, num_stripes, st));
+  return OZEC_OK;
+}
+
+// ---- checksums -----------------------------------------------------------------------------------
+
+static int make_crc_args(DevCtx *ctx, int checksum_type, const uint8_t *d_base, int64_t cell_stride, size_t ncells,
+                         size_t len, size_t bpc, uint32_t *d_out, int64_t out_cell_stride, int big_endian, int raw,
+                         CrcArgs *a) {
+  CrcType t;
+  if (int rc = crc_type_of(checksum_type, &t)) return rc;
+  if (bpc == 0) return fail(OZEC_EINVAL, "bytesPerChecksum must be positive");
+  const CrcMath &cm = CrcMath::get(t);
+  *a = CrcArgs{};
+  a->base = d_base;
+  a->cell_stride = cell_stride;
+  a->ncells = static_cast<int64_t>(ncells);
+  a->len = static_cast<int64_t>(len);
+  a->bpc = static_cast<int64_t>(bpc);
+  a->nwin = static_cast<int64_t>((len + bpc - 1) / bpc);
+  a->out = d_out;
+  a->out_cell_stride = out_cell_stride;
+  a->tables = ctx->crc_tables[static_cast<int>(t)];
+  a->init_full = cm.shift(0xffffffffu, bpc);
+  a->init_last = cm.shift(0xffffffffu, len - (a->nwin ? (a->nwin - 1) * bpc : 0));
+  a->big_endian = big_endian;
+  a->raw = raw;
+  return OZEC_OK;
+}
+
+int ozec_checksum_windows_batch(int checksum_type, const uint8_t *d_base, int64_t cell_stride, size_t num_cells,
+                                size_t len, size_t bpc, uint32_t *d_out, int big_endian, void *stream) {
+  if (len == 0 || num_cells == 0) return OZEC_OK;
+  if (!d_base || !d_out) return fail(OZEC_EINVAL, "null buffer");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  CrcArgs a;
+  const int64_t nwin = static_cast<int64_t>((len + (bpc ? bpc : 1) - 1) / (bpc ? bpc : 1));
+  if (int rc = make_crc_args(ctx, checksum_type, d_base, cell_stride, num_cells, len, bpc, d_out, nwin, big_endian, 0,
+                             &a))
+    return rc;
+  OZEC_HIP(ozec::launch_crc_windows(a, pick_stream(ctx, stream)));
+  return OZEC_OK;
+}
+
+int ozec_checksum_windows_device(int checksum_type, const uint8_t *d_data, size_t len, size_t bpc, uint32_t *d_out,
+                                 int big_endian, void *stream) {
+  return ozec_checksum_windows_batch(checksum_type, d_data, 0, 1, len, bpc, d_out, big_endian, stream);
+}
+
+// host buffers: stage -> GPU -> copy back; `raw` returns the raw registers (streaming update)
+static int checksum_host(int checksum_type, const uint8_t *data, size_t len, size_t bpc, uint32_t *out, int big_endian,
+                         int raw) {
+  CrcType t;
+  if (int rc = crc_type_of(checksum_type, &t)) return rc;
+  if (bpc == 0) return fail(OZEC_EINVAL, "bytesPerChecksum must be positive");
+  if (len == 0) return OZEC_OK;
+  if (!data || !out) return fail(OZEC_EINVAL, "null buffer");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  const size_t nwin = (len + bpc - 1) / bpc;
+  const size_t lp = round_up(len, kStageAlign);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (int rc = ctx->reserve(lp + nwin * sizeof(uint32_t))) return rc;
+  std::memcpy(ctx->pinned, data, len);
+  OZEC_HIP(hipMemcpyAsync(ctx->dbuf, ctx->pinned, len, hipMemcpyHostToDevice, ctx->stream));
+  CrcArgs a;
+  uint32_t *d_out = reinterpret_cast<uint32_t *>(ctx->dbuf + lp);
+  if (int rc = make_crc_args(ctx, checksum_type, ctx->dbuf, 0, 1, len, bpc, d_out, static_cast<int64_t>(nwin),
+                             big_endian, raw, &a))
+    return rc;
+  OZEC_HIP(ozec::launch_crc_windows(a, ctx->stream));
+  OZEC_HIP(hipMemcpyAsync(ctx->pinned + lp, d_out, nwin * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  OZEC_HIP(hipStreamSynchronize(ctx->stream));
+  std::memcpy(out, ctx->pinned + lp, nwin * sizeof(uint32_t));
+  return OZEC_OK;
+}
+
+int ozec_checksum_windows(int checksum_type, const uint8_t *data, size_t len, size_t bpc, uint32_t *out,
+                          int big_endian) {
+  return checksum_host(checksum_type, data, len, bpc, out, big_endian, 0);
+}
+
+int ozec_checksum_verify(int checksum_type, const uint8_t *data, size_t len, size_t bpc, const uint32_t *expected,
+                         size_t num_expected, size_t start_index, int64_t *mismatch_index) {
+  if (mismatch_index) *mismatch_index = -1;
+  if (checksum_type == OZEC_CHECKSUM_NONE) return OZEC_OK;  // Checksum.java:250-253
+  if (num_expected == 0) return fail(OZEC_EMISMATCH, "Original checksumData has no checksums");
+  if (bpc == 0) return fail(OZEC_EINVAL, "bytesPerChecksum must be positive");
+  const size_t nwin = (len + bpc - 1) / bpc;
+  if (nwin == 0) return fail(OZEC_EMISMATCH, "Computed checksumData has no checksums");
+  std::vector<uint32_t> got(nwin);
+  if (int rc = checksum_host(checksum_type, data, len, bpc, got.data(), 0, 0)) return rc;
+  for (size_t i = 0; i < nwin; ++i) {
+    if (start_index + i >= num_expected)
+      return fail(OZEC_EMISMATCH, "Computed checksum has " + std::to_string(nwin) +
+                                      " number of checksums. Original checksum has " +
+                                      std::to_string(num_expected - std::min(num_expected, start_index)) +
+                                      " number of checksums starting from index " + std::to_string(start_index));
+    if (got[i] != expected[start_index + i]) {
+      if (mismatch_index) *mismatch_index = static_cast<int64_t>(i);
+      return fail(OZEC_EMISMATCH, "Checksum mismatch at index " + std::to_string(i));
+    }
+  }
+  return OZEC_OK;
+}
+
+uint32_t ozec_crc_reset(int) { return 0xffffffffu; }
+
+int ozec_crc_update(int checksum_type, uint32_t *state, const uint8_t *data, size_t len) {
+  CrcType t;
+  if (int rc = crc_type_of(checksum_type, &t)) return rc;
+  if (!state) return fail(OZEC_EINVAL, "null state");
+  if (len == 0) return OZEC_OK;
+  uint32_t raw = 0;
+  if (int rc = checksum_host(checksum_type, data, len, len, &raw, 0, 1)) return rc;
+  // register after (state, data) = shift(state, len) ^ f(data)
+  *state = CrcMath::get(t).shift(*state, len) ^ raw;
+  return OZEC_OK;
+}
+
+uint32_t ozec_crc_value(int, uint32_t state) { return ~state; }
+
+// ---- fused encode + CRC --------------------------------------------------------------------------
+
+int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
+                          uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes,
+                          size_t len, int checksum_type, size_t bpc, uint32_t *d_crcs, int big_endian, void *stream) {
+  if (int rc = check_open(enc, "encode")) return rc;
+  if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
+  if (len == 0 || num_stripes == 0) return OZEC_OK;
+  if (!d_in || !d_out || !d_crcs) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  const int k = enc->k, rows = out_rows(enc), units = k + rows;
+  ozec::EncCrcArgs e{};
+  CodeArgs &a = e.code;
+  a.in = d_in;
+  a.out = d_out;
+  a.in_stripe_stride = in_stripe_stride;
+  a.out_stripe_stride = out_stripe_stride;
+  a.nstripes = static_cast<int64_t>(num_stripes);
+  a.len = static_cast<int64_t>(len);
+  std::vector<uint8_t> coef;
+  encode_rows(enc, coef);
+  fill_coef(a, rows, k, coef.data());
+  for (int j = 0; j < k; ++j) a.in_off[j] = j * in_unit_stride;
+  for (int r = 0; r < rows; ++r) a.out_off[r] = r * out_unit_stride;
+  const int64_t nwin = static_cast<int64_t>((len + (bpc ? bpc : 1) - 1) / (bpc ? bpc : 1));
+  if (int rc = make_crc_args(ctx, checksum_type, nullptr, 0, num_stripes, len, bpc, d_crcs, nwin, big_endian, 0,
+                             &e.crc))
+    return rc;
+  if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
+    OZEC_HIP(ozec::launch_encode_crc(e, st));
+    return OZEC_OK;
+  }
+  // unfused: encode, then one CRC pass per unit (crcs[s][u][w] layout kept)
+  OZEC_HIP(ozec::launch_code(a, st));
+  for (int u = 0; u < units; ++u) {
+    CrcArgs c = e.crc;
+    c.base = u < k ? d_in + u * in_unit_stride : d_out + (u - k) * out_unit_stride;
+    c.cell_stride = u < k ? in_stripe_stride : out_stripe_stride;
+    c.out = d_crcs + u * nwin;
+    c.out_cell_stride = units * nwin;
+    OZEC_HIP(ozec::launch_crc_windows(c, st));
+  }
+  return OZEC_OK;
+}
+
+// ---- host-side math ----------------------------------------------------------------------------
+
+int ozec_rs_encode_matrix(int k, int p, uint8_t *matrix) {
+  if (!matrix || k <= 0 || p <= 0 || k + p >= 256) return fail(OZEC_EINVAL, "Invalid numDataUnits and numParityUnits");
+  std::vector<uint8_t> m = ozec::cauchy_matrix(k, p);
+  std::memcpy(matrix, m.data(), m.size());
+  return OZEC_OK;
+}
+
+int ozec_rs_decode_matrix(int k, int p, const int *valid, const int *erased, int n_erased, uint8_t *out) {
+  if (!valid || (n_erased && (!erased || !out)) || k <= 0 || p <= 0 || k + p >= 256)
+    return fail(OZEC_EINVAL, "invalid arguments");
+  for (int i = 0; i < k; ++i)
+    if (valid[i] < 0 || valid[i] >= k + p) return fail(OZEC_EINVAL, "valid index out of range");
+  for (int i = 0; i < n_erased; ++i)
+    if (erased[i] < 0 || erased[i] >= k + p) return fail(OZEC_EINVAL, "erased index out of range");
+  std::vector<uint8_t> rows;
+  if (!ozec::decode_matrix(k, p, valid, erased, n_erased, rows)) return fail(OZEC_ENOTINVERTIBLE, "Not invertible");
+  std::memcpy(out, rows.data(), rows.size());
+  return OZEC_OK;
+}
+
+int ozec_gf_invert_matrix(uint8_t *in, uint8_t *out, int n) {
+  if (!in || !out || n <= 0) return fail(OZEC_EINVAL, "invalid arguments");
+  if (!ozec::invert_matrix(in, out, n)) return fail(OZEC_ENOTINVERTIBLE, "Not invertible");
+  return OZEC_OK;
+}
+
+uint8_t ozec_gf_mul(uint8_t a, uint8_t b) { return ozec::GF256::get().mul(a, b); }
+
+int ozec_parse_replication(const char *s, int *codec, int *k, int *p, int *chunk) {
+  // ECReplicationConfig(String), ECReplicationConfig.java:96-130
+  static const std::regex re("([a-zA-Z]+)-(\\d+)-(\\d+)-(\\d+)([kK])?");
+  std::cmatch m;
+  if (!s || !std::regex_match(s, m, re))
+    return fail(OZEC_EINVAL, std::string("EC replication config should be defined in the form rs-3-2-1024k, "
+                                         "rs-6-3-1024k; or rs-10-4-1024k. Provided configuration was: ") +
+                                 (s ? s : "null"));
+  std::string name = m[1].str();
+  for (auto &ch : name) ch = static_cast<char>(std::tolower(ch));
+  int c;
+  if (name == "rs") c = OZEC_CODEC_RS;
+  else if (name == "xor") c = OZEC_CODEC_XOR;
+  else return fail(OZEC_EINVAL, "The codec " + m[1].str() + " is invalid. It must be one of rs,xor.");
+  long long d = 0, q = 0, cs = 0;
+  try {
+    d = std::stoll(m[2].str());
+    q = std::stoll(m[3].str());
+    cs = std::stoll(m[4].str());
+  } catch (...) {
+    return fail(OZEC_EINVAL, "NumberFormatException");
+  }
+  if (d > INT32_MAX || q > INT32_MAX || cs > INT32_MAX) return fail(OZEC_EINVAL, "NumberFormatException");
+  if (d <= 0 || q <= 0)
+    return fail(OZEC_EINVAL, "Data and parity part in EC replication config supposed to be positive numbers");
+  if (cs <= 0) return fail(OZEC_EINVAL, "The ecChunkSize (" + std::to_string(cs) + ") be greater than zero");
+  if (m[5].matched) cs *= 1024;  // Java int arithmetic wraps here; values that large are rejected upstream
+  if (codec) *codec = c;
+  if (k) *k = static_cast<int>(d);
+  if (p) *p = static_cast<int>(q);
+  if (chunk) *chunk = static_cast<int>(static_cast<int32_t>(cs));
+  return OZEC_OK;
+}
+
+uint32_t ozec_crc_combine(int checksum_type, uint32_t a, uint32_t b, uint64_t len_b) {
+  CrcType t;
+  if (crc_type_of(checksum_type, &t)) return 0;
+  return CrcMath::get(t).combine(a, b, len_b);
+}
+
+// ---- harness utilities ------------------------------------------------------------------------------
+
+int ozec_fill_splitmix64_cells(uint8_t *d_base, int64_t cell_stride, size_t ncells, size_t n, uint64_t seed,
+                               uint64_t first_stream, void *stream) {
+  if (n == 0 || ncells == 0) return OZEC_OK;
+  if (!d_base) return fail(OZEC_EINVAL, "null buffer");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  OZEC_HIP(ozec::launch_fill_splitmix64(d_base, cell_stride, static_cast<int64_t>(ncells), static_cast<int64_t>(n),
+                                        seed, first_stream, pick_stream(ctx, stream)));
+  return OZEC_OK;
+}
+
+int ozec_fill_splitmix64(uint8_t *d_dst, size_t n, uint64_t seed, uint64_t stream_id, void *stream) {
+  return ozec_fill_splitmix64_cells(d_dst, 0, 1, n, seed, stream_id, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,32 @@
+// Host-side CRC math: table construction for the GPU kernels and GF(2) shift/combine operators.
+// Reflected CRC-32 (poly 0xEDB88320) and CRC-32C (poly 0x82F63B78), init/xorout 0xFFFFFFFF -- the
+// arithmetic of ChecksumByteBuffer.CrcIntTable (CM/ChecksumByteBuffer.java:51-121) and the JDK
+// java.util.zip.CRC32 / CRC32C that ChecksumByteBufferFactory hands out (ChecksumByteBufferFactory.java:74-89).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace ozec {
+
+enum class CrcType { kCrc32 = 0, kCrc32c = 1 };
+
+class CrcMath {
+ public:
+  static const CrcMath &get(CrcType t);
+  // raw register after appending n zero bytes (multiplication by x^(8n) mod P)
+  uint32_t shift(uint32_t reg, uint64_t n) const;
+  // crc(A||B) from the finished values crc(A), crc(B) and |B| (zlib-style combine)
+  uint32_t combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) const { return shift(crc_a, len_b) ^ crc_b; }
+  // the device table blob (kernels.hpp CrcTables layout)
+  const std::vector<uint32_t> &device_tables() const { return blob_; }
+  uint32_t byte_table(int v) const { return t0_[v]; }
+
+ private:
+  explicit CrcMath(uint32_t poly);
+  uint32_t t0_[256];
+  // op_[i] = operator for 2^i zero BYTES as a 32x32 GF(2) matrix (column c = image of bit c)
+  uint32_t op_[64][32];
+  std::vector<uint32_t> blob_;
+};
+
+}  // namespace ozec

@@ -1,0 +1,710 @@
+// gfx950 (CDNA4) kernels for the Ozone EC + chunk-checksum hot path.
+//
+// GF(2^8) coding (RSUtil.encodeData, EC/rawcoder/util/RSUtil.java:87-133, and the XOR coders):
+//   Each coefficient c becomes three byte-permute tables held in registers:
+//     T_lo  = c*{0..7}              (2 dwords)   indexed by bits 0-2 of a data byte
+//     T_mid = c*{0,8,..,56}         (2 dwords)   indexed by bits 3-5
+//     T_top = c*{0,64,128,192}      (1 dword)    indexed by bits 6-7
+//   so c*x = T_lo[x&7] ^ T_mid[(x>>3)&7] ^ T_top[x>>6] (GF multiplication is GF(2)-linear in x).  One
+//   v_perm_b32 looks up 4 bytes at once, so a 4-byte word costs 3 perms + 2 xors per coefficient, and the
+//   per-input selector extraction (5 ops) is shared by every output row.  This is the CDNA4 analogue of the
+//   split-nibble pshufb tables GF256.gfVectMulInit builds (GF256.java:259-330): the lookup happens in the
+//   VALU permute unit instead of LDS, so it costs no LDS bandwidth and has no bank conflicts.
+//   Loads/stores are 16 B per lane (global_load_dwordx4), fully coalesced: lane i of a 256-thread block
+//   owns bytes [16i, 16i+16) of a 4 KiB chunk of every unit of one stripe.
+//
+// CRC32 / CRC32C per bytesPerChecksum window (ChecksumByteBuffer.CrcIntTable, CM/ChecksumByteBuffer.java:51-121):
+//   One wave per window.  Lane l owns 16-B blocks l, l+64, l+128, ... of the window (coalesced 1 KiB per
+//   wave-instruction) and folds them with Horner's rule  S = S*x^(8*1024) ^ f16(block)  where f16 is the raw
+//   CRC of one block (16 slice tables in LDS) and the 1 KiB shift is 4 table lookups.  A 6-level shuffle
+//   tree then merges the 64 lane registers (shift by 16*2^m bytes at level m).  Windows whose length is
+//   not a multiple of 1 KiB are front-padded with virtual zero blocks (leading zeros do not change a raw
+//   CRC that starts from 0); the init value is added back as a precomputed shift(0xFFFFFFFF, N).
+#include "kernels.hpp"
+
+namespace ozec {
+namespace {
+
+constexpr int kBlock = 256;
+#ifndef OZEC_GF_WAVES
+#define OZEC_GF_WAVES 4  // >= 4 waves per SIMD: <= 128 VGPRs for the coding kernels
+#endif
+constexpr int kMaxGrid = 256 * 8;  // 8 blocks of 256 threads per CU, grid-stride beyond
+
+// ------------------------------------------------------------------------------------------------
+// GF(2^8) helpers
+
+__device__ __forceinline__ uint32_t gf_mul_byte(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r ^= (b & 1u) ? a : 0u;
+    b >>= 1;
+    a = (a << 1) ^ ((a & 0x80u) ? 0x11du : 0u);
+  }
+  return r & 0xffu;
+}
+
+struct PermTab {
+  uint32_t lo0, lo1, mid0, mid1, top;
+};
+
+__device__ __forceinline__ uint32_t pack4(uint32_t c, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
+  return gf_mul_byte(c, m0) | (gf_mul_byte(c, m1) << 8) | (gf_mul_byte(c, m2) << 16) | (gf_mul_byte(c, m3) << 24);
+}
+
+__device__ __forceinline__ PermTab make_tab(uint32_t c) {
+  PermTab t;
+  t.lo0 = pack4(c, 0, 1, 2, 3);
+  t.lo1 = pack4(c, 4, 5, 6, 7);
+  t.mid0 = pack4(c, 0, 8, 16, 24);
+  t.mid1 = pack4(c, 32, 40, 48, 56);
+  t.top = pack4(c, 0, 64, 128, 192);
+  return t;
+}
+
+struct Sel {
+  uint32_t s0, s1, s2;
+};
+
+__device__ __forceinline__ Sel make_sel(uint32_t w) {
+  Sel s;
+  s.s0 = w & 0x07070707u;
+  s.s1 = (w >> 3) & 0x07070707u;
+  s.s2 = (w >> 6) & 0x03030303u;
+  return s;
+}
+
+// c * w for the 4 bytes of w. v_perm_b32(S0, S1, sel): selector byte 0-3 picks a byte of S1, 4-7 of S0.
+__device__ __forceinline__ uint32_t gf_mul4(const PermTab &t, const Sel &s) {
+  return __builtin_amdgcn_perm(t.lo1, t.lo0, s.s0) ^ __builtin_amdgcn_perm(t.mid1, t.mid0, s.s1) ^
+         __builtin_amdgcn_perm(t.top, t.top, s.s2);
+}
+
+// ---- register-resident tables: lo1/mid1/top are wave-uniform and live in SGPRs, lo0/mid0 in VGPRs, so
+// each v_perm_b32 reads exactly one SGPR (the gfx9 constant-bus limit) and a coefficient costs 2 VGPRs.
+__device__ __forceinline__ uint32_t perm_sv(uint32_t hi_s, uint32_t lo_v, uint32_t sel) {
+  uint32_t d;
+  asm("v_perm_b32 %0, %1, %2, %3" : "=v"(d) : "s"(hi_s), "v"(lo_v), "v"(sel));
+  return d;
+}
+__device__ __forceinline__ uint32_t perm_top_s(uint32_t top_s, uint32_t sel) {
+  uint32_t d;  // selectors 0..3 only read S1 (= the SGPR table); S0 is a don't-care VGPR
+  asm("v_perm_b32 %0, %1, %2, %1" : "=v"(d) : "v"(sel), "s"(top_s));
+  return d;
+}
+__device__ __forceinline__ uint32_t perm_vv(uint32_t hi, uint32_t lo, uint32_t sel) {
+  uint32_t d;
+  asm("v_perm_b32 %0, %1, %2, %3" : "=v"(d) : "v"(hi), "v"(lo), "v"(sel));
+  return d;
+}
+// gfx950 3-input bitwise op; truth table 0x96 = a ^ b ^ c
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+struct RegTab {
+  uint32_t lo0, mid0;      // VGPR
+  uint32_t lo1, mid1, top; // SGPR (wave-uniform)
+};
+
+__device__ __forceinline__ uint32_t gf_mul4_reg(const RegTab &t, const Sel &s) {
+  return xor3(perm_sv(t.lo1, t.lo0, s.s0), perm_sv(t.mid1, t.mid0, s.s1), perm_top_s(t.top, s.s2));
+}
+__device__ __forceinline__ uint32_t gf_mul4_lds(const PermTab &t, const Sel &s) {
+  return xor3(perm_vv(t.lo1, t.lo0, s.s0), perm_vv(t.mid1, t.mid0, s.s1), perm_vv(t.top, t.top, s.s2));
+}
+
+__device__ __forceinline__ void build_tabs(PermTab *s_tab, const CodeArgs &a, int rows, int k) {
+  for (int t = threadIdx.x; t < rows * k; t += blockDim.x) s_tab[t] = make_tab(a.coef[t]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Coding kernels
+
+// Host-built permute tables for the templated kernels, passed by value in the kernarg segment so they are
+// s_load'ed straight into SGPRs (no LDS round trip, no readfirstlane).
+template <int N>
+struct TabArgs {
+  uint32_t w[N][5];  // per coefficient: lo0, lo1, mid0, mid1, top
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
+  // raw buffer (stride 0), full 4 GiB range; bounds are checked explicitly by the kernels
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0xffffffff, 0x00020000);
+}
+
+// Fully unrolled K inputs x R outputs.  Addressing: one buffer descriptor per stripe side (SGPRs), the unit
+// offset in soffset (SGPR) and the lane offset v*16 in a single VGPR, so a lane spends 1 VGPR on addresses.
+// SREG: lo1/mid1/top are SGPR operands straight from the kernarg segment, lo0/mid0 live in VGPRs (loaded once
+// from LDS as single dwords); K*R <= 18.  Otherwise all five dwords are re-read from LDS for every unit
+// (uniform-address broadcasts), which keeps large schemas (rs-10-4 decode) inside 128 VGPRs.
+template <int K, int R, bool SREG>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_WAVES, 8))) void gf_code_vec(
+    const CodeArgs a, const TabArgs<K * R> tabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_w[5][K * R];
+  for (int t = threadIdx.x; t < K * R; t += blockDim.x)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) s_w[q][t] = tabs.w[t][q];
+  __syncthreads();
+  uint32_t vlo0[SREG ? K * R : 1], vmid0[SREG ? K * R : 1];
+  if constexpr (SREG) {
+#pragma unroll
+    for (int t = 0; t < K * R; ++t) {
+      vlo0[t] = s_w[0][t];
+      vmid0[t] = s_w[2][t];
+    }
+  }
+
+  const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
+  const uint32_t cpc = (nvec + kBlock - 1) / kBlock;  // 4 KiB chunks per unit
+  const uint32_t units = static_cast<uint32_t>(a.nstripes) * cpc;
+  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+    if constexpr (!SREG) asm volatile("" ::: "memory");  // keep the LDS table reads inside the loop
+    const uint32_t s = u / cpc;
+    const uint32_t v = (u - s * cpc) * kBlock + threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + static_cast<int64_t>(s) * a.in_stripe_stride);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + static_cast<int64_t>(s) * a.out_stripe_stride);
+    if (v >= nvec) continue;
+    const uint32_t voff = v * 16u;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, static_cast<int>(a.in_off[j]), 0);
+      x[j] = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+    uint4 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const Sel sx = make_sel(x[j].x), sy = make_sel(x[j].y), sz = make_sel(x[j].z), sw = make_sel(x[j].w);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int t = r * K + j;
+        uint4 m;
+        if constexpr (SREG) {
+          const RegTab tb{vlo0[t], vmid0[t], tabs.w[t][1], tabs.w[t][3], tabs.w[t][4]};
+          m.x = gf_mul4_reg(tb, sx);
+          m.y = gf_mul4_reg(tb, sy);
+          m.z = gf_mul4_reg(tb, sz);
+          m.w = gf_mul4_reg(tb, sw);
+        } else {
+          const PermTab tb{s_w[0][t], s_w[1][t], s_w[2][t], s_w[3][t], s_w[4][t]};
+          m.x = gf_mul4_lds(tb, sx);
+          m.y = gf_mul4_lds(tb, sy);
+          m.z = gf_mul4_lds(tb, sz);
+          m.w = gf_mul4_lds(tb, sw);
+        }
+        acc[r].x ^= m.x;
+        acc[r].y ^= m.y;
+        acc[r].z ^= m.z;
+        acc[r].w ^= m.w;
+      }
+      // bound live ranges: input j's selectors (and, in LDS mode, its table reads) stay in this group
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+      __builtin_amdgcn_raw_buffer_store_b128(d, rout, voff, static_cast<int>(a.out_off[r]), 0);
+    }
+  }
+}
+
+// Runtime k, R outputs (tables re-read from LDS per input). Used for schemas not instantiated above.
+template <int R>
+__global__ __launch_bounds__(kBlock) void gf_code_vec_generic(const CodeArgs a, int row0) {
+  __shared__ PermTab s_tab[OZEC_MAX_ROWS * OZEC_MAX_K];
+  const int k = a.k;
+  for (int t = threadIdx.x; t < R * k; t += blockDim.x) s_tab[t] = make_tab(a.coef[row0 * k + t]);
+  __syncthreads();
+  const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
+  const uint32_t cpc = (nvec + kBlock - 1) / kBlock;
+  const uint32_t units = static_cast<uint32_t>(a.nstripes) * cpc;
+  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const uint32_t s = u / cpc;
+    const uint32_t v = (u - s * cpc) * kBlock + threadIdx.x;
+    if (v >= nvec) continue;
+    const uint8_t *ib = a.in + static_cast<int64_t>(s) * a.in_stripe_stride + static_cast<int64_t>(v) * 16;
+    uint8_t *ob = a.out + static_cast<int64_t>(s) * a.out_stripe_stride + static_cast<int64_t>(v) * 16;
+    uint4 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < k; ++j) {
+      const uint4 x = *reinterpret_cast<const uint4 *>(ib + a.in_off[j]);
+      const Sel sx = make_sel(x.x), sy = make_sel(x.y), sz = make_sel(x.z), sw = make_sel(x.w);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const PermTab t = s_tab[r * k + j];
+        acc[r].x ^= gf_mul4(t, sx);
+        acc[r].y ^= gf_mul4(t, sy);
+        acc[r].z ^= gf_mul4(t, sz);
+        acc[r].w ^= gf_mul4(t, sw);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) *reinterpret_cast<uint4 *>(ob + a.out_off[row0 + r]) = acc[r];
+  }
+}
+
+// XOR of K inputs (XORRawEncoder / XORRawDecoder): one output.
+template <int K>
+__global__ __launch_bounds__(kBlock) void xor_vec(const CodeArgs a) {
+  const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
+  const uint32_t cpc = (nvec + kBlock - 1) / kBlock;
+  const uint32_t units = static_cast<uint32_t>(a.nstripes) * cpc;
+  const int k = K > 0 ? K : a.k;
+  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const uint32_t s = u / cpc;
+    const uint32_t v = (u - s * cpc) * kBlock + threadIdx.x;
+    if (v >= nvec) continue;
+    const uint8_t *ib = a.in + static_cast<int64_t>(s) * a.in_stripe_stride + static_cast<int64_t>(v) * 16;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < (K > 0 ? K : OZEC_MAX_K); ++j) {
+      if (K == 0 && j >= k) break;
+      const uint4 x = *reinterpret_cast<const uint4 *>(ib + a.in_off[j]);
+      acc.x ^= x.x;
+      acc.y ^= x.y;
+      acc.z ^= x.z;
+      acc.w ^= x.w;
+    }
+    *reinterpret_cast<uint4 *>(a.out + static_cast<int64_t>(s) * a.out_stripe_stride + a.out_off[0] +
+                               static_cast<int64_t>(v) * 16) = acc;
+  }
+}
+
+// Byte-granular coding for lengths not a multiple of 16 (tail) and unaligned layouts.
+__global__ __launch_bounds__(kBlock) void gf_code_bytes(const CodeArgs a, int64_t start) {
+  __shared__ PermTab s_tab[OZEC_MAX_ROWS * OZEC_MAX_K];
+  const int k = a.k, rows = a.rows;
+  build_tabs(s_tab, a, rows, k);
+  __syncthreads();
+  const int64_t span = a.len - start;
+  const int64_t total = span * a.nstripes;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t s = i / span;
+    const int64_t x = start + (i - s * span);
+    const uint8_t *ib = a.in + s * a.in_stripe_stride + x;
+    uint8_t *ob = a.out + s * a.out_stripe_stride + x;
+    for (int r = 0; r < rows; ++r) {
+      uint32_t acc = 0;
+      for (int j = 0; j < k; ++j) {
+        const uint32_t b = ib[a.in_off[j]];
+        acc ^= a.all_ones ? b : (gf_mul4(s_tab[r * k + j], make_sel(b)) & 0xffu);
+      }
+      ob[a.out_off[r]] = static_cast<uint8_t>(acc);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// CRC helpers (tables in LDS, see CrcTables layout in kernels.hpp)
+
+__device__ __forceinline__ uint32_t crc_f16(const uint32_t *T, const uint4 b) {
+  // byte i of the block (little-endian in b.x..b.w) contributes T_{15-i}[b_i]
+  uint32_t r0 = T[15 * 256 + (b.x & 0xff)] ^ T[14 * 256 + ((b.x >> 8) & 0xff)] ^
+                T[13 * 256 + ((b.x >> 16) & 0xff)] ^ T[12 * 256 + (b.x >> 24)];
+  uint32_t r1 = T[11 * 256 + (b.y & 0xff)] ^ T[10 * 256 + ((b.y >> 8) & 0xff)] ^
+                T[9 * 256 + ((b.y >> 16) & 0xff)] ^ T[8 * 256 + (b.y >> 24)];
+  uint32_t r2 = T[7 * 256 + (b.z & 0xff)] ^ T[6 * 256 + ((b.z >> 8) & 0xff)] ^
+                T[5 * 256 + ((b.z >> 16) & 0xff)] ^ T[4 * 256 + (b.z >> 24)];
+  uint32_t r3 = T[3 * 256 + (b.w & 0xff)] ^ T[2 * 256 + ((b.w >> 8) & 0xff)] ^
+                T[1 * 256 + ((b.w >> 16) & 0xff)] ^ T[0 * 256 + (b.w >> 24)];
+  return r0 ^ r1 ^ r2 ^ r3;
+}
+
+// shift a raw register by the byte distance Z encodes: Z is 4 x 256 (one table per register byte)
+__device__ __forceinline__ uint32_t crc_shift(const uint32_t *Z, uint32_t s) {
+  return Z[s & 0xff] ^ Z[256 + ((s >> 8) & 0xff)] ^ Z[512 + ((s >> 16) & 0xff)] ^ Z[768 + (s >> 24)];
+}
+
+// level 0 (16 B) of the lane tree uses the slice tables T_15..T_12
+__device__ __forceinline__ uint32_t crc_shift16(const uint32_t *T, uint32_t s) {
+  return T[15 * 256 + (s & 0xff)] ^ T[14 * 256 + ((s >> 8) & 0xff)] ^ T[13 * 256 + ((s >> 16) & 0xff)] ^
+         T[12 * 256 + (s >> 24)];
+}
+
+// merge the 64 lane registers of a wave into the register of the whole window (every lane gets it)
+__device__ __forceinline__ uint32_t crc_lane_tree(const uint32_t *tabs, uint32_t v, int lane) {
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), 1 << m, 64));
+    const bool upper = (lane >> m) & 1;
+    const uint32_t lower = upper ? other : v;
+    const uint32_t hi = upper ? v : other;
+    const uint32_t shifted =
+        m == 0 ? crc_shift16(tabs + kCrcSliceOff, lower) : crc_shift(tabs + kCrcTreeOff + (m - 1) * 1024, lower);
+    v = shifted ^ hi;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void load_crc_tables(uint32_t *s_crc, const uint32_t *g) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(g);
+  uint4 *dst = reinterpret_cast<uint4 *>(s_crc);
+  for (int i = threadIdx.x; i < kCrcTableWords / 4; i += blockDim.x) dst[i] = src[i];
+}
+
+__device__ __forceinline__ uint32_t crc_finish(uint32_t raw, uint32_t init, int raw_out, int big_endian) {
+  uint32_t v = raw_out ? raw : ~(raw ^ init);
+  return big_endian ? __builtin_bswap32(v) : v;
+}
+
+// One wave per (cell, window). Requires 16-B aligned cells and bpc % 16 == 0; any len.
+constexpr int kCrcUnroll = 4;
+__global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_crc[kCrcTableWords];
+  load_crc_tables(s_crc, a.tables);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t units = a.ncells * a.nwin;
+  for (int64_t u = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + wave; u < units;
+       u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
+    const int64_t c = u / a.nwin;
+    const int64_t w = u - c * a.nwin;
+    const bool last = w == a.nwin - 1;
+    const int64_t N = last ? a.len - w * a.bpc : a.bpc;
+    const int64_t m = N >> 4;
+    const int64_t T = (m + 63) >> 6;
+    const int64_t P = T * 64 - m;  // virtual zero blocks in front
+    const uint8_t *win = a.base + c * a.cell_stride + w * a.bpc;
+    uint32_t S = 0;
+    for (int64_t t0 = 0; t0 < T; t0 += kCrcUnroll) {
+      uint4 blk[kCrcUnroll];
+#pragma unroll
+      for (int q = 0; q < kCrcUnroll; ++q) {
+        const int64_t vb = (t0 + q) * 64 + lane - P;
+        blk[q] = make_uint4(0, 0, 0, 0);
+        if (t0 + q < T && vb >= 0) blk[q] = *reinterpret_cast<const uint4 *>(win + vb * 16);
+      }
+#pragma unroll
+      for (int q = 0; q < kCrcUnroll; ++q) {
+        if (t0 + q < T) S = crc_shift(s_crc + kCrcZ1024Off, S) ^ crc_f16(s_crc, blk[q]);
+      }
+    }
+    S = crc_lane_tree(s_crc, S, lane);
+    for (int64_t i = m * 16; i < N; ++i) S = (S >> 8) ^ s_crc[(S ^ win[i]) & 0xff];
+    if (lane == 0) a.out[c * a.out_cell_stride + w] = crc_finish(S, last ? a.init_last : a.init_full, a.raw, a.big_endian);
+  }
+}
+
+// Scalar fallback: one thread per window, byte-at-a-time (any alignment, any bpc).
+__global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
+  __shared__ uint32_t s_t0[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_t0[i] = a.tables[i];
+  __syncthreads();
+  const int64_t units = a.ncells * a.nwin;
+  for (int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; u < units;
+       u += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t c = u / a.nwin;
+    const int64_t w = u - c * a.nwin;
+    const bool last = w == a.nwin - 1;
+    const int64_t N = last ? a.len - w * a.bpc : a.bpc;
+    const uint8_t *win = a.base + c * a.cell_stride + w * a.bpc;
+    uint32_t S = 0;
+    for (int64_t i = 0; i < N; ++i) S = (S >> 8) ^ s_t0[(S ^ win[i]) & 0xff];
+    a.out[c * a.out_cell_stride + w] = crc_finish(S, last ? a.init_last : a.init_full, a.raw, a.big_endian);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused encode + CRC: one wave per (stripe, window); lanes walk the window 1 KiB at a time, producing
+// parity and folding all K+R units into their CRC registers while the bytes are in VGPRs.
+template <int K, int R>
+__global__ __launch_bounds__(kBlock) void encode_crc_vec(const EncCrcArgs e) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_crc[kCrcTableWords];
+  __shared__ PermTab s_tab[K * R];
+  const CodeArgs &a = e.code;
+  const CrcArgs &cr = e.crc;
+  load_crc_tables(s_crc, cr.tables);
+  build_tabs(s_tab, a, R, K);
+  __syncthreads();
+  PermTab tab[R][K];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int j = 0; j < K; ++j) tab[r][j] = s_tab[r * K + j];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t nwin = cr.nwin;
+  const int64_t units = a.nstripes * nwin;
+  for (int64_t u = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + wave; u < units;
+       u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
+    const int64_t s = u / nwin;
+    const int64_t w = u - s * nwin;
+    const bool last = w == nwin - 1;
+    const int64_t N = last ? a.len - w * cr.bpc : cr.bpc;
+    const int64_t m = N >> 4;
+    const int64_t T = (m + 63) >> 6;
+    const int64_t P = T * 64 - m;
+    const uint8_t *ib = a.in + s * a.in_stripe_stride + w * cr.bpc;
+    uint8_t *ob = a.out + s * a.out_stripe_stride + w * cr.bpc;
+    uint32_t S[K + R];
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) S[q] = 0;
+    for (int64_t t = 0; t < T; ++t) {
+      const int64_t vb = t * 64 + lane - P;
+      uint4 x[K];
+      uint4 acc[R];
+      if (vb >= 0) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = *reinterpret_cast<const uint4 *>(ib + a.in_off[j] + vb * 16);
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const Sel sx = make_sel(x[j].x), sy = make_sel(x[j].y), sz = make_sel(x[j].z), sw = make_sel(x[j].w);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            acc[r].x ^= gf_mul4(tab[r][j], sx);
+            acc[r].y ^= gf_mul4(tab[r][j], sy);
+            acc[r].z ^= gf_mul4(tab[r][j], sz);
+            acc[r].w ^= gf_mul4(tab[r][j], sw);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) *reinterpret_cast<uint4 *>(ob + a.out_off[r] + vb * 16) = acc[r];
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < K; ++j) S[j] = crc_shift(s_crc + kCrcZ1024Off, S[j]) ^ crc_f16(s_crc, x[j]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) S[K + r] = crc_shift(s_crc + kCrcZ1024Off, S[K + r]) ^ crc_f16(s_crc, acc[r]);
+    }
+    const uint32_t init = last ? cr.init_last : cr.init_full;
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) {
+      const uint32_t v = crc_lane_tree(s_crc, S[q], lane);
+      if (lane == q) cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// splitmix64 fill (bench / test data), twin of tests/golden/synth.py
+
+__global__ __launch_bounds__(kBlock) void fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t ncells,
+                                                          int64_t n, uint64_t seed, uint64_t first_stream) {
+  const int64_t words = (n + 7) >> 3;
+  const int64_t total = words * ncells;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t c = i / words;
+    const int64_t wi = i - c * words;
+    const uint64_t state0 = seed ^ ((first_stream + static_cast<uint64_t>(c)) * 0x9E3779B97F4A7C15ull);
+    uint64_t z = state0 + static_cast<uint64_t>(wi + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    uint8_t *dst = base + c * cell_stride + wi * 8;
+    const int64_t nb = n - wi * 8 < 8 ? n - wi * 8 : 8;
+    if (nb == 8 && (reinterpret_cast<uintptr_t>(dst) & 7) == 0) {
+      *reinterpret_cast<uint64_t *>(dst) = z;
+    } else {
+      for (int b = 0; b < nb; ++b) dst[b] = static_cast<uint8_t>(z >> (8 * b));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launch helpers
+
+inline unsigned grid_for(int64_t work_items, int per_block) {
+  int64_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > kMaxGrid) g = kMaxGrid;
+  return static_cast<unsigned>(g);
+}
+
+inline bool aligned16(int64_t v) { return (v & 15) == 0; }
+
+bool vec_ok(const CodeArgs &a) {
+  if (!aligned16(reinterpret_cast<intptr_t>(a.in)) || !aligned16(reinterpret_cast<intptr_t>(a.out))) return false;
+  if (a.nstripes > 1 && (!aligned16(a.in_stripe_stride) || !aligned16(a.out_stripe_stride))) return false;
+  for (int j = 0; j < a.k; ++j)
+    if (!aligned16(a.in_off[j])) return false;
+  for (int r = 0; r < a.rows; ++r)
+    if (!aligned16(a.out_off[r])) return false;
+  return true;
+}
+
+uint32_t gf_mul_host(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (b & 1) r ^= a;
+    b >>= 1;
+    a = (a << 1) ^ ((a & 0x80) ? 0x11d : 0);
+  }
+  return r & 0xff;
+}
+
+uint32_t pack4_host(uint32_t c, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
+  return gf_mul_host(c, m0) | (gf_mul_host(c, m1) << 8) | (gf_mul_host(c, m2) << 16) | (gf_mul_host(c, m3) << 24);
+}
+
+template <int N>
+TabArgs<N> host_tabs(const CodeArgs &a) {
+  TabArgs<N> t;
+  for (int i = 0; i < N; ++i) {
+    const uint32_t c = a.coef[i];
+    t.w[i][0] = pack4_host(c, 0, 1, 2, 3);
+    t.w[i][1] = pack4_host(c, 4, 5, 6, 7);
+    t.w[i][2] = pack4_host(c, 0, 8, 16, 24);
+    t.w[i][3] = pack4_host(c, 32, 40, 48, 56);
+    t.w[i][4] = pack4_host(c, 0, 64, 128, 192);
+  }
+  return t;
+}
+
+// Fold the smallest unit offset into the base pointers so every unit offset fits the 32-bit buffer soffset.
+bool rebase32(CodeArgs &a) {
+  const int64_t lim = (int64_t{1} << 31) - a.len - 16;
+  int64_t mn = a.in_off[0], mx = a.in_off[0];
+  for (int j = 1; j < a.k; ++j) {
+    mn = a.in_off[j] < mn ? a.in_off[j] : mn;
+    mx = a.in_off[j] > mx ? a.in_off[j] : mx;
+  }
+  if (mx - mn > lim) return false;
+  a.in = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(a.in) + mn);
+  for (int j = 0; j < a.k; ++j) a.in_off[j] -= mn;
+  mn = mx = a.out_off[0];
+  for (int r = 1; r < a.rows; ++r) {
+    mn = a.out_off[r] < mn ? a.out_off[r] : mn;
+    mx = a.out_off[r] > mx ? a.out_off[r] : mx;
+  }
+  if (mx - mn > lim) return false;
+  a.out = reinterpret_cast<uint8_t *>(reinterpret_cast<uintptr_t>(a.out) + mn);
+  for (int r = 0; r < a.rows; ++r) a.out_off[r] -= mn;
+  return true;
+}
+
+template <int K, int R>
+hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
+  constexpr bool kSreg = K * R <= 18;
+  const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
+  const int64_t units = a.nstripes * ((nvec + kBlock - 1) / kBlock);
+  const TabArgs<K * R> tabs = host_tabs<K * R>(a);
+  hipLaunchKernelGGL((gf_code_vec<K, R, kSreg>), dim3(grid_for(units, 1)), dim3(kBlock), 0, st, a, tabs);
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_xor(const CodeArgs &a, hipStream_t st) {
+  const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
+  const int64_t units = a.nstripes * ((nvec + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL((xor_vec<K>), dim3(grid_for(units, 1)), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
+  if (a.all_ones && a.rows == 1) {
+    switch (a.k) {
+      case 2: return launch_xor<2>(a, st);
+      case 3: return launch_xor<3>(a, st);
+      case 4: return launch_xor<4>(a, st);
+      case 6: return launch_xor<6>(a, st);
+      case 10: return launch_xor<10>(a, st);
+      default: return launch_xor<0>(a, st);
+    }
+  }
+  CodeArgs rb = a;
+  const bool fits32 = rebase32(rb);
+#define OZEC_KR(KK, RR) \
+  if (fits32 && a.k == KK && a.rows == RR) return launch_kr<KK, RR>(rb, st);
+  OZEC_KR(3, 1) OZEC_KR(3, 2)
+  OZEC_KR(6, 1) OZEC_KR(6, 2) OZEC_KR(6, 3)
+  OZEC_KR(10, 1) OZEC_KR(10, 2) OZEC_KR(10, 3) OZEC_KR(10, 4)
+#undef OZEC_KR
+  const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
+  const int64_t units = a.nstripes * ((nvec + kBlock - 1) / kBlock);
+  const unsigned grid = grid_for(units, 1);
+  for (int row0 = 0; row0 < a.rows; row0 += 4) {
+    const int rr = a.rows - row0 < 4 ? a.rows - row0 : 4;
+    switch (rr) {
+      case 1: hipLaunchKernelGGL(gf_code_vec_generic<1>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+      case 2: hipLaunchKernelGGL(gf_code_vec_generic<2>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+      case 3: hipLaunchKernelGGL(gf_code_vec_generic<3>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+      default: hipLaunchKernelGGL(gf_code_vec_generic<4>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+    }
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_code(const CodeArgs &a, hipStream_t st) {
+  if (a.len <= 0 || a.nstripes <= 0) return hipSuccess;
+  int64_t start = 0;
+  if (vec_ok(a) && a.len >= 16) {
+    hipError_t err = launch_vec(a, st);
+    if (err != hipSuccess) return err;
+    start = a.len & ~static_cast<int64_t>(15);
+  }
+  if (start < a.len) {
+    const int64_t total = (a.len - start) * a.nstripes;
+    hipLaunchKernelGGL(gf_code_bytes, dim3(grid_for(total, kBlock)), dim3(kBlock), 0, st, a, start);
+    return hipGetLastError();
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
+  const int64_t units = a.ncells * a.nwin;
+  if (units <= 0) return hipSuccess;
+  const bool vec = aligned16(reinterpret_cast<intptr_t>(a.base)) && (a.ncells == 1 || aligned16(a.cell_stride)) &&
+                   aligned16(a.bpc);
+  if (vec) {
+    hipLaunchKernelGGL(crc_windows_vec, dim3(grid_for(units, kBlock / 64)), dim3(kBlock), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(crc_windows_bytes, dim3(grid_for(units, kBlock)), dim3(kBlock), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
+  const bool kr = (a.k == 3 && a.rows == 2) || (a.k == 6 && a.rows == 3) || (a.k == 10 && a.rows == 4) ||
+                  (a.k == 2 && a.rows == 1);
+  return kr && bpc > 0 && aligned16(bpc) && aligned16(a.len) && vec_ok(a);
+}
+
+hipError_t launch_encode_crc(const EncCrcArgs &e, hipStream_t st) {
+  const int64_t units = e.code.nstripes * e.crc.nwin;
+  if (units <= 0) return hipSuccess;
+  const dim3 grid(grid_for(units, kBlock / 64)), block(kBlock);
+  if (e.code.k == 6 && e.code.rows == 3) {
+    hipLaunchKernelGGL((encode_crc_vec<6, 3>), grid, block, 0, st, e);
+  } else if (e.code.k == 3 && e.code.rows == 2) {
+    hipLaunchKernelGGL((encode_crc_vec<3, 2>), grid, block, 0, st, e);
+  } else if (e.code.k == 10 && e.code.rows == 4) {
+    hipLaunchKernelGGL((encode_crc_vec<10, 4>), grid, block, 0, st, e);
+  } else if (e.code.k == 2 && e.code.rows == 1) {
+    hipLaunchKernelGGL((encode_crc_vec<2, 1>), grid, block, 0, st, e);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t ncells, int64_t n, uint64_t seed,
+                                  uint64_t first_stream, hipStream_t st) {
+  const int64_t total = ((n + 7) >> 3) * ncells;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_splitmix64, dim3(grid_for(total, kBlock)), dim3(kBlock), 0, st, base, cell_stride, ncells,
+                     n, seed, first_stream);
+  return hipGetLastError();
+}
+
+}  // namespace ozec

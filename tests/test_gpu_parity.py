@@ -1,0 +1,326 @@
+"""HIP path vs the oracle, bit-exact, through the C ABI (host, device and batch entry points).
+
+Sizes: every committed golden vector (up to 1 MiB cells), seeded random batches the oracle finishes in
+seconds, and BASELINE.json's full configurations through size-independent properties
+(encode -> erase -> decode round trips, CRC of concatenation == combine of CRCs).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from golden_io import case_id, case_inputs, ec_cases, load, matches
+from synth import SEED, cells, splitmix64_bytes
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from ozone_amd import _lib as L  # noqa: E402
+from ozone_amd import checksum as ck  # noqa: E402
+from ozone_amd import rawcoder as rc  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def enc(codec, k, p):
+    return rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec))
+
+
+def dec(codec, k, p):
+    return rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec))
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def h(x):
+    torch.cuda.synchronize()
+    return x.cpu().numpy()
+
+
+# ------------------------------------------------------------------------------------------ golden
+
+
+@pytest.mark.parametrize("case", ec_cases("encode"), ids=case_id)
+def test_encode_golden_host_path(case):
+    data = case_inputs(case)
+    par = [np.zeros(case["len"], np.uint8) for _ in range(case["p"])]
+    enc(case["codec"], case["k"], case["p"]).encode(data, par)
+    n_rows = case["p"] if case["codec"] == "rs" else 1
+    assert all(matches(b, x) for b, x in zip(case["parity"], par[:n_rows]))
+    assert all(not x.any() for x in par[n_rows:])  # XOR p>1: extra outputs zero-filled
+
+
+@pytest.mark.parametrize("case", ec_cases("decode"), ids=case_id)
+def test_decode_golden_host_path(case):
+    k, p = case["k"], case["p"]
+    data = case_inputs(case)
+    units = data + (oracle.rs_encode(k, p, data) if case["codec"] == "rs" else [oracle.xor_encode(data)])
+    inputs = [units[u] if u in case["present"] else None for u in range(k + p)]
+    outs = [np.full(case["len"], 0xA5, np.uint8) for _ in case["erased"]]  # garbage: must be overwritten
+    dec(case["codec"], k, p).decode(inputs, case["erased"], outs)
+    assert all(matches(b, x) for b, x in zip(case["outputs"], outs))
+
+
+@pytest.mark.parametrize("case", ec_cases("encode", max_len=20000), ids=case_id)
+def test_encode_golden_device_path(case):
+    data = case_inputs(case)
+    d_in = [t(x) for x in data]
+    d_out = [torch.zeros(case["len"], dtype=torch.uint8, device=DEV) for _ in range(case["p"])]
+    enc(case["codec"], case["k"], case["p"]).encode_device(d_in, d_out, case["len"])
+    n_rows = case["p"] if case["codec"] == "rs" else 1
+    assert all(matches(b, h(x)) for b, x in zip(case["parity"], d_out[:n_rows]))
+
+
+@pytest.mark.parametrize("case", [c for c in ec_cases("decode", max_len=2000)], ids=case_id)
+def test_decode_golden_device_path(case):
+    k, p = case["k"], case["p"]
+    data = case_inputs(case)
+    units = data + (oracle.rs_encode(k, p, data) if case["codec"] == "rs" else [oracle.xor_encode(data)])
+    d_in = [t(units[u]) if u in case["present"] else None for u in range(k + p)]
+    d_out = [torch.zeros(case["len"], dtype=torch.uint8, device=DEV) for _ in case["erased"]]
+    dec(case["codec"], k, p).decode_device(d_in, case["erased"], d_out, case["len"])
+    assert all(matches(b, h(x)) for b, x in zip(case["outputs"], d_out))
+
+
+# ------------------------------------------------------------------------------------------ batches
+
+
+@pytest.mark.parametrize("k,p,n,S", [(6, 3, 1 << 20, 8), (3, 2, 1 << 20, 4), (10, 4, 65536, 8), (6, 3, 1040, 33),
+                                     (6, 3, 1007, 17), (10, 4, 4096 + 16, 5), (2, 1, 65536, 4), (12, 4, 8192, 3),
+                                     (5, 2, 4096, 3), (4, 7, 2048, 2)])
+def test_encode_batch_vs_oracle(k, p, n, S):
+    data = np.stack([np.stack(cells(SEED, 1000 + s * k, k, n)) for s in range(S)])
+    d = t(data)
+    e = enc("rs", k, p)
+    par = h(e.encode_stripes(d))
+    for s in range(S):
+        ref = oracle.rs_encode(k, p, list(data[s]))
+        assert all((par[s, r] == ref[r]).all() for r in range(p)), s
+
+
+def test_encode_batch_block_major_layout():
+    """Units laid out block-major ([unit][stripe][cell]) as a datanode keeps one block file per unit."""
+    k, p, n, S = 6, 3, 1 << 16, 16
+    blocks = np.stack([np.concatenate(cells(SEED, 5000 + u * S, S, n)) for u in range(k)])  # [k][S*n]
+    d_in = t(blocks)
+    d_out = torch.empty((p, S * n), dtype=torch.uint8, device=DEV)
+    enc("rs", k, p).encode_batch(d_in, n, S * n, d_out, n, S * n, S, n)
+    out = h(d_out)
+    for s in (0, 7, 15):
+        ref = oracle.rs_encode(k, p, [blocks[u, s * n:(s + 1) * n] for u in range(k)])
+        assert all((out[r, s * n:(s + 1) * n] == ref[r]).all() for r in range(p))
+
+
+def test_encode_unaligned_addresses():
+    """16-B misaligned cells (ByteBuffer position 11 / arrayOffset != 0, TestCoderBase.java:327-342)."""
+    k, p, n = 6, 3, 5000
+    data = cells(SEED, 9000, k, n)
+    raw = torch.zeros((k, n + 32), dtype=torch.uint8, device=DEV)
+    for j in range(k):
+        raw[j, 11:11 + n] = t(data[j])
+    out = torch.zeros((p, n + 32), dtype=torch.uint8, device=DEV)
+    enc("rs", k, p).encode_device([raw[j, 11:] for j in range(k)], [out[r, 3:] for r in range(p)], n)
+    ref = oracle.rs_encode(k, p, data)
+    got = h(out)
+    assert all((got[r, 3:3 + n] == ref[r]).all() for r in range(p))
+    assert not got[:, :3].any() and not got[:, 3 + n:].any()  # nothing written outside the cells
+
+
+@pytest.mark.parametrize("k,p,erased", [(6, 3, [0, 1, 2]), (6, 3, [1, 7]), (10, 4, [0, 1, 2, 3]),
+                                        (10, 4, [1, 4, 10, 13]), (3, 2, [2, 4]), (6, 3, [6, 7, 8]),
+                                        (10, 4, [5]), (10, 4, [0, 13])])
+def test_decode_batch_vs_oracle(k, p, erased):
+    n, S = 65536 + 16, 6
+    data = [cells(SEED, 20000 + s * k, k, n) for s in range(S)]
+    units = np.stack([np.stack(d + oracle.rs_encode(k, p, d)) for d in data])  # [S][k+p][n]
+    present = [u for u in range(k + p) if u not in erased]
+    d_in = t(units)
+    d_out = torch.zeros((S, len(erased), n), dtype=torch.uint8, device=DEV)
+    dec("rs", k, p).decode_batch(d_in, (k + p) * n, n, present, erased, d_out, len(erased) * n, n, S, n)
+    got = h(d_out)
+    for s in range(S):
+        assert all((got[s, i] == units[s, e]).all() for i, e in enumerate(erased)), s
+
+
+def test_decode_uses_first_k_valid_inputs():
+    """RSRawDecoder.java:79-82: with more than k inputs present only the first k are read -- corrupting a later
+    one must not change the output."""
+    k, p, n = 6, 3, 4096
+    d = cells(SEED, 31000, k, n)
+    units = d + oracle.rs_encode(k, p, d)
+    ins = [None] + units[1:]
+    ins[8] = np.zeros(n, np.uint8)  # 9th unit (beyond the first 6 valid) corrupted
+    out = [np.zeros(n, np.uint8)]
+    dec("rs", k, p).decode(ins, [0], out)
+    assert (out[0] == units[0]).all()
+
+
+# ------------------------------------------------------------------------------------------ checksums
+
+
+def _crc_type(name):
+    return ck.ChecksumType.CRC32 if name == "crc32" else ck.ChecksumType.CRC32C
+
+
+@pytest.mark.parametrize("case", load("crc_vectors.json")["cases"],
+                         ids=lambda c: f"{c['type']}-n{c['len']}-bpc{c['bpc']}")
+def test_checksum_golden(case):
+    data = splitmix64_bytes(case["seed"], case["stream"], case["len"])
+    cd = ck.Checksum(_crc_type(case["type"]), case["bpc"]).compute_checksum(data)
+    assert [int.from_bytes(b, "big") for b in cd.get_checksums()] == case["crcs"]
+
+
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32, oracle.CRC32), (ck.ChecksumType.CRC32C, oracle.CRC32C)])
+@pytest.mark.parametrize("bpc", [16, 512, 1024, 2048, 4096, 16384, 32768, 1 << 20, 1000, 10, 4097])
+def test_checksum_batch_vs_oracle(ctype, otype, bpc):
+    n, C = 3 * 65536 + 5, 5
+    data = np.stack(cells(SEED, 40000, C, n))
+    nwin = (n + bpc - 1) // bpc
+    d_out = torch.zeros((C, nwin), dtype=torch.int32, device=DEV)
+    ck.checksum_windows_batch(ctype, t(data), n, C, n, bpc, d_out)
+    got = h(d_out).view(np.uint32)
+    for c in range(C):
+        assert (got[c] == oracle.crc_windows(otype, data[c], bpc)).all(), c
+
+
+def test_checksum_unaligned_and_big_endian():
+    n, bpc = 70000, 16384
+    data = cells(SEED, 41000, 1, n + 3)[0]
+    d = t(data)
+    nwin = (n + bpc - 1) // bpc
+    out = torch.zeros(nwin, dtype=torch.int32, device=DEV)
+    rc_ = L.lib().ozec_checksum_windows_device(L.OZEC_CHECKSUM_CRC32C, d.data_ptr() + 3, n, bpc, out.data_ptr(), 1,
+                                               torch.cuda.current_stream().cuda_stream)
+    assert rc_ == 0
+    got = h(out).view(np.uint32)
+    ref = oracle.crc_windows(oracle.CRC32C, data[3:], bpc)
+    assert (got == ref.byteswap()).all()  # big-endian = the bytes Ints.toByteArray stores
+
+
+def test_checksum_reference_shapes():
+    # TestChecksum.java:48-96: 55 bytes, bpc 10 -> 6 checksums; verify ok; corruption detected
+    data = np.frombuffer(bytes(range(55)), np.uint8)
+    c = ck.Checksum(ck.ChecksumType.CRC32, 10)
+    cd = c.compute_checksum(data)
+    assert len(cd.get_checksums()) == 6
+    assert ck.Checksum.verify_checksum(data, cd)
+    bad = data.copy()
+    bad[25] ^= 1
+    with pytest.raises(ck.OzoneChecksumException) as ei:
+        ck.Checksum.verify_checksum(bad, cd)
+    assert ei.value.index == 2
+    assert ck.Checksum(ck.ChecksumType.NONE, 10).compute_checksum(data).get_checksums() == []
+    assert ck.Checksum(ck.ChecksumType.CRC32C, 16).compute_checksum(b"").get_checksums() == []
+
+
+def test_streaming_checksum_prefixes():
+    """TestChecksumByteBuffer.java:36-119: update byte-by-byte / chunk-wise equals the one-shot value."""
+    data = cells(SEED, 42000, 1, 1000)[0]
+    for ctype, otype in ((ck.ChecksumType.CRC32, oracle.CRC32), (ck.ChecksumType.CRC32C, oracle.CRC32C)):
+        s = ck.ChecksumByteBuffer(ctype)
+        for i, cut in enumerate((0, 1, 9, 100, 577, 1000)):
+            if i:
+                s.update(data, (0, 1, 9, 100, 577, 1000)[i - 1], cut - (0, 1, 9, 100, 577, 1000)[i - 1])
+            assert s.get_value() == oracle.crc(otype, data[:cut])
+        s.reset()
+        s.update(int(data[0]))
+        assert s.get_value() == oracle.crc(otype, data[:1])
+
+
+def test_checksum_impls_compute_same_values_64mib():
+    """TestChecksumImplsComputeSameValues.java:39-101 scale: 64 MiB random, several bpc."""
+    n = 64 << 20
+    d = torch.empty(n, dtype=torch.uint8, device=DEV)
+    rc.fill_splitmix64_cells(d, 0, 1, n, SEED, 43000)
+    host = h(d)
+    assert (host[:4096] == splitmix64_bytes(SEED, 43000, 4096)).all()
+    for ctype, otype in ((ck.ChecksumType.CRC32, oracle.CRC32), (ck.ChecksumType.CRC32C, oracle.CRC32C)):
+        for bpc in (512, 1024, 2048, 4096, 32768, 1 << 20):
+            nwin = n // bpc
+            out = torch.zeros(nwin, dtype=torch.int32, device=DEV)
+            ck.checksum_windows_batch(ctype, d, 0, 1, n, bpc, out)
+            got = h(out).view(np.uint32)
+            idx = np.linspace(0, nwin - 1, 40).astype(int)
+            ref = [oracle.crc(otype, host[i * bpc:(i + 1) * bpc]) for i in idx]
+            assert (got[idx] == np.array(ref, np.uint32)).all()
+
+
+# ------------------------------------------------------------------------------------------ fused
+
+
+@pytest.mark.parametrize("k,p,codec,n,bpc,S", [(6, 3, "rs", 1 << 20, 16384, 4), (3, 2, "rs", 1 << 20, 16384, 2),
+                                               (10, 4, "rs", 1 << 18, 16384, 3), (2, 1, "xor", 1 << 20, 16384, 3),
+                                               (6, 3, "rs", 65536, 4096, 3), (6, 3, "rs", 1040 * 16, 1040, 2),
+                                               (6, 3, "rs", 50000, 16384, 2), (5, 2, "rs", 65536, 16384, 2)])
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
+def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
+    data = np.stack([np.stack(cells(SEED, 50000 + s * k, k, n)) for s in range(S)])
+    rows = p if codec == "rs" else 1
+    nwin = (n + bpc - 1) // bpc
+    d_in = t(data)
+    d_out = torch.zeros((S, rows, n), dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, k + rows, nwin), dtype=torch.int32, device=DEV)
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, rows, codec))
+    e.encode_crc_batch(d_in, k * n, n, d_out, rows * n, n, S, n, ctype, bpc, d_crc)
+    par, crcs = h(d_out), h(d_crc).view(np.uint32)
+    for s in range(S):
+        ref = oracle.rs_encode(k, rows, list(data[s])) if codec == "rs" else [oracle.xor_encode(list(data[s]))]
+        units = list(data[s]) + ref
+        assert all((par[s, r] == ref[r]).all() for r in range(rows))
+        for u in range(k + rows):
+            assert (crcs[s, u] == oracle.crc_windows(otype, units[u], bpc)).all(), (s, u)
+
+
+# ------------------------------------------------------------------------------------------ full size
+
+
+def test_full_size_rs_6_3_roundtrip_4096_stripes():
+    """BASELINE config C2 shape (24 GiB data): encode, erase 3 data units, decode, compare bytes on the GPU."""
+    k, p, n, S = 6, 3, 1 << 20, 4096
+    units = torch.empty((S, k + p, n), dtype=torch.uint8, device=DEV)
+    rc.fill_splitmix64_cells(units, (k + p) * n, S, n, SEED, 0)  # unit 0 of each stripe only; fill the rest:
+    for u in range(1, k):
+        rc.fill_splitmix64_cells(units[:, u], (k + p) * n, S, n, SEED, 100000 * u)
+    e = enc("rs", k, p)
+    e.encode_batch(units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n)
+    erased = [0, 2, 4]
+    out = torch.empty((S, 3, n), dtype=torch.uint8, device=DEV)
+    present = [u for u in range(k + p) if u not in erased]
+    dec("rs", k, p).decode_batch(units, (k + p) * n, n, present, erased, out, 3 * n, n, S, n)
+    for i, u in enumerate(erased):
+        assert torch.equal(out[:, i], units[:, u])
+    # spot-check parity bytes of a few stripes against the oracle
+    for s in (0, 1234, S - 1):
+        host = h(units[s])
+        ref = oracle.rs_encode(k, p, list(host[:k]))
+        assert all((host[k + r] == ref[r]).all() for r in range(p))
+    del units, out
+    torch.cuda.empty_cache()
+
+
+def test_full_size_rs_10_4_decode_4_erased():
+    """BASELINE config C3 shape (2048 stripes of rs-10-4-1024k), both erasure sets of BASELINE.md."""
+    k, p, n, S = 10, 4, 1 << 20, 2048
+    units = torch.empty((S, k + p, n), dtype=torch.uint8, device=DEV)
+    for u in range(k):
+        rc.fill_splitmix64_cells(units[:, u], (k + p) * n, S, n, SEED, 200000 * (u + 1))
+    enc("rs", k, p).encode_batch(units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n)
+    d = dec("rs", k, p)
+    out = torch.empty((S, 4, n), dtype=torch.uint8, device=DEV)
+    for erased in ([0, 1, 2, 3], [1, 4, 10, 13]):
+        present = [u for u in range(k + p) if u not in erased]
+        d.decode_batch(units, (k + p) * n, n, present, erased, out, 4 * n, n, S, n)
+        for i, u in enumerate(erased):
+            assert torch.equal(out[:, i], units[:, u]), (erased, u)
+    del units, out
+    torch.cuda.empty_cache()
+
+
+def test_splitmix_fill_matches_cpu_twin():
+    n = 12345
+    d = torch.empty((3, n + 5), dtype=torch.uint8, device=DEV)
+    rc.fill_splitmix64_cells(d, n + 5, 3, n, SEED, 77)
+    got = h(d)
+    for c in range(3):
+        assert (got[c, :n] == splitmix64_bytes(SEED, 77 + c, n)).all()

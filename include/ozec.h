@@ -14,8 +14,8 @@
  *   - "host" entry points take host pointers (any alignment, pageable or pinned) and are synchronous, like
  *     RawErasureEncoder.encode (EC/rawcoder/RawErasureEncoder.java:66-97).  They stage through a
  *     process-global, per-GPU pinned buffer pool.
- *   - "_device" / "_batch" entry points take device pointers and an optional hipStream_t (NULL = the
- *     library's stream for the current device) and are asynchronous on that stream.
+ *   - "_device" / "_batch" entry points take device pointers and a hipStream_t (NULL = the default stream
+ *     of the current device) and are asynchronous on that stream.
  *   - Outputs are fully overwritten (the reference zero-fills, then accumulates: CoderUtil.java:84-98).
  *   - Inputs are never modified (TestRawCoderBase.java:180-220).
  */

@@ -101,9 +101,9 @@ int get_ctx(DevCtx **out) {
   return OZEC_OK;
 }
 
-hipStream_t pick_stream(DevCtx *ctx, void *stream) {
-  return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-}
+// NULL selects the device's default (null) stream, as in every HIP/CUDA API: work is then ordered with the
+// caller's default-stream operations (torch's default stream handle is 0).
+hipStream_t pick_stream(DevCtx *, void *stream) { return static_cast<hipStream_t>(stream); }
 
 constexpr size_t kStageAlign = 256;
 inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }

@@ -229,10 +229,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    from ozone_amd.shard import max_over_ranks
+    elapsed = max_over_ranks(elapsed, dist, device="cuda")
     value = wl.data_bytes * world * args.steps / elapsed / 1e9
     achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None

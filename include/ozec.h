@@ -162,6 +162,8 @@ int ozec_parse_replication(const char *s, int *codec, int *num_data, int *num_pa
 uint32_t ozec_crc_combine(int checksum_type, uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
 /* ---- harness utilities ------------------------------------------------------------------------------- */
+/* process-wide kernel tuning knobs for benchmarking ("grid", "gf_variant", "crc_variant"; 0 = default) */
+int ozec_set_tuning(const char *key, int64_t value);
 /* fill n bytes with splitmix64 stream `stream_id` of `seed` (tests/golden/synth.py is the CPU twin) */
 int ozec_fill_splitmix64(uint8_t *d_dst, size_t n, uint64_t seed, uint64_t stream_id, void *stream);
 /* same, many cells: cell c (stream first_stream + c) at d_base + c*cell_stride */

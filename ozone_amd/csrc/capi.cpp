@@ -52,7 +52,7 @@ struct DevCtx {
   size_t pinned_cap = 0;
   uint8_t *dbuf = nullptr;
   size_t dbuf_cap = 0;
-  uint32_t *crc_tables[2] = {nullptr, nullptr};
+  uint32_t *crc_tables[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [type][B == 4]
 
   int reserve(size_t bytes) {
     if (bytes > pinned_cap) {
@@ -90,11 +90,12 @@ int get_ctx(DevCtx **out) {
     auto c = std::make_unique<DevCtx>();
     c->device = dev;
     OZEC_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    for (int t = 0; t < 2; ++t) {
-      const auto &blob = CrcMath::get(static_cast<CrcType>(t)).device_tables();
-      OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->crc_tables[t]), blob.size() * sizeof(uint32_t)));
-      OZEC_HIP(hipMemcpy(c->crc_tables[t], blob.data(), blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    }
+    for (int t = 0; t < 2; ++t)
+      for (int b = 0; b < 2; ++b) {
+        const auto &blob = CrcMath::get(static_cast<CrcType>(t)).device_tables(b ? 4 : 1);
+        OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->crc_tables[t][b]), blob.size() * sizeof(uint32_t)));
+        OZEC_HIP(hipMemcpy(c->crc_tables[t][b], blob.data(), blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+      }
     g_ctx[dev] = std::move(c);
   }
   *out = g_ctx[dev].get();
@@ -520,7 +521,8 @@ static int make_crc_args(DevCtx *ctx, int checksum_type, const uint8_t *d_base, 
   a->nwin = static_cast<int64_t>((len + bpc - 1) / bpc);
   a->out = d_out;
   a->out_cell_stride = out_cell_stride;
-  a->tables = ctx->crc_tables[static_cast<int>(t)];
+  a->tables_b1 = ctx->crc_tables[static_cast<int>(t)][0];
+  a->tables_b4 = ctx->crc_tables[static_cast<int>(t)][1];
   a->init_full = cm.shift(0xffffffffu, bpc);
   a->init_last = cm.shift(0xffffffffu, len - (a->nwin ? (a->nwin - 1) * bpc : 0));
   a->big_endian = big_endian;
@@ -729,6 +731,17 @@ int ozec_parse_replication(const char *s, int *codec, int *k, int *p, int *chunk
   if (k) *k = static_cast<int>(d);
   if (p) *p = static_cast<int>(q);
   if (chunk) *chunk = static_cast<int>(static_cast<int32_t>(cs));
+  return OZEC_OK;
+}
+
+int ozec_set_tuning(const char *key, int64_t value) {
+  if (!key) return fail(OZEC_EINVAL, "null key");
+  const std::string k(key);
+  if (k == "grid") ozec::g_tune.grid = value;
+  else if (k == "gf_variant") ozec::g_tune.gf_variant = static_cast<int>(value);
+  else if (k == "crc_variant") ozec::g_tune.crc_variant = static_cast<int>(value);
+  else if (k == "crc_grid") ozec::g_tune.crc_grid = value;
+  else return fail(OZEC_EINVAL, "unknown tuning key " + k);
   return OZEC_OK;
 }
 

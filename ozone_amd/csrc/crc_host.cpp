@@ -37,18 +37,30 @@ CrcMath::CrcMath(uint32_t poly) {
   }
   for (int i = 1; i < 64; ++i) mat_square(op_[i - 1], op_[i]);
 
-  // device blob
-  blob_.assign(kCrcTableWords, 0);
-  // slice tables T_m[v] = shift(T0[v], m) for m = 0..15
-  for (int m = 0; m < 16; ++m)
-    for (int v = 0; v < 256; ++v) blob_[kCrcSliceOff + m * 256 + v] = shift(t0_[v], m);
-  // Z_n[j][v] = shift(v << 8j, n)
-  auto fill_z = [&](int off, uint64_t n) {
-    for (int j = 0; j < 4; ++j)
-      for (int v = 0; v < 256; ++v) blob_[off + j * 256 + v] = shift(static_cast<uint32_t>(v) << (8 * j), n);
+  blob_b1_ = build_blob(1);
+  blob_b4_ = build_blob(4);
+}
+
+std::vector<uint32_t> CrcMath::build_blob(int B) const {
+  std::vector<uint32_t> blob(kG5Words, 0);
+  // contribution of block bit p (byte p/8, bit p%8) to the raw CRC of a 16-B block processed from 0
+  uint32_t bit[128];
+  for (int p = 0; p < 128; ++p) bit[p] = shift(t0_[1u << (p & 7)], 15 - (p >> 3));
+  for (int g = 0; g < 26; ++g)
+    for (uint32_t v = 0; v < 32; ++v) {
+      uint32_t r = 0;
+      for (int t = 0; t < 5; ++t)
+        if (((v >> t) & 1) && 5 * g + t < 128) r ^= bit[5 * g + t];
+      blob[kG5Blk + g * 32 + v] = r;
+    }
+  auto fill_shift = [&](int off, uint64_t n) {
+    for (int g = 0; g < 7; ++g)
+      for (uint32_t v = 0; v < 32; ++v) blob[off + g * 32 + v] = shift(static_cast<uint32_t>(uint64_t{v} << (5 * g)), n);
   };
-  fill_z(kCrcZ1024Off, 1024);
-  for (int m = 1; m <= 5; ++m) fill_z(kCrcTreeOff + (m - 1) * 1024, 16ull << m);
+  fill_shift(kG5Step, static_cast<uint64_t>(63) * B * 16);
+  for (int m = 0; m < 6; ++m) fill_shift(kG5Tree + m * 224, static_cast<uint64_t>(16) * B << m);
+  for (int v = 0; v < 256; ++v) blob[kG5T0 + v] = t0_[v];
+  return blob;
 }
 
 uint32_t CrcMath::shift(uint32_t reg, uint64_t n) const {

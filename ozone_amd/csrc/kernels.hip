@@ -20,9 +20,14 @@
 //   tree then merges the 64 lane registers (shift by 16*2^m bytes at level m).  Windows whose length is
 //   not a multiple of 1 KiB are front-padded with virtual zero blocks (leading zeros do not change a raw
 //   CRC that starts from 0); the init value is added back as a precomputed shift(0xFFFFFFFF, N).
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace ozec {
+
+TuneKnobs g_tune;
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -141,7 +146,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
 // SREG: lo1/mid1/top are SGPR operands straight from the kernarg segment, lo0/mid0 live in VGPRs (loaded once
 // from LDS as single dwords); K*R <= 18.  Otherwise all five dwords are re-read from LDS for every unit
 // (uniform-address broadcasts), which keeps large schemas (rs-10-4 decode) inside 128 VGPRs.
-template <int K, int R, bool SREG>
+// VPT vectors of 16 B per lane per unit (a unit = VPT x 4 KiB of every cell of one stripe); LAUX/SAUX are the
+// cache-policy bits of the loads/stores (0 = default, 2 = nt).
+template <int K, int R, bool SREG, int VPT, int LAUX, int SAUX>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_WAVES, 8))) void gf_code_vec(
     const CodeArgs a, const TabArgs<K * R> tabs) {
   __shared__ __attribute__((aligned(16))) uint32_t s_w[5][K * R];
@@ -159,57 +166,68 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
   }
 
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
-  const uint32_t cpc = (nvec + kBlock - 1) / kBlock;  // 4 KiB chunks per unit
+  constexpr uint32_t kChunk = kBlock * VPT;
+  const uint32_t cpc = (nvec + kChunk - 1) / kChunk;  // units per cell
   const uint32_t units = static_cast<uint32_t>(a.nstripes) * cpc;
   for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
     if constexpr (!SREG) asm volatile("" ::: "memory");  // keep the LDS table reads inside the loop
     const uint32_t s = u / cpc;
-    const uint32_t v = (u - s * cpc) * kBlock + threadIdx.x;
+    const uint32_t v0 = (u - s * cpc) * kChunk + threadIdx.x;
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + static_cast<int64_t>(s) * a.in_stripe_stride);
     const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + static_cast<int64_t>(s) * a.out_stripe_stride);
-    if (v >= nvec) continue;
-    const uint32_t voff = v * 16u;
-    uint4 x[K];
+    uint4 x[VPT][K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, static_cast<int>(a.in_off[j]), 0);
-      x[j] = make_uint4(d[0], d[1], d[2], d[3]);
+    for (int q = 0; q < VPT; ++q) {
+      const uint32_t v = v0 + q * kBlock;
+      if (v < nvec) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, v * 16u, static_cast<int>(a.in_off[j]), LAUX);
+          x[q][j] = make_uint4(d[0], d[1], d[2], d[3]);
+        }
+      }
     }
-    uint4 acc[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+    for (int q = 0; q < VPT; ++q) {
+      const uint32_t v = v0 + q * kBlock;
+      if (v >= nvec) continue;
+      uint4 acc[R];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const Sel sx = make_sel(x[j].x), sy = make_sel(x[j].y), sz = make_sel(x[j].z), sw = make_sel(x[j].w);
+      for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const Sel sx = make_sel(x[q][j].x), sy = make_sel(x[q][j].y), sz = make_sel(x[q][j].z),
+                  sw = make_sel(x[q][j].w);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int t = r * K + j;
+          uint4 m;
+          if constexpr (SREG) {
+            const RegTab tb{vlo0[t], vmid0[t], tabs.w[t][1], tabs.w[t][3], tabs.w[t][4]};
+            m.x = gf_mul4_reg(tb, sx);
+            m.y = gf_mul4_reg(tb, sy);
+            m.z = gf_mul4_reg(tb, sz);
+            m.w = gf_mul4_reg(tb, sw);
+          } else {
+            const PermTab tb{s_w[0][t], s_w[1][t], s_w[2][t], s_w[3][t], s_w[4][t]};
+            m.x = gf_mul4_lds(tb, sx);
+            m.y = gf_mul4_lds(tb, sy);
+            m.z = gf_mul4_lds(tb, sz);
+            m.w = gf_mul4_lds(tb, sw);
+          }
+          acc[r].x ^= m.x;
+          acc[r].y ^= m.y;
+          acc[r].z ^= m.z;
+          acc[r].w ^= m.w;
+        }
+        // bound live ranges: input j's selectors (and, in LDS mode, its table reads) stay in this group
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int t = r * K + j;
-        uint4 m;
-        if constexpr (SREG) {
-          const RegTab tb{vlo0[t], vmid0[t], tabs.w[t][1], tabs.w[t][3], tabs.w[t][4]};
-          m.x = gf_mul4_reg(tb, sx);
-          m.y = gf_mul4_reg(tb, sy);
-          m.z = gf_mul4_reg(tb, sz);
-          m.w = gf_mul4_reg(tb, sw);
-        } else {
-          const PermTab tb{s_w[0][t], s_w[1][t], s_w[2][t], s_w[3][t], s_w[4][t]};
-          m.x = gf_mul4_lds(tb, sx);
-          m.y = gf_mul4_lds(tb, sy);
-          m.z = gf_mul4_lds(tb, sz);
-          m.w = gf_mul4_lds(tb, sw);
-        }
-        acc[r].x ^= m.x;
-        acc[r].y ^= m.y;
-        acc[r].z ^= m.z;
-        acc[r].w ^= m.w;
+        __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+        __builtin_amdgcn_raw_buffer_store_b128(d, rout, v * 16u, static_cast<int>(a.out_off[r]), SAUX);
       }
-      // bound live ranges: input j's selectors (and, in LDS mode, its table reads) stay in this group
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
-      __builtin_amdgcn_raw_buffer_store_b128(d, rout, voff, static_cast<int>(a.out_off[r]), 0);
     }
   }
 }
@@ -303,51 +321,55 @@ __global__ __launch_bounds__(kBlock) void gf_code_bytes(const CodeArgs a, int64_
 }
 
 // ------------------------------------------------------------------------------------------------
-// CRC helpers (tables in LDS, see CrcTables layout in kernels.hpp)
+// CRC helpers.  Every 32-bit-output linear map (block -> raw CRC, register shift by n bytes) is evaluated
+// as an XOR of lookups in 32-entry tables indexed by 5-bit groups of its input.  A 32-entry table aligned
+// to 128 B covers each of the 32 LDS banks exactly once, so a ds_read_b32 of 64 random lanes is
+// conflict-free (2 LDS cycles) -- with 256-entry byte tables random indices cost ~3.5x that in bank
+// conflicts, which is what bounded the first version.  Layout: kernels.hpp (kG5*).
 
-__device__ __forceinline__ uint32_t crc_f16(const uint32_t *T, const uint4 b) {
-  // byte i of the block (little-endian in b.x..b.w) contributes T_{15-i}[b_i]
-  uint32_t r0 = T[15 * 256 + (b.x & 0xff)] ^ T[14 * 256 + ((b.x >> 8) & 0xff)] ^
-                T[13 * 256 + ((b.x >> 16) & 0xff)] ^ T[12 * 256 + (b.x >> 24)];
-  uint32_t r1 = T[11 * 256 + (b.y & 0xff)] ^ T[10 * 256 + ((b.y >> 8) & 0xff)] ^
-                T[9 * 256 + ((b.y >> 16) & 0xff)] ^ T[8 * 256 + (b.y >> 24)];
-  uint32_t r2 = T[7 * 256 + (b.z & 0xff)] ^ T[6 * 256 + ((b.z >> 8) & 0xff)] ^
-                T[5 * 256 + ((b.z >> 16) & 0xff)] ^ T[4 * 256 + (b.z >> 24)];
-  uint32_t r3 = T[3 * 256 + (b.w & 0xff)] ^ T[2 * 256 + ((b.w >> 8) & 0xff)] ^
-                T[1 * 256 + ((b.w >> 16) & 0xff)] ^ T[0 * 256 + (b.w >> 24)];
-  return r0 ^ r1 ^ r2 ^ r3;
+__device__ __forceinline__ uint32_t g5_idx(uint32_t v) { return v & 31u; }
+
+// raw CRC of one 16-B block (26 groups of 5 bits; group 25 holds bits 125..127)
+__device__ __forceinline__ uint32_t g5_block(const uint32_t *T, const uint4 b) {
+  const uint32_t w[4] = {b.x, b.y, b.z, b.w};
+  uint32_t t[26];
+#pragma unroll
+  for (int g = 0; g < 26; ++g) {
+    const int o = 5 * g, d = o >> 5, sh = o & 31;
+    const uint32_t v = (sh <= 27 || d == 3) ? (w[d] >> sh) : __builtin_amdgcn_alignbit(w[d + 1], w[d], sh);
+    t[g] = T[kG5Blk + g * 32 + g5_idx(v)];
+  }
+  uint32_t r = xor3(t[0], t[1], t[2]);
+#pragma unroll
+  for (int g = 3; g + 1 < 26; g += 2) r = xor3(r, t[g], t[g + 1]);
+  return r ^ t[25];
 }
 
-// shift a raw register by the byte distance Z encodes: Z is 4 x 256 (one table per register byte)
-__device__ __forceinline__ uint32_t crc_shift(const uint32_t *Z, uint32_t s) {
-  return Z[s & 0xff] ^ Z[256 + ((s >> 8) & 0xff)] ^ Z[512 + ((s >> 16) & 0xff)] ^ Z[768 + (s >> 24)];
+// register shift by the byte distance the 7 x 32 table block at T encodes
+__device__ __forceinline__ uint32_t g5_shift(const uint32_t *T, uint32_t s) {
+  uint32_t t[7];
+#pragma unroll
+  for (int g = 0; g < 7; ++g) t[g] = T[g * 32 + g5_idx(s >> (5 * g))];
+  return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6]);
 }
 
-// level 0 (16 B) of the lane tree uses the slice tables T_15..T_12
-__device__ __forceinline__ uint32_t crc_shift16(const uint32_t *T, uint32_t s) {
-  return T[15 * 256 + (s & 0xff)] ^ T[14 * 256 + ((s >> 8) & 0xff)] ^ T[13 * 256 + ((s >> 16) & 0xff)] ^
-         T[12 * 256 + (s >> 24)];
-}
-
-// merge the 64 lane registers of a wave into the register of the whole window (every lane gets it)
-__device__ __forceinline__ uint32_t crc_lane_tree(const uint32_t *tabs, uint32_t v, int lane) {
+// merge the 64 lane registers of a wave (lane l's chunk precedes lane l+1's) -> every lane gets the total
+__device__ __forceinline__ uint32_t g5_lane_tree(const uint32_t *T, uint32_t v, int lane) {
 #pragma unroll
   for (int m = 0; m < 6; ++m) {
     const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), 1 << m, 64));
     const bool upper = (lane >> m) & 1;
     const uint32_t lower = upper ? other : v;
     const uint32_t hi = upper ? v : other;
-    const uint32_t shifted =
-        m == 0 ? crc_shift16(tabs + kCrcSliceOff, lower) : crc_shift(tabs + kCrcTreeOff + (m - 1) * 1024, lower);
-    v = shifted ^ hi;
+    v = g5_shift(T + kG5Tree + m * 224, lower) ^ hi;
   }
   return v;
 }
 
-__device__ __forceinline__ void load_crc_tables(uint32_t *s_crc, const uint32_t *g) {
+__device__ __forceinline__ void load_tables(uint32_t *s_t, const uint32_t *g, int words) {
   const uint4 *src = reinterpret_cast<const uint4 *>(g);
-  uint4 *dst = reinterpret_cast<uint4 *>(s_crc);
-  for (int i = threadIdx.x; i < kCrcTableWords / 4; i += blockDim.x) dst[i] = src[i];
+  uint4 *dst = reinterpret_cast<uint4 *>(s_t);
+  for (int i = threadIdx.x; i < words / 4; i += blockDim.x) dst[i] = src[i];
 }
 
 __device__ __forceinline__ uint32_t crc_finish(uint32_t raw, uint32_t init, int raw_out, int big_endian) {
@@ -355,11 +377,14 @@ __device__ __forceinline__ uint32_t crc_finish(uint32_t raw, uint32_t init, int 
   return big_endian ? __builtin_bswap32(v) : v;
 }
 
-// One wave per (cell, window). Requires 16-B aligned cells and bpc % 16 == 0; any len.
-constexpr int kCrcUnroll = 4;
+// One wave per (cell, window).  Lane l owns B consecutive 16-B blocks of every 64*B-block step and folds them
+// into its register (state XORed into the next block's first 4 bytes); between steps the register jumps
+// (63*B)*16 bytes.  Windows are front-padded with virtual zero blocks to a whole number of steps.
+// Requires 16-B aligned cells and bpc % 16 == 0 (the tail of a short last window goes byte-by-byte).
+template <int B>
 __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_crc[kCrcTableWords];
-  load_crc_tables(s_crc, a.tables);
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[kG5Words];
+  load_tables(s_t, B == 1 ? a.tables_b1 : a.tables_b4, kG5Words);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -371,25 +396,38 @@ __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
     const bool last = w == a.nwin - 1;
     const int64_t N = last ? a.len - w * a.bpc : a.bpc;
     const int64_t m = N >> 4;
-    const int64_t T = (m + 63) >> 6;
-    const int64_t P = T * 64 - m;  // virtual zero blocks in front
+    const int64_t T = (m + 64 * B - 1) / (64 * B);
+    const int64_t P = T * 64 * B - m;  // virtual zero blocks in front
     const uint8_t *win = a.base + c * a.cell_stride + w * a.bpc;
     uint32_t S = 0;
-    for (int64_t t0 = 0; t0 < T; t0 += kCrcUnroll) {
-      uint4 blk[kCrcUnroll];
+    uint4 cur[B], nxt[B];
+    auto load_step = [&](int64_t t, uint4 (&dst)[B]) {
 #pragma unroll
-      for (int q = 0; q < kCrcUnroll; ++q) {
-        const int64_t vb = (t0 + q) * 64 + lane - P;
-        blk[q] = make_uint4(0, 0, 0, 0);
-        if (t0 + q < T && vb >= 0) blk[q] = *reinterpret_cast<const uint4 *>(win + vb * 16);
+      for (int q = 0; q < B; ++q) {
+        const int64_t vb = t * 64 * B + lane * B + q - P;
+        dst[q] = make_uint4(0, 0, 0, 0);
+        if (t < T && vb >= 0) {
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(win + vb * 16));
+          dst[q] = make_uint4(d[0], d[1], d[2], d[3]);
+        }
+      }
+    };
+    load_step(0, cur);
+    for (int64_t t = 0; t < T; ++t) {
+      load_step(t + 1, nxt);
+      if (t > 0) S = g5_shift(s_t + kG5Step, S);
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        uint4 b = cur[q];
+        b.x ^= S;
+        S = g5_block(s_t, b);
       }
 #pragma unroll
-      for (int q = 0; q < kCrcUnroll; ++q) {
-        if (t0 + q < T) S = crc_shift(s_crc + kCrcZ1024Off, S) ^ crc_f16(s_crc, blk[q]);
-      }
+      for (int q = 0; q < B; ++q) cur[q] = nxt[q];
     }
-    S = crc_lane_tree(s_crc, S, lane);
-    for (int64_t i = m * 16; i < N; ++i) S = (S >> 8) ^ s_crc[(S ^ win[i]) & 0xff];
+    S = g5_lane_tree(s_t, S, lane);
+    for (int64_t i = m * 16; i < N; ++i) S = (S >> 8) ^ s_t[kG5T0 + ((S ^ win[i]) & 0xff)];
     if (lane == 0) a.out[c * a.out_cell_stride + w] = crc_finish(S, last ? a.init_last : a.init_full, a.raw, a.big_endian);
   }
 }
@@ -397,7 +435,7 @@ __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
 // Scalar fallback: one thread per window, byte-at-a-time (any alignment, any bpc).
 __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
   __shared__ uint32_t s_t0[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_t0[i] = a.tables[i];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_t0[i] = a.tables_b1[kG5T0 + i];
   __syncthreads();
   const int64_t units = a.ncells * a.nwin;
   for (int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; u < units;
@@ -414,22 +452,28 @@ __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Fused encode + CRC: one wave per (stripe, window); lanes walk the window 1 KiB at a time, producing
-// parity and folding all K+R units into their CRC registers while the bytes are in VGPRs.
-template <int K, int R>
-__global__ __launch_bounds__(kBlock) void encode_crc_vec(const EncCrcArgs e) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_crc[kCrcTableWords];
-  __shared__ PermTab s_tab[K * R];
+// Fused encode + CRC: one wave per (stripe, window); lanes walk the window 1 KiB at a time (B = 1 block per
+// lane per step), produce parity and fold all K+R units into their CRC registers while the bytes are in
+// VGPRs.  Coefficient tables as in gf_code_vec (SGPR/VGPR split when K*R <= 18, else LDS).
+template <int K, int R, bool SREG>
+__global__ __launch_bounds__(kBlock) void encode_crc_vec(const EncCrcArgs e, const TabArgs<K * R> tabs) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[kG5Words];
+  __shared__ __attribute__((aligned(16))) uint32_t s_w[5][K * R];
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
-  load_crc_tables(s_crc, cr.tables);
-  build_tabs(s_tab, a, R, K);
+  load_tables(s_t, cr.tables_b1, kG5Words);
+  for (int t = threadIdx.x; t < K * R; t += blockDim.x)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) s_w[q][t] = tabs.w[t][q];
   __syncthreads();
-  PermTab tab[R][K];
+  uint32_t vlo0[SREG ? K * R : 1], vmid0[SREG ? K * R : 1];
+  if constexpr (SREG) {
 #pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int j = 0; j < K; ++j) tab[r][j] = s_tab[r * K + j];
+    for (int t = 0; t < K * R; ++t) {
+      vlo0[t] = s_w[0][t];
+      vmid0[t] = s_w[2][t];
+    }
+  }
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -444,48 +488,80 @@ __global__ __launch_bounds__(kBlock) void encode_crc_vec(const EncCrcArgs e) {
     const int64_t m = N >> 4;
     const int64_t T = (m + 63) >> 6;
     const int64_t P = T * 64 - m;
-    const uint8_t *ib = a.in + s * a.in_stripe_stride + w * cr.bpc;
-    uint8_t *ob = a.out + s * a.out_stripe_stride + w * cr.bpc;
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + s * a.in_stripe_stride + w * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + s * a.out_stripe_stride + w * cr.bpc);
     uint32_t S[K + R];
 #pragma unroll
     for (int q = 0; q < K + R; ++q) S[q] = 0;
     for (int64_t t = 0; t < T; ++t) {
+      if constexpr (!SREG) asm volatile("" ::: "memory");
       const int64_t vb = t * 64 + lane - P;
+      const uint32_t voff = static_cast<uint32_t>(vb) * 16u;
       uint4 x[K];
       uint4 acc[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
       if (vb >= 0) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = *reinterpret_cast<const uint4 *>(ib + a.in_off[j] + vb * 16);
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+        for (int j = 0; j < K; ++j) {
+          const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, static_cast<int>(a.in_off[j]), 2);
+          x[j] = make_uint4(d[0], d[1], d[2], d[3]);
+        }
 #pragma unroll
         for (int j = 0; j < K; ++j) {
           const Sel sx = make_sel(x[j].x), sy = make_sel(x[j].y), sz = make_sel(x[j].z), sw = make_sel(x[j].w);
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            acc[r].x ^= gf_mul4(tab[r][j], sx);
-            acc[r].y ^= gf_mul4(tab[r][j], sy);
-            acc[r].z ^= gf_mul4(tab[r][j], sz);
-            acc[r].w ^= gf_mul4(tab[r][j], sw);
+            const int tt = r * K + j;
+            uint4 mm;
+            if constexpr (SREG) {
+              const RegTab tb{vlo0[tt], vmid0[tt], tabs.w[tt][1], tabs.w[tt][3], tabs.w[tt][4]};
+              mm.x = gf_mul4_reg(tb, sx);
+              mm.y = gf_mul4_reg(tb, sy);
+              mm.z = gf_mul4_reg(tb, sz);
+              mm.w = gf_mul4_reg(tb, sw);
+            } else {
+              const PermTab tb{s_w[0][tt], s_w[1][tt], s_w[2][tt], s_w[3][tt], s_w[4][tt]};
+              mm.x = gf_mul4_lds(tb, sx);
+              mm.y = gf_mul4_lds(tb, sy);
+              mm.z = gf_mul4_lds(tb, sz);
+              mm.w = gf_mul4_lds(tb, sw);
+            }
+            acc[r].x ^= mm.x;
+            acc[r].y ^= mm.y;
+            acc[r].z ^= mm.z;
+            acc[r].w ^= mm.w;
           }
         }
 #pragma unroll
-        for (int r = 0; r < R; ++r) *reinterpret_cast<uint4 *>(ob + a.out_off[r] + vb * 16) = acc[r];
+        for (int r = 0; r < R; ++r) {
+          __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+          __builtin_amdgcn_raw_buffer_store_b128(d, rout, voff, static_cast<int>(a.out_off[r]), 2);
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < K; ++j) x[j] = make_uint4(0, 0, 0, 0);
+      }
+      // CRC: S = G(block ^ shift_1008(S)) for every data and parity unit
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+      for (int j = 0; j < K; ++j) {
+        uint4 b = x[j];
+        b.x ^= t > 0 ? g5_shift(s_t + kG5Step, S[j]) : 0u;
+        S[j] = g5_block(s_t, b);
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int j = 0; j < K; ++j) S[j] = crc_shift(s_crc + kCrcZ1024Off, S[j]) ^ crc_f16(s_crc, x[j]);
-#pragma unroll
-      for (int r = 0; r < R; ++r) S[K + r] = crc_shift(s_crc + kCrcZ1024Off, S[K + r]) ^ crc_f16(s_crc, acc[r]);
+      for (int r = 0; r < R; ++r) {
+        uint4 b = acc[r];
+        b.x ^= t > 0 ? g5_shift(s_t + kG5Step, S[K + r]) : 0u;
+        S[K + r] = g5_block(s_t, b);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     const uint32_t init = last ? cr.init_last : cr.init_full;
 #pragma unroll
     for (int q = 0; q < K + R; ++q) {
-      const uint32_t v = crc_lane_tree(s_crc, S[q], lane);
+      const uint32_t v = g5_lane_tree(s_t, S[q], lane);
       if (lane == q) cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
     }
   }
@@ -589,14 +665,37 @@ bool rebase32(CodeArgs &a) {
   return true;
 }
 
-template <int K, int R>
-hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
+template <int K, int R, int VPT, int LAUX, int SAUX>
+hipError_t launch_krv(const CodeArgs &a, hipStream_t st, int64_t default_grid) {
   constexpr bool kSreg = K * R <= 18;
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
-  const int64_t units = a.nstripes * ((nvec + kBlock - 1) / kBlock);
+  const int64_t units = a.nstripes * ((nvec + kBlock * VPT - 1) / (kBlock * VPT));
   const TabArgs<K * R> tabs = host_tabs<K * R>(a);
-  hipLaunchKernelGGL((gf_code_vec<K, R, kSreg>), dim3(grid_for(units, 1)), dim3(kBlock), 0, st, a, tabs);
+  int64_t grid = g_tune.grid > 0 ? g_tune.grid : default_grid;
+  grid = std::max<int64_t>(1, std::min<int64_t>(grid, units));
+  hipLaunchKernelGGL((gf_code_vec<K, R, kSreg, VPT, LAUX, SAUX>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0,
+                     st, a, tabs);
   return hipGetLastError();
+}
+
+// Defaults measured on MI355X (scripts/tune.py, profiles/r01/tune_*.log): register-table kernels run best as
+// one 4 KiB chunk per block (a non-persistent grid keeps the in-flight chunks contiguous in HBM) with
+// non-temporal loads and stores; LDS-table kernels (K*R > 18) prefer 2 chunks per lane and a 8192-block
+// grid.  ozec_set_tuning("gf_variant", 1..6) pins one (VPT, load policy, store policy) combination.
+template <int K, int R>
+hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
+  constexpr int64_t kAll = int64_t{1} << 40;
+  switch (g_tune.gf_variant) {
+    case 1: return launch_krv<K, R, 1, 0, 0>(a, st, kAll);
+    case 2: return launch_krv<K, R, 1, 2, 0>(a, st, kAll);
+    case 3: return launch_krv<K, R, 1, 0, 2>(a, st, kAll);
+    case 4: return launch_krv<K, R, 1, 2, 2>(a, st, kAll);
+    case 5: return launch_krv<K, R, 2, 0, 0>(a, st, 8192);
+    case 6: return launch_krv<K, R, 2, 2, 2>(a, st, 8192);
+    default: break;
+  }
+  if constexpr (K * R <= 18) return launch_krv<K, R, 1, 2, 2>(a, st, kAll);
+  else return launch_krv<K, R, 2, 2, 2>(a, st, 8192);
 }
 
 template <int K>
@@ -667,7 +766,11 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
   const bool vec = aligned16(reinterpret_cast<intptr_t>(a.base)) && (a.ncells == 1 || aligned16(a.cell_stride)) &&
                    aligned16(a.bpc);
   if (vec) {
-    hipLaunchKernelGGL(crc_windows_vec, dim3(grid_for(units, kBlock / 64)), dim3(kBlock), 0, st, a);
+    // defaults measured on MI355X: B = 1 (fully coalesced loads), 16384 blocks
+    const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : 16384;
+    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
+    if (g_tune.crc_variant == 4) hipLaunchKernelGGL(crc_windows_vec<4>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(crc_windows_vec<1>, grid, block, 0, st, a);
   } else {
     hipLaunchKernelGGL(crc_windows_bytes, dim3(grid_for(units, kBlock)), dim3(kBlock), 0, st, a);
   }
@@ -680,22 +783,31 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
   return kr && bpc > 0 && aligned16(bpc) && aligned16(a.len) && vec_ok(a);
 }
 
-hipError_t launch_encode_crc(const EncCrcArgs &e, hipStream_t st) {
+template <int K, int R>
+hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
   const int64_t units = e.code.nstripes * e.crc.nwin;
-  if (units <= 0) return hipSuccess;
-  const dim3 grid(grid_for(units, kBlock / 64)), block(kBlock);
-  if (e.code.k == 6 && e.code.rows == 3) {
-    hipLaunchKernelGGL((encode_crc_vec<6, 3>), grid, block, 0, st, e);
-  } else if (e.code.k == 3 && e.code.rows == 2) {
-    hipLaunchKernelGGL((encode_crc_vec<3, 2>), grid, block, 0, st, e);
-  } else if (e.code.k == 10 && e.code.rows == 4) {
-    hipLaunchKernelGGL((encode_crc_vec<10, 4>), grid, block, 0, st, e);
-  } else if (e.code.k == 2 && e.code.rows == 1) {
-    hipLaunchKernelGGL((encode_crc_vec<2, 1>), grid, block, 0, st, e);
+  const TabArgs<K * R> tabs = host_tabs<K * R>(e.code);
+  // defaults measured on MI355X: one wave per window with no grid-stride, LDS coefficient tables
+  const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : (units + 3) / 4;
+  const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
+  if (K * R <= 18 && g_tune.crc_variant == 3) {
+    hipLaunchKernelGGL((encode_crc_vec<K, R, (K * R <= 18)>), grid, block, 0, st, e, tabs);
   } else {
-    return hipErrorInvalidValue;
+    hipLaunchKernelGGL((encode_crc_vec<K, R, false>), grid, block, 0, st, e, tabs);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
+  if (e0.code.nstripes * e0.crc.nwin <= 0) return hipSuccess;
+  EncCrcArgs e = e0;
+  if (!rebase32(e.code)) return hipErrorInvalidValue;
+  const int k = e.code.k, r = e.code.rows;
+  if (k == 6 && r == 3) return launch_enc_crc_kr<6, 3>(e, st);
+  if (k == 3 && r == 2) return launch_enc_crc_kr<3, 2>(e, st);
+  if (k == 10 && r == 4) return launch_enc_crc_kr<10, 4>(e, st);
+  if (k == 2 && r == 1) return launch_enc_crc_kr<2, 1>(e, st);
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t ncells, int64_t n, uint64_t seed,

@@ -38,7 +38,8 @@ struct CrcArgs {
   int64_t nwin;            // ceil(len / bpc)
   uint32_t *out;           // out[c * out_cell_stride + w]
   int64_t out_cell_stride; // in uint32 elements
-  const uint32_t *tables;  // device CRC tables for this type (CrcTables layout)
+  const uint32_t *tables_b1;  // device G5 table blob for this CRC type, B = 1 block per lane per step
+  const uint32_t *tables_b4;  // ... B = 4
   uint32_t init_full;      // shift(0xFFFFFFFF, bpc bytes)
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
@@ -51,14 +52,27 @@ struct EncCrcArgs {
   CrcArgs crc;  // crc.base unused; crc.out = crcs[s][unit][w] with crc.out_cell_stride = nwin
 };
 
-// Device CRC table blob layout (uint32 entries), built on the host (crc_host.cpp):
-//   [0, 4096)        slice tables T_0..T_15: T_m[v] = register after byte v then m zero bytes
-//   [4096, 5120)     Z_1024: shift by 1024 bytes, 4 x 256 (one table per register byte)
-//   [5120, 10240)    Z_32, Z_64, Z_128, Z_256, Z_512 (lane-combine tree levels 1..5; level 0 = T_15..T_12)
-constexpr int kCrcSliceOff = 0;
-constexpr int kCrcZ1024Off = 4096;
-constexpr int kCrcTreeOff = 5120;
-constexpr int kCrcTableWords = 10240;
+// Device CRC "G5" table blob (uint32 entries), built on the host (crc_host.cpp), one per (CRC type, B) where
+// B = 16-B blocks a lane folds per step.  Every table has 32 entries indexed by a 5-bit group of its input
+// and starts on a 128-B boundary, so a ds_read_b32 of random indices is bank-conflict-free.
+//   [kG5Blk,  +26*32)   block -> raw CRC: table g holds the contribution of block bits [5g, 5g+5)
+//   [kG5Step, +7*32)    register shift by (63*B)*16 bytes (jump to the lane's next chunk)
+//   [kG5Tree, +6*7*32)  register shift by 16*B*2^m bytes, m = 0..5 (lane-combine tree)
+//   [kG5T0,   +256)     classic byte table T0 (tails of windows not a multiple of 16 B)
+constexpr int kG5Blk = 0;
+constexpr int kG5Step = 832;
+constexpr int kG5Tree = 1056;
+constexpr int kG5T0 = 2400;
+constexpr int kG5Words = 2656;
+
+// Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.
+struct TuneKnobs {
+  int64_t grid = 0;       // blocks for the coding kernels
+  int gf_variant = 0;     // coding-kernel variant 1..6 (VPT / cache policy), see launch_kr
+  int crc_variant = 0;    // 4: CRC kernel with B = 4; 3: fused kernel with SGPR coefficient tables
+  int64_t crc_grid = 0;   // blocks for the CRC / fused kernels
+};
+extern TuneKnobs g_tune;
 
 hipError_t launch_code(const CodeArgs &a, hipStream_t stream);
 hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t stream);

@@ -1,0 +1,79 @@
+"""world_size-2 gloo run of the multi-GPU path's host logic on CPU: each rank takes its stripe range, encodes it
+(oracle stands in for the GPU here), the union of the shards equals the single-process encode, and the
+max-over-ranks reduction bench.py uses picks the slowest rank."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ozone_amd.shard import max_over_ranks, stripe_range
+
+
+def test_stripe_range_partitions():
+    for S in (1, 7, 4096, 8192, 8191):
+        for G in (1, 2, 3, 4, 8):
+            ranges = [stripe_range(S, g, G) for g in range(G)]
+            covered = [i for lo, hi in ranges for i in range(lo, hi)]
+            assert covered == list(range(S))
+            assert max(hi - lo for lo, hi in ranges) - min(hi - lo for lo, hi in ranges) <= (S + G - 1) // G
+    with pytest.raises(ValueError):
+        stripe_range(10, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, S, k, p, n, q):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import oracle
+    from synth import SEED, cells
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = stripe_range(S, rank, world)
+    digests = {}
+    for s in range(lo, hi):
+        par = oracle.rs_encode(k, p, cells(SEED, s * k, k, n))
+        digests[s] = int(np.bitwise_xor.reduce(np.concatenate(par).view(np.uint64)))
+    gathered = [None] * world
+    dist.all_gather_object(gathered, digests)
+    slowest = max_over_ranks(1.0 + rank, dist)
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank == 0:
+        q.put((gathered, slowest))
+
+
+def test_two_rank_gloo_sharded_encode():
+    S, k, p, n, world = 6, 6, 3, 4096, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, S, k, p, n, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    gathered, slowest = q.get(timeout=120)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    import oracle
+    from synth import SEED, cells
+    merged = {}
+    for d in gathered:
+        assert not set(d) & set(merged)  # disjoint shards
+        merged.update(d)
+    assert sorted(merged) == list(range(S))
+    for s in range(S):
+        par = oracle.rs_encode(k, p, cells(SEED, s * k, k, n))
+        assert merged[s] == int(np.bitwise_xor.reduce(np.concatenate(par).view(np.uint64)))
+    assert slowest == 2.0

@@ -52,7 +52,7 @@ struct DevCtx {
   size_t pinned_cap = 0;
   uint8_t *dbuf = nullptr;
   size_t dbuf_cap = 0;
-  uint32_t *crc_tables[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [type][B == 4]
+  uint32_t *crc_tables[2][3] = {};  // [type][B = 1, 2, 4]
 
   int reserve(size_t bytes) {
     if (bytes > pinned_cap) {
@@ -91,8 +91,8 @@ int get_ctx(DevCtx **out) {
     c->device = dev;
     OZEC_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int t = 0; t < 2; ++t)
-      for (int b = 0; b < 2; ++b) {
-        const auto &blob = CrcMath::get(static_cast<CrcType>(t)).device_tables(b ? 4 : 1);
+      for (int b = 0; b < 3; ++b) {
+        const auto &blob = CrcMath::get(static_cast<CrcType>(t)).device_tables(1 << b);
         OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->crc_tables[t][b]), blob.size() * sizeof(uint32_t)));
         OZEC_HIP(hipMemcpy(c->crc_tables[t][b], blob.data(), blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
       }
@@ -521,8 +521,7 @@ static int make_crc_args(DevCtx *ctx, int checksum_type, const uint8_t *d_base, 
   a->nwin = static_cast<int64_t>((len + bpc - 1) / bpc);
   a->out = d_out;
   a->out_cell_stride = out_cell_stride;
-  a->tables_b1 = ctx->crc_tables[static_cast<int>(t)][0];
-  a->tables_b4 = ctx->crc_tables[static_cast<int>(t)][1];
+  for (int b = 0; b < 3; ++b) a->tables[b] = ctx->crc_tables[static_cast<int>(t)][b];
   a->init_full = cm.shift(0xffffffffu, bpc);
   a->init_last = cm.shift(0xffffffffu, len - (a->nwin ? (a->nwin - 1) * bpc : 0));
   a->big_endian = big_endian;

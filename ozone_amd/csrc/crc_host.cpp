@@ -38,6 +38,7 @@ CrcMath::CrcMath(uint32_t poly) {
   for (int i = 1; i < 64; ++i) mat_square(op_[i - 1], op_[i]);
 
   blob_b1_ = build_blob(1);
+  blob_b2_ = build_blob(2);
   blob_b4_ = build_blob(4);
 }
 

@@ -384,7 +384,7 @@ __device__ __forceinline__ uint32_t crc_finish(uint32_t raw, uint32_t init, int 
 template <int B>
 __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_t[kG5Words];
-  load_tables(s_t, B == 1 ? a.tables_b1 : a.tables_b4, kG5Words);
+  load_tables(s_t, a.tables[g5_slot(B)], kG5Words);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
 // Scalar fallback: one thread per window, byte-at-a-time (any alignment, any bpc).
 __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
   __shared__ uint32_t s_t0[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_t0[i] = a.tables_b1[kG5T0 + i];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_t0[i] = a.tables[0][kG5T0 + i];
   __syncthreads();
   const int64_t units = a.ncells * a.nwin;
   for (int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; u < units;
@@ -452,16 +452,18 @@ __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Fused encode + CRC: one wave per (stripe, window); lanes walk the window 1 KiB at a time (B = 1 block per
-// lane per step), produce parity and fold all K+R units into their CRC registers while the bytes are in
-// VGPRs.  Coefficient tables as in gf_code_vec (SGPR/VGPR split when K*R <= 18, else LDS).
-template <int K, int R, bool SREG>
-__global__ __launch_bounds__(kBlock) void encode_crc_vec(const EncCrcArgs e, const TabArgs<K * R> tabs) {
+// Fused encode + CRC: one wave per (stripe, window); each step a lane takes B consecutive 16-B blocks of
+// every data unit (lanes interleaved, 64*B blocks per step), produces the parity blocks and folds all K+R
+// units into their CRC registers while the bytes are in VGPRs.  PF: issue the next step's loads before
+// computing the current one.  Coefficient tables as in gf_code_vec (SREG: SGPR/VGPR split, else LDS).
+template <int K, int R, bool SREG, int B, bool PF, int WAVES = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_vec(
+    const EncCrcArgs e, const TabArgs<K * R> tabs) {
   __shared__ __attribute__((aligned(16))) uint32_t s_t[kG5Words];
   __shared__ __attribute__((aligned(16))) uint32_t s_w[5][K * R];
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
-  load_tables(s_t, cr.tables_b1, kG5Words);
+  load_tables(s_t, cr.tables[g5_slot(B)], kG5Words);
   for (int t = threadIdx.x; t < K * R; t += blockDim.x)
 #pragma unroll
     for (int q = 0; q < 5; ++q) s_w[q][t] = tabs.w[t][q];
@@ -486,30 +488,48 @@ __global__ __launch_bounds__(kBlock) void encode_crc_vec(const EncCrcArgs e, con
     const bool last = w == nwin - 1;
     const int64_t N = last ? a.len - w * cr.bpc : cr.bpc;
     const int64_t m = N >> 4;
-    const int64_t T = (m + 63) >> 6;
-    const int64_t P = T * 64 - m;
+    const int64_t T = (m + 64 * B - 1) / (64 * B);
+    const int64_t P = T * 64 * B - m;
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + s * a.in_stripe_stride + w * cr.bpc);
     const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + s * a.out_stripe_stride + w * cr.bpc);
     uint32_t S[K + R];
 #pragma unroll
     for (int q = 0; q < K + R; ++q) S[q] = 0;
+    uint4 x[B][K], xn[PF ? B : 1][K];
+    auto load = [&](int64_t t, uint4 (&dst)[B][K]) {
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        const int64_t vb = t * 64 * B + lane * B + q - P;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          if (t < T && vb >= 0) {
+            const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<uint32_t>(vb) * 16u,
+                                                                 static_cast<int>(a.in_off[j]), 2);
+            dst[q][j] = make_uint4(d[0], d[1], d[2], d[3]);
+          } else {
+            dst[q][j] = make_uint4(0, 0, 0, 0);
+          }
+        }
+      }
+    };
+    if constexpr (PF) load(0, x);
     for (int64_t t = 0; t < T; ++t) {
       if constexpr (!SREG) asm volatile("" ::: "memory");
-      const int64_t vb = t * 64 + lane - P;
-      const uint32_t voff = static_cast<uint32_t>(vb) * 16u;
-      uint4 x[K];
-      uint4 acc[R];
+      if constexpr (PF) {
+        load(t + 1, xn);
+      } else {
+        load(t, x);
+      }
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
-      if (vb >= 0) {
+      for (int q = 0; q < B; ++q) {
+        const int64_t vb = t * 64 * B + lane * B + q - P;
+        uint4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, static_cast<int>(a.in_off[j]), 2);
-          x[j] = make_uint4(d[0], d[1], d[2], d[3]);
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const Sel sx = make_sel(x[j].x), sy = make_sel(x[j].y), sz = make_sel(x[j].z), sw = make_sel(x[j].w);
+          const Sel sx = make_sel(x[q][j].x), sy = make_sel(x[q][j].y), sz = make_sel(x[q][j].z),
+                    sw = make_sel(x[q][j].w);
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             const int tt = r * K + j;
@@ -533,29 +553,29 @@ __global__ __launch_bounds__(kBlock) void encode_crc_vec(const EncCrcArgs e, con
             acc[r].w ^= mm.w;
           }
         }
+        if (vb >= 0) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
-          __builtin_amdgcn_raw_buffer_store_b128(d, rout, voff, static_cast<int>(a.out_off[r]), 2);
+          for (int r = 0; r < R; ++r) {
+            __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+            __builtin_amdgcn_raw_buffer_store_b128(d, rout, static_cast<uint32_t>(vb) * 16u,
+                                                   static_cast<int>(a.out_off[r]), 2);
+          }
         }
-      } else {
+        // CRC: the first block of a step jumps the register (63*B)*16 bytes, then every block folds in
 #pragma unroll
-        for (int j = 0; j < K; ++j) x[j] = make_uint4(0, 0, 0, 0);
+        for (int j = 0; j < K + R; ++j) {
+          uint4 b = j < K ? x[q][j] : acc[j - K];
+          if (q == 0) b.x ^= t > 0 ? g5_shift(s_t + kG5Step, S[j]) : 0u;
+          else b.x ^= S[j];
+          S[j] = g5_block(s_t, b);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-      // CRC: S = G(block ^ shift_1008(S)) for every data and parity unit
+      if constexpr (PF) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        uint4 b = x[j];
-        b.x ^= t > 0 ? g5_shift(s_t + kG5Step, S[j]) : 0u;
-        S[j] = g5_block(s_t, b);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+        for (int q = 0; q < B; ++q)
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        uint4 b = acc[r];
-        b.x ^= t > 0 ? g5_shift(s_t + kG5Step, S[K + r]) : 0u;
-        S[K + r] = g5_block(s_t, b);
-        __builtin_amdgcn_sched_barrier(0);
+          for (int j = 0; j < K; ++j) x[q][j] = xn[q][j];
       }
     }
     const uint32_t init = last ? cr.init_last : cr.init_full;
@@ -766,11 +786,12 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
   const bool vec = aligned16(reinterpret_cast<intptr_t>(a.base)) && (a.ncells == 1 || aligned16(a.cell_stride)) &&
                    aligned16(a.bpc);
   if (vec) {
-    // defaults measured on MI355X: B = 1 (fully coalesced loads), 16384 blocks
+    // defaults measured on MI355X: B = 2 (32-B lane chunks), 16384 blocks
     const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : 16384;
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
     if (g_tune.crc_variant == 4) hipLaunchKernelGGL(crc_windows_vec<4>, grid, block, 0, st, a);
-    else hipLaunchKernelGGL(crc_windows_vec<1>, grid, block, 0, st, a);
+    else if (g_tune.crc_variant == 1) hipLaunchKernelGGL(crc_windows_vec<1>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(crc_windows_vec<2>, grid, block, 0, st, a);
   } else {
     hipLaunchKernelGGL(crc_windows_bytes, dim3(grid_for(units, kBlock)), dim3(kBlock), 0, st, a);
   }
@@ -790,10 +811,16 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
   // defaults measured on MI355X: one wave per window with no grid-stride, LDS coefficient tables
   const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : (units + 3) / 4;
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
-  if (K * R <= 18 && g_tune.crc_variant == 3) {
-    hipLaunchKernelGGL((encode_crc_vec<K, R, (K * R <= 18)>), grid, block, 0, st, e, tabs);
-  } else {
-    hipLaunchKernelGGL((encode_crc_vec<K, R, false>), grid, block, 0, st, e, tabs);
+  constexpr bool kS = K * R <= 18;
+  switch (g_tune.crc_variant) {
+    case 3: hipLaunchKernelGGL((encode_crc_vec<K, R, kS, 1, false>), grid, block, 0, st, e, tabs); break;
+    case 5: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, true>), grid, block, 0, st, e, tabs); break;
+    case 6: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 2, false>), grid, block, 0, st, e, tabs); break;
+    case 7: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 2, true>), grid, block, 0, st, e, tabs); break;
+    case 8: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 5>), grid, block, 0, st, e, tabs); break;
+    case 9: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 6>), grid, block, 0, st, e, tabs); break;
+    case 10: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 8>), grid, block, 0, st, e, tabs); break;
+    default: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs); break;
   }
   return hipGetLastError();
 }

@@ -38,8 +38,7 @@ struct CrcArgs {
   int64_t nwin;            // ceil(len / bpc)
   uint32_t *out;           // out[c * out_cell_stride + w]
   int64_t out_cell_stride; // in uint32 elements
-  const uint32_t *tables_b1;  // device G5 table blob for this CRC type, B = 1 block per lane per step
-  const uint32_t *tables_b4;  // ... B = 4
+  const uint32_t *tables[3];  // device G5 table blobs for this CRC type, B = 1, 2, 4 blocks per lane per step
   uint32_t init_full;      // shift(0xFFFFFFFF, bpc bytes)
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
@@ -64,12 +63,14 @@ constexpr int kG5Step = 832;
 constexpr int kG5Tree = 1056;
 constexpr int kG5T0 = 2400;
 constexpr int kG5Words = 2656;
+constexpr int g5_slot(int B) { return B == 1 ? 0 : B == 2 ? 1 : 2; }
 
 // Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.
 struct TuneKnobs {
   int64_t grid = 0;       // blocks for the coding kernels
   int gf_variant = 0;     // coding-kernel variant 1..6 (VPT / cache policy), see launch_kr
-  int crc_variant = 0;    // 4: CRC kernel with B = 4; 3: fused kernel with SGPR coefficient tables
+  int crc_variant = 0;    // CRC kernel: 1/4 = B (default 2); fused: 3 SGPR tables, 5 prefetch, 6 B = 2, 7 both,
+                          //   8/9/10 = at least 5/6/8 waves per SIMD
   int64_t crc_grid = 0;   // blocks for the CRC / fused kernels
 };
 extern TuneKnobs g_tune;

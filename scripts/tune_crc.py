@@ -1,4 +1,5 @@
-"""Interleaved A/B of the CRC / fused encode+CRC kernel variants and grids in one process."""
+"""Interleaved A/B of the CRC / fused encode+CRC kernel variants and grids in one process.
+Every variant's outputs are compared bit-for-bit with the default variant's before timing."""
 import itertools, json, os, sys
 sys.path.insert(0, os.getcwd())
 import numpy as np, torch
@@ -9,28 +10,43 @@ torch.cuda.set_device(0)
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 n, bpc = 1 << 20, 16384
 lib = L.lib()
-steps = {}
-# fused rs-6-3 + CRC32C, 4096 stripes
 k, p, S = 6, 3, 4096
 U = torch.empty((S, k + p, n), dtype=torch.uint8, device="cuda")
 for u in range(k):
     rc.fill_splitmix64_cells(U[:, u], (k + p) * n, S, n, 1, u * S)
 crcs = torch.empty((S, k + p, n // bpc), dtype=torch.int32, device="cuda")
+crc2 = torch.empty((S * k, n // bpc), dtype=torch.int32, device="cuda")
 e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
 st = (k + p) * n
-steps["c5"] = (lambda: e.encode_crc_batch(U, st, n, U[:, k:], st, n, S, n, ck.ChecksumType.CRC32C, bpc, crcs), S * 9 * n)
-# crc only over the 4096 x 6 data cells (as one 24 GiB batch of cells)
-crc2 = torch.empty((S * k, n // bpc), dtype=torch.int32, device="cuda")
-D = U[:, :k]
-steps["crc"] = (lambda: [ck.checksum_windows_batch(ck.ChecksumType.CRC32C, U[:, j], st, S, n, bpc, crc2[j * S:]) for j in range(k)], S * k * n)
-variants = [int(v) for v in os.environ.get("VARIANTS", "0,3,4").split(",")]
-grids = [int(g) for g in os.environ.get("GRIDS", "0,4096,8192,16384,1000000").split(",")]
-configs = list(itertools.product(steps, variants, grids))
+steps = {
+    "c5": (lambda: e.encode_crc_batch(U, st, n, U[:, k:], st, n, S, n, ck.ChecksumType.CRC32C, bpc, crcs),
+           S * 9 * n, lambda: (crcs.clone(), U[:, k:].clone())),
+    "crc": (lambda: [ck.checksum_windows_batch(ck.ChecksumType.CRC32C, U[:, j], st, S, n, bpc, crc2[j * S:])
+                     for j in range(k)], S * k * n, lambda: (crc2.clone(),)),
+}
+VAR = {"c5": [int(v) for v in os.environ.get("C5VARIANTS", "0,3,5,6,7").split(",")],
+       "crc": [int(v) for v in os.environ.get("CRCVARIANTS", "0,2,4").split(",")]}
+grids = [int(g) for g in os.environ.get("GRIDS", "0,16384").split(",")]
+configs = [(w, v, g) for w in steps for v in VAR[w] for g in grids]
+# correctness: every variant equals variant 0 bit for bit
+for w in steps:
+    lib.ozec_set_tuning(b"crc_variant", 0); lib.ozec_set_tuning(b"crc_grid", 0)
+    steps[w][0](); torch.cuda.synchronize(); ref = steps[w][2]()
+    for v in VAR[w]:
+        lib.ozec_set_tuning(b"crc_variant", v)
+        for t in ref: pass
+        if w == "c5": crcs.zero_(); U[:, k:].zero_()
+        else: crc2.zero_()
+        steps[w][0](); torch.cuda.synchronize(); got = steps[w][2]()
+        ok = all(torch.equal(a, b) for a, b in zip(ref, got))
+        print(json.dumps({"check": w, "variant": v, "bit_exact_vs_default": ok}), flush=True)
+        if not ok:
+            sys.exit(2)
 times = {c: [] for c in configs}
 for r in range(rounds):
     for c in configs:
         lib.ozec_set_tuning(b"crc_variant", c[1]); lib.ozec_set_tuning(b"crc_grid", c[2])
-        fn, alg = steps[c[0]]
+        fn = steps[c[0]][0]
         fn()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(); fn(); fn(); b.record(); torch.cuda.synchronize()

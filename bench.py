@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5", "crc", "e2e"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3r", "c4", "c5", "crc", "e2e"])
     ap.add_argument("--stripes", type=int, default=0, help="override the stripe count (profiling only)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -62,7 +62,7 @@ class Workload:
         self.n = n
         if name in ("c2", "c5", "e2e"):
             k, p, S = 6, 3, stripes_override or (4096 if name != "e2e" else 1024)
-        elif name == "c3":
+        elif name in ("c3", "c3r"):
             k, p, S = 10, 4, stripes_override or 2048
         elif name == "c4":
             k, p, S = 2, 1, stripes_override or 16 * 256
@@ -121,6 +121,26 @@ class Workload:
                            "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S}
             self._step = lambda: self.dec.decode_batch(self.units, stride, n, present, self.erased, self.out, 4 * n,
                                                        n, S, n)
+        elif name == "c3r":
+            enc.encode_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n)
+            self.dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
+            self.erased = [0, 1, 2, 3]
+            present = [u for u in range(units) if u not in self.erased]
+            self.stored = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
+            ck.checksum_windows_batch(self.crc_type, self.units, n, S * units, n, self.bpc, self.stored)
+            self.out = torch.empty((S, 4, n), dtype=torch.uint8, device=dev)
+            self.out_crc = torch.empty((S, 4, self.nwin), dtype=torch.int32, device=dev)
+            self.mism = torch.empty(S, dtype=torch.int32, device=dev)
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * (k + 4) * n + S * (k + 4) * self.nwin * 4
+            self.kernel = "encode_crc_vec<10,4> (reconstruct mode)"
+            self.config = {"workload": "rs-10-4-1024k reconstruction: verify CRC32C of 10 read units + decode 4 + "
+                                       "CRC32C of rebuilt units, 2048 stripes, fused, device-resident",
+                           "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
+                           "bytes_per_checksum": self.bpc}
+            self._step = lambda: self.dec.reconstruct_crc_batch(
+                self.units, stride, n, present, self.erased, self.out, 4 * n, n, S, n, self.crc_type, self.bpc,
+                self.out_crc, d_expected=self.stored, d_mismatch=self.mism)
         elif name in ("c4", "c5"):
             self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n

@@ -140,6 +140,30 @@ int ozec_checksum_verify(int checksum_type, const uint8_t *data, size_t len, siz
                          const uint32_t *expected, size_t num_expected, size_t start_index,
                          int64_t *mismatch_index);
 
+/* ---- batched checksum verify for the datanode scanner
+ *      (KeyValueContainerCheck.verifyChecksum, hadoop-hdds/container-service/.../KeyValueContainerCheck.java:378-430)
+ *      and Checksum.verifyChecksum over many chunks: recompute every window of num_cells cells and compare with
+ *      d_expected[c][w] (stored big-endian when expected_big_endian, i.e. the raw ByteString bytes).
+ *      d_mismatch[c] = -1 when every window matches, else the first failing window index. ------------------ */
+int ozec_checksum_verify_batch(int checksum_type, const uint8_t *d_base, int64_t cell_stride, size_t num_cells,
+                               size_t len, size_t bytes_per_checksum, const uint32_t *d_expected,
+                               int expected_big_endian, int32_t *d_mismatch, void *stream);
+
+/* ---- fused reconstruction, one pass over HBM for what
+ *      ECReconstructionCoordinator.reconstructECBlockGroup (ECReconstructionCoordinator.java:240-352) does in three:
+ *      verify the stored CRCs of the units read (ChunkInputStream.java:493-506), decode the erased units
+ *      (RSRawDecoder / XORRawDecoder, same semantics as ozec_decode_batch), and compute the CRCs of the rebuilt units
+ *      (BlockOutputStream.java:835).
+ *      d_expected: [stripe][k+p][window] stored CRCs (NULL = skip verification; only the k units read are checked);
+ *      d_out_crcs: [stripe][num_erased][window]; d_mismatch[s] = -1, or the smallest (unit * nwin + window) whose
+ *      CRC did not verify. ---------------------------------------------------------------------------------- */
+int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_stripe_stride,
+                               int64_t in_unit_stride, const int *present, int num_present, const int *erased,
+                               int num_erased, uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride,
+                               size_t num_stripes, size_t len, int checksum_type, size_t bytes_per_checksum,
+                               const uint32_t *d_expected, int expected_big_endian, uint32_t *d_out_crcs,
+                               int out_big_endian, int32_t *d_mismatch, void *stream);
+
 /* ---- streaming ChecksumByteBuffer (CM/ChecksumByteBuffer.java:32-44): update(ByteBuffer) / getValue /
  *      reset over an opaque 32-bit state.  The GPU computes the raw CRC of the buffer and the host combines
  *      it with the running state (x^(8n) mod P shift), so results equal the sequential CrcIntTable. ---- */

@@ -193,5 +193,15 @@ def checksum_windows_batch(checksum_type, d_base, cell_stride, num_cells, length
         raise OzoneChecksumException(L.last_error())
 
 
+def checksum_verify_batch(checksum_type, d_base, cell_stride, num_cells, length, bytes_per_checksum, d_expected,
+                          d_mismatch, expected_big_endian=False, stream=None):
+    """Datanode-scanner style batch verify: d_mismatch[c] = -1 or first failing window."""
+    rc = L.lib().ozec_checksum_verify_batch(int(checksum_type), _dev_ptr(d_base), cell_stride, num_cells, length,
+                                            bytes_per_checksum, _dev_ptr(d_expected), 1 if expected_big_endian else 0,
+                                            _dev_ptr(d_mismatch), _stream_ptr(stream))
+    if rc != L.OZEC_OK:
+        raise OzoneChecksumException(L.last_error())
+
+
 def crc_combine(checksum_type, crc_a, crc_b, len_b):
     return int(L.lib().ozec_crc_combine(int(checksum_type), crc_a, crc_b, len_b))

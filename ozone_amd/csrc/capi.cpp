@@ -669,6 +669,123 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
   return OZEC_OK;
 }
 
+// ---- batched verify and fused reconstruction -------------------------------
+
+int ozec_checksum_verify_batch(int checksum_type, const uint8_t *d_base, int64_t cell_stride, size_t num_cells,
+                               size_t len, size_t bpc, const uint32_t *d_expected, int expected_big_endian,
+                               int32_t *d_mismatch, void *stream) {
+  if (num_cells == 0) return OZEC_OK;
+  if (!d_mismatch) return fail(OZEC_EINVAL, "null mismatch buffer");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  OZEC_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_mismatch), 0x7fffffff, num_cells, st));
+  if (len > 0) {
+    if (!d_base || !d_expected) return fail(OZEC_EINVAL, "null buffer");
+    CrcArgs a;
+    const int64_t nwin = static_cast<int64_t>((len + (bpc ? bpc : 1) - 1) / (bpc ? bpc : 1));
+    if (int rc = make_crc_args(ctx, checksum_type, d_base, cell_stride, num_cells, len, bpc, nullptr, nwin, 0, 0, &a))
+      return rc;
+    a.expected = d_expected;
+    a.expected_be = expected_big_endian;
+    a.mismatch = d_mismatch;
+    OZEC_HIP(ozec::launch_crc_windows(a, st));
+  }
+  OZEC_HIP(ozec::launch_finish_mismatch(d_mismatch, static_cast<int64_t>(num_cells), st));
+  return OZEC_OK;
+}
+
+int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
+                               const int *present_units, int num_present, const int *erased, int n_erased,
+                               uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes,
+                               size_t len, int checksum_type, size_t bpc, const uint32_t *d_expected,
+                               int expected_big_endian, uint32_t *d_out_crcs, int out_big_endian, int32_t *d_mismatch,
+                               void *stream) {
+  if (int rc = check_open(dec, "decode")) return rc;
+  if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
+  const int n_all = dec->k + dec->p;
+  bool present[256] = {false};
+  for (int i = 0; i < num_present; ++i) {
+    if (present_units[i] < 0 || present_units[i] >= n_all) return fail(OZEC_EINVAL, "present unit out of range");
+    present[present_units[i]] = true;
+  }
+  std::vector<int> units;
+  std::vector<uint8_t> rows;
+  if (int rc = plan_decode(dec, present, erased, n_erased, units, rows)) return rc;
+  if (num_stripes == 0) return OZEC_OK;
+  if (!d_in || (n_erased && (!d_out || !d_out_crcs))) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  if (d_expected && !d_mismatch) return fail(OZEC_EINVAL, "verification needs a mismatch buffer");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  if (d_mismatch)
+    OZEC_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_mismatch), 0x7fffffff, num_stripes, st));
+  if (len == 0) {
+    if (d_mismatch) OZEC_HIP(ozec::launch_finish_mismatch(d_mismatch, static_cast<int64_t>(num_stripes), st));
+    return OZEC_OK;
+  }
+  const int nin = static_cast<int>(units.size());
+  const int nrows = dec->codec == OZEC_CODEC_XOR ? (n_erased ? 1 : 0) : n_erased;
+  const int64_t nwin = static_cast<int64_t>((len + (bpc ? bpc : 1) - 1) / (bpc ? bpc : 1));
+  ozec::EncCrcArgs e{};
+  CodeArgs &a = e.code;
+  a.in = d_in;
+  a.out = d_out;
+  a.in_stripe_stride = in_stripe_stride;
+  a.out_stripe_stride = out_stripe_stride;
+  a.nstripes = static_cast<int64_t>(num_stripes);
+  a.len = static_cast<int64_t>(len);
+  if (nrows) {
+    fill_coef(a, nrows, nin, rows.data());
+    if (int rc = check_limits(a.k, a.rows)) return rc;
+  } else {
+    a.k = nin;
+    a.rows = 0;
+  }
+  for (int j = 0; j < nin; ++j) a.in_off[j] = units[j] * in_unit_stride;
+  for (int r = 0; r < nrows; ++r) a.out_off[r] = r * out_unit_stride;
+  if (int rc = make_crc_args(ctx, checksum_type, nullptr, 0, num_stripes, len, bpc, d_out_crcs, nwin, out_big_endian, 0,
+                             &e.crc))
+    return rc;
+  e.crc.expected = d_expected;
+  e.crc.expected_be = expected_big_endian;
+  e.crc.mismatch = d_mismatch;
+  e.verify = 1;
+  e.exp_units = n_all;
+  for (int j = 0; j < nin; ++j) e.in_unit[j] = units[j];
+  if (nrows && n_erased == nrows && ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
+    OZEC_HIP(ozec::launch_encode_crc(e, st));
+  } else {
+    // unfused: verify the read units, decode, CRC the rebuilt units
+    if (d_expected) {
+      for (int j = 0; j < nin; ++j) {
+        CrcArgs c = e.crc;
+        c.base = d_in + units[j] * in_unit_stride;
+        c.cell_stride = in_stripe_stride;
+        c.expected = d_expected + units[j] * nwin;
+        c.out_cell_stride = n_all * nwin;
+        c.mismatch_base = static_cast<int32_t>(units[j] * nwin);
+        OZEC_HIP(ozec::launch_crc_windows(c, st));
+      }
+    }
+    if (nrows) OZEC_HIP(ozec::launch_code(a, st));
+    for (int r = 0; r < n_erased; ++r) {
+      if (r >= nrows) {  // XOR decoders zero-fill outputs beyond erasedIndexes[0]
+        OZEC_HIP(hipMemset2DAsync(d_out + r * out_unit_stride, out_stripe_stride, 0, len, num_stripes, st));
+      }
+      CrcArgs c = e.crc;
+      c.base = d_out + r * out_unit_stride;
+      c.cell_stride = out_stripe_stride;
+      c.out = d_out_crcs + r * nwin;
+      c.out_cell_stride = n_erased * nwin;
+      c.expected = nullptr;
+      OZEC_HIP(ozec::launch_crc_windows(c, st));
+    }
+  }
+  if (d_mismatch) OZEC_HIP(ozec::launch_finish_mismatch(d_mismatch, static_cast<int64_t>(num_stripes), st));
+  return OZEC_OK;
+}
+
 // ---- host-side math ----------------------------------------------------------------------------
 
 int ozec_rs_encode_matrix(int k, int p, uint8_t *matrix) {

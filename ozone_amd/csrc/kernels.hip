@@ -377,6 +377,19 @@ __device__ __forceinline__ uint32_t crc_finish(uint32_t raw, uint32_t init, int 
   return big_endian ? __builtin_bswap32(v) : v;
 }
 
+// store the window CRC, or (verify mode) compare it with the expected value and record the first failure
+__device__ __forceinline__ void crc_emit(const CrcArgs &a, int64_t cell, int64_t w, uint32_t raw, bool last) {
+  const uint32_t init = last ? a.init_last : a.init_full;
+  const int64_t idx = cell * a.out_cell_stride + w;
+  if (a.expected) {
+    const uint32_t v = crc_finish(raw, init, 0, 0);
+    const uint32_t e = a.expected_be ? __builtin_bswap32(a.expected[idx]) : a.expected[idx];
+    if (v != e) atomicMin(a.mismatch + cell, a.mismatch_base + static_cast<int32_t>(w));
+  } else {
+    a.out[idx] = crc_finish(raw, init, a.raw, a.big_endian);
+  }
+}
+
 // One wave per (cell, window).  Lane l owns B consecutive 16-B blocks of every 64*B-block step and folds them
 // into its register (state XORed into the next block's first 4 bytes); between steps the register jumps
 // (63*B)*16 bytes.  Windows are front-padded with virtual zero blocks to a whole number of steps.
@@ -428,7 +441,7 @@ __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
     }
     S = g5_lane_tree(s_t, S, lane);
     for (int64_t i = m * 16; i < N; ++i) S = (S >> 8) ^ s_t[kG5T0 + ((S ^ win[i]) & 0xff)];
-    if (lane == 0) a.out[c * a.out_cell_stride + w] = crc_finish(S, last ? a.init_last : a.init_full, a.raw, a.big_endian);
+    if (lane == 0) crc_emit(a, c, w, S, last);
   }
 }
 
@@ -447,7 +460,7 @@ __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
     const uint8_t *win = a.base + c * a.cell_stride + w * a.bpc;
     uint32_t S = 0;
     for (int64_t i = 0; i < N; ++i) S = (S >> 8) ^ s_t0[(S ^ win[i]) & 0xff];
-    a.out[c * a.out_cell_stride + w] = crc_finish(S, last ? a.init_last : a.init_full, a.raw, a.big_endian);
+    crc_emit(a, c, w, S, last);
   }
 }
 
@@ -582,9 +595,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 #pragma unroll
     for (int q = 0; q < K + R; ++q) {
       const uint32_t v = g5_lane_tree(s_t, S[q], lane);
-      if (lane == q) cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+      if (lane == q) {
+        if (!e.verify) {
+          cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+        } else if (q >= K) {
+          cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+        } else if (cr.expected) {
+          const int64_t idx = (s * e.exp_units + e.in_unit[q]) * nwin + w;
+          const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
+          if (crc_finish(v, init, 0, 0) != ex)
+            atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
+        }
+      }
     }
   }
+}
+
+__global__ void finish_mismatch(int32_t *m, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n && m[i] == 0x7fffffff) m[i] = -1;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -798,11 +827,7 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
   return hipGetLastError();
 }
 
-bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
-  const bool kr = (a.k == 3 && a.rows == 2) || (a.k == 6 && a.rows == 3) || (a.k == 10 && a.rows == 4) ||
-                  (a.k == 2 && a.rows == 1);
-  return kr && bpc > 0 && aligned16(bpc) && aligned16(a.len) && vec_ok(a);
-}
+namespace {
 
 template <int K, int R>
 hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
@@ -812,17 +837,32 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
   const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : (units + 3) / 4;
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
   constexpr bool kS = K * R <= 18;
-  switch (g_tune.crc_variant) {
-    case 3: hipLaunchKernelGGL((encode_crc_vec<K, R, kS, 1, false>), grid, block, 0, st, e, tabs); break;
-    case 5: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, true>), grid, block, 0, st, e, tabs); break;
-    case 6: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 2, false>), grid, block, 0, st, e, tabs); break;
-    case 7: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 2, true>), grid, block, 0, st, e, tabs); break;
-    case 8: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 5>), grid, block, 0, st, e, tabs); break;
-    case 9: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 6>), grid, block, 0, st, e, tabs); break;
-    case 10: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 8>), grid, block, 0, st, e, tabs); break;
-    default: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs); break;
+  if constexpr (K == 6 && R == 3) {  // the headline shape carries the tuning variants (scripts/tune_crc.py)
+    switch (g_tune.crc_variant) {
+      case 3: hipLaunchKernelGGL((encode_crc_vec<K, R, kS, 1, false>), grid, block, 0, st, e, tabs); break;
+      case 5: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, true>), grid, block, 0, st, e, tabs); break;
+      case 6: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 2, false>), grid, block, 0, st, e, tabs); break;
+      case 7: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 2, true>), grid, block, 0, st, e, tabs); break;
+      case 8: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 5>), grid, block, 0, st, e, tabs); break;
+      default: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs); break;
+    }
+  } else {
+    hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs);
   }
   return hipGetLastError();
+}
+
+#define OZEC_FUSED_SHAPES(X) X(6, 3) X(6, 2) X(6, 1) X(3, 2) X(3, 1) X(10, 4) X(10, 3) X(10, 2) X(10, 1) X(2, 1)
+
+}  // namespace
+
+bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
+  bool kr = false;
+#define OZEC_SHAPE_OK(KK, RR) kr |= (a.k == KK && a.rows == RR);
+  OZEC_FUSED_SHAPES(OZEC_SHAPE_OK)
+#undef OZEC_SHAPE_OK
+  CodeArgs rb = a;
+  return kr && bpc > 0 && aligned16(bpc) && aligned16(a.len) && vec_ok(a) && rebase32(rb);
 }
 
 hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
@@ -830,11 +870,17 @@ hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   EncCrcArgs e = e0;
   if (!rebase32(e.code)) return hipErrorInvalidValue;
   const int k = e.code.k, r = e.code.rows;
-  if (k == 6 && r == 3) return launch_enc_crc_kr<6, 3>(e, st);
-  if (k == 3 && r == 2) return launch_enc_crc_kr<3, 2>(e, st);
-  if (k == 10 && r == 4) return launch_enc_crc_kr<10, 4>(e, st);
-  if (k == 2 && r == 1) return launch_enc_crc_kr<2, 1>(e, st);
+#define OZEC_SHAPE_LAUNCH(KK, RR) \
+  if (k == KK && r == RR) return launch_enc_crc_kr<KK, RR>(e, st);
+  OZEC_FUSED_SHAPES(OZEC_SHAPE_LAUNCH)
+#undef OZEC_SHAPE_LAUNCH
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_finish_mismatch(int32_t *d_mismatch, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(finish_mismatch, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, st, d_mismatch, n);
+  return hipGetLastError();
 }
 
 hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t ncells, int64_t n, uint64_t seed,

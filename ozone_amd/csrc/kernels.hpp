@@ -43,12 +43,25 @@ struct CrcArgs {
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
   int32_t raw;             // emit the raw (init 0, no xorout) register instead of getValue()
+  // verify mode (expected != null): instead of storing, compare with expected[c * out_cell_stride + w]
+  // (stored big-endian when expected_be) and atomicMin (mismatch_base + w) into mismatch[c]
+  const uint32_t *expected;
+  int32_t *mismatch;
+  int32_t expected_be;
+  int32_t mismatch_base;
 };
 
-// Fused encode + CRC of every data and parity unit (bpc % 16 == 0, len % 16 == 0, 16-B aligned).
+// Fused encode + CRC (bpc % 16 == 0, len % 16 == 0, 16-B aligned).
+//   encode mode (verify == 0): crc.out = crcs[s][unit][w] for all K inputs and R outputs (out_cell_stride = nwin)
+//   reconstruct mode (verify == 1): the K inputs are checked against crc.expected[s][in_unit[j]][w]
+//     (exp_units units per stripe) with failures atomicMin'ed into crc.mismatch[s] as in_unit*nwin + w, and only
+//     the R rebuilt units' CRCs are stored: crc.out[s][r][w]
 struct EncCrcArgs {
   CodeArgs code;
-  CrcArgs crc;  // crc.base unused; crc.out = crcs[s][unit][w] with crc.out_cell_stride = nwin
+  CrcArgs crc;
+  int32_t verify;
+  int32_t exp_units;
+  int32_t in_unit[OZEC_MAX_K];
 };
 
 // Device CRC "G5" table blob (uint32 entries), built on the host (crc_host.cpp), one per (CRC type, B) where
@@ -78,6 +91,8 @@ extern TuneKnobs g_tune;
 hipError_t launch_code(const CodeArgs &a, hipStream_t stream);
 hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t stream);
 hipError_t launch_encode_crc(const EncCrcArgs &a, hipStream_t stream);
+// d_mismatch[i] == INT32_MAX (no failure recorded) -> -1
+hipError_t launch_finish_mismatch(int32_t *d_mismatch, int64_t n, hipStream_t stream);
 hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t ncells, int64_t n, uint64_t seed,
                                   uint64_t first_stream, hipStream_t stream);
 // true when the fused kernel supports this (k, rows) pair with the given geometry

@@ -381,6 +381,22 @@ class RawErasureDecoder(_Coder):
             _raise_for(rc)
 
 
+    def reconstruct_crc_batch(self, d_in, in_stripe_stride, in_unit_stride, present_units, erased_indexes, d_out,
+                              out_stripe_stride, out_unit_stride, num_stripes, length, checksum_type,
+                              bytes_per_checksum, d_out_crcs, d_expected=None, d_mismatch=None,
+                              expected_big_endian=False, out_big_endian=False, stream=None):
+        """Fused reconstruction: verify the read units' stored CRCs, decode, CRC the rebuilt
+        units.  d_mismatch[s] = -1 or the smallest unit*nwin + window that failed verification."""
+        rc = L.lib().ozec_reconstruct_crc_batch(
+            self._handle, _dev_ptr(d_in), in_stripe_stride, in_unit_stride, L.int_array(list(present_units)),
+            len(present_units), L.int_array(list(erased_indexes)), len(erased_indexes), _dev_ptr(d_out),
+            out_stripe_stride, out_unit_stride, num_stripes, length, int(checksum_type), bytes_per_checksum,
+            _dev_ptr(d_expected), 1 if expected_big_endian else 0, _dev_ptr(d_out_crcs), 1 if out_big_endian else 0,
+            _dev_ptr(d_mismatch), _stream_ptr(stream))
+        if rc != L.OZEC_OK:
+            _raise_for(rc)
+
+
 # ---------------------------------------------------------------- factories / registry -------------------
 
 class RawErasureCoderFactory:

@@ -1,0 +1,94 @@
+"""SURVEY.md §8(f) rows 1-2 on the GPU vs the oracle: batched checksum verify (datanode scanner) and the fused
+reconstruction pass (verify read units' CRCs + decode + CRC of rebuilt units)."""
+import numpy as np
+import pytest
+
+import oracle
+from synth import SEED, cells
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from ozone_amd import checksum as ck  # noqa: E402
+from ozone_amd import rawcoder as rc  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def h(x):
+    torch.cuda.synchronize()
+    return x.cpu().numpy()
+
+
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
+@pytest.mark.parametrize("bpc,big_endian", [(16384, False), (16384, True), (4096, False), (1000, False)])
+def test_checksum_verify_batch(ctype, otype, bpc, big_endian):
+    C, n = 6, 100_000
+    data = np.stack(cells(SEED, 60000, C, n))
+    nwin = (n + bpc - 1) // bpc
+    exp = np.stack([oracle.crc_windows(otype, data[c], bpc) for c in range(C)]).astype(np.uint32)
+    if big_endian:
+        exp = exp.byteswap()
+    bad = data.copy()
+    bad[2, 5 * bpc + 7] ^= 0x40          # window 5 of cell 2
+    bad[4, n - 1] ^= 1                   # last window of cell 4
+    d_exp = t(exp.view(np.int32))
+    mism = torch.zeros(C, dtype=torch.int32, device=DEV)
+    ck.checksum_verify_batch(ctype, t(bad), n, C, n, bpc, d_exp, mism, expected_big_endian=big_endian)
+    got = h(mism)
+    assert got.tolist() == [-1, -1, 5, -1, nwin - 1, -1]
+    ck.checksum_verify_batch(ctype, t(data), n, C, n, bpc, d_exp, mism, expected_big_endian=big_endian)
+    assert h(mism).tolist() == [-1] * C
+
+
+def _stripe_units(codec, k, p, n, S, first):
+    out = []
+    for s in range(S):
+        d = cells(SEED, first + s * k, k, n)
+        par = oracle.rs_encode(k, p, d) if codec == "rs" else [oracle.xor_encode(d)]
+        out.append(np.stack(d + par))
+    return np.stack(out)  # [S][k+p][n]
+
+
+@pytest.mark.parametrize("codec,k,p,erased,n,bpc", [
+    ("rs", 6, 3, [0, 2, 7], 1 << 18, 16384),      # fused shape (6,3)
+    ("rs", 6, 3, [1], 1 << 18, 16384),            # fused shape (6,1)
+    ("rs", 10, 4, [0, 1, 2, 3], 1 << 17, 16384),  # fused shape (10,4)
+    ("rs", 10, 4, [1, 4, 10, 13], 1 << 17, 16384),
+    ("rs", 3, 2, [0, 4], 1 << 16, 4096),
+    ("xor", 2, 1, [1], 1 << 16, 16384),           # fused shape (2,1)
+    ("rs", 5, 2, [0, 6], 1 << 16, 16384),         # unfused fallback (shape not instantiated)
+    ("rs", 6, 3, [0, 2, 7], 50000, 1000),         # unfused fallback (bpc not a multiple of 16)
+])
+def test_reconstruct_crc_batch(codec, k, p, erased, n, bpc):
+    S = 4
+    units = _stripe_units(codec, k, p, n, S, 70000)
+    ctype, otype = ck.ChecksumType.CRC32C, oracle.CRC32C
+    nwin = (n + bpc - 1) // bpc
+    stored = np.stack([np.stack([oracle.crc_windows(otype, units[s, u], bpc) for u in range(k + p)])
+                       for s in range(S)]).astype(np.uint32)                     # [S][k+p][nwin]
+    present = [u for u in range(k + p) if u not in erased]
+    read = present[:k]
+    corrupted = units.copy()
+    corrupted[:, [e for e in erased]] = 0xEE                                     # erased units are garbage
+    corrupted[1, read[-1], 3 * bpc + 1] ^= 0x10                                  # stripe 1: silent corruption
+    d_in = t(corrupted)
+    d_out = torch.zeros((S, len(erased), n), dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, len(erased), nwin), dtype=torch.int32, device=DEV)
+    mism = torch.zeros(S, dtype=torch.int32, device=DEV)
+    dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec))
+    dec.reconstruct_crc_batch(d_in, (k + p) * n, n, present, erased, d_out, len(erased) * n, n, S, n, ctype, bpc,
+                              d_crc, d_expected=t(stored.view(np.int32)), d_mismatch=mism)
+    out, crcs, m = h(d_out), h(d_crc).view(np.uint32), h(mism)
+    assert m[0] == -1 and m[2] == -1 and m[3] == -1
+    assert m[1] == read[-1] * nwin + 3
+    for s in (0, 2, 3):  # clean stripes rebuild exactly, and their CRCs equal the stored ones
+        for i, e in enumerate(erased):
+            assert (out[s, i] == units[s, e]).all(), (s, e)
+            assert (crcs[s, i] == stored[s, e]).all(), (s, e)
+    for i in range(len(erased)):  # the corrupted stripe's rebuilt CRCs still describe what was written
+        assert (crcs[1, i] == oracle.crc_windows(otype, out[1, i], bpc)).all()

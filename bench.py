@@ -224,11 +224,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # OZEC_BENCH_SAME_DEVICE=1 + OZEC_DIST_BACKEND=gloo rehearse the N-rank path on a one-GPU box
+    dev_idx = 0 if os.environ.get("OZEC_BENCH_SAME_DEVICE") == "1" else local
+    torch.cuda.set_device(dev_idx)
+    backend = os.environ.get("OZEC_DIST_BACKEND", "nccl")
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(backend)
     wl = Workload(args.workload, rank, args.stripes)
 
     def barrier():
@@ -250,7 +256,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     from ozone_amd.shard import max_over_ranks
-    elapsed = max_over_ranks(elapsed, dist, device="cuda")
+    elapsed = max_over_ranks(elapsed, dist, device="cuda" if backend == "nccl" else "cpu")
     value = wl.data_bytes * world * args.steps / elapsed / 1e9
     achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None

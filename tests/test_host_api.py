@@ -1,0 +1,70 @@
+"""Host-side mirror of the reference API on CPU (no GPU call): java.nio buffer semantics the coders rely on,
+ECChunk, ChecksumData matching rules (ChecksumData.java:118-150), Checksum NONE/SHA256/MD5 delegation."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from ozone_amd import ByteBuffer, ECChunk
+from ozone_amd import checksum as ck
+
+
+def test_bytebuffer_wrap_slice_positions():
+    arr = np.arange(64, dtype=np.uint8)
+    b = ByteBuffer.wrap(arr, 11, 20)  # ByteBuffer.wrap(array, offset, length)
+    assert (b.position(), b.limit(), b.remaining(), b.array_offset()) == (11, 31, 20, 0)
+    s = b.slice()
+    assert (s.position(), s.remaining(), s.array_offset()) == (0, 20, 11)
+    assert s.get(0) == 11 and s.address() == arr.ctypes.data + 11
+    d = ByteBuffer.allocate_direct(8)
+    assert d.is_direct() and not d.has_array()
+    with pytest.raises(TypeError):
+        d.array()
+    h = ByteBuffer.allocate(8)
+    h.put(b"\x01\x02\x03")
+    assert h.position() == 3
+    h.flip()
+    assert (h.position(), h.limit()) == (0, 3)
+    ro = h.as_read_only_buffer()
+    with pytest.raises(TypeError):
+        ro.put(b"x")
+
+
+def test_ecchunk_offset_slice_and_all_zero():
+    buf = ByteBuffer.wrap(np.arange(100, dtype=np.uint8))
+    c = ECChunk(buf, 10, 30)  # ECChunk(ByteBuffer, offset, len) slices (ECChunk.java:41-49)
+    assert c.get_buffer().remaining() == 30 and c.get_buffer().get(0) == 10
+    z = ECChunk(ByteBuffer.wrap(np.full(16, 7, np.uint8)), all_zero=True)
+    assert not ECChunk.to_buffers([z, None])[0].view().any()
+
+
+def test_checksum_data_matching_rules():
+    a = ck.ChecksumData(ck.ChecksumType.CRC32, 4, [b"\x00\x00\x00\x01", b"\x00\x00\x00\x02", b"\x00\x00\x00\x03"])
+    assert a.verify_checksum_data_matches(ck.ChecksumData(ck.ChecksumType.CRC32, 4, a.checksums[1:]), 1)
+    with pytest.raises(ck.OzoneChecksumException) as e:
+        a.verify_checksum_data_matches(ck.ChecksumData(ck.ChecksumType.CRC32, 4, [b"\x00\x00\x00\x09"]), 0)
+    assert e.value.index == 0
+    with pytest.raises(ck.OzoneChecksumException, match="starting from index 2"):
+        a.verify_checksum_data_matches(ck.ChecksumData(ck.ChecksumType.CRC32, 4, [a.checksums[2]] * 2), 2)
+    with pytest.raises(ck.OzoneChecksumException, match="Original checksumData has no checksums"):
+        ck.ChecksumData(ck.ChecksumType.CRC32, 4).verify_checksum_data_matches(a, 0)
+    with pytest.raises(ck.OzoneChecksumException, match="Computed checksumData has no checksums"):
+        a.verify_checksum_data_matches(ck.ChecksumData(ck.ChecksumType.CRC32, 4), 0)
+
+
+def test_int2bytes_is_big_endian_of_int_value():
+    assert ck.int2bytes(0xE3069283) == bytes.fromhex("e3069283")
+
+
+def test_checksum_none_and_digests_on_host():
+    data = np.arange(55, dtype=np.uint8)
+    assert ck.Checksum(ck.ChecksumType.NONE, 10).compute_checksum(data).get_checksums() == []
+    sha = ck.Checksum(ck.ChecksumType.SHA256, 10).compute_checksum(data).get_checksums()
+    assert sha == [hashlib.sha256(data[o:o + 10].tobytes()).digest() for o in range(0, 55, 10)]
+    md5 = ck.Checksum(ck.ChecksumType.MD5, 16).compute_checksum(data).get_checksums()
+    assert len(md5) == 4 and md5[0] == hashlib.md5(data[:16].tobytes()).digest()
+    assert ck.Checksum.verify_checksum(data, ck.ChecksumData(ck.ChecksumType.NONE, 10))
+
+
+def test_checksum_empty_needs_no_device():
+    assert ck.Checksum(ck.ChecksumType.CRC32C, 16384).compute_checksum(b"").get_checksums() == []

@@ -104,7 +104,7 @@ class Workload:
             self.data_bytes = S * k * n
             self.alg_bytes = S * units * n
             self.kernel = "gf_code_vec<6,3>"
-            self.config = {"workload": "rs-6-3-1024k encode, 4096 stripes, device-resident (BASELINE configs[1])",
+            self.config = {"workload": f"rs-6-3-1024k encode, {S} stripes, device-resident (BASELINE configs[1])",
                            "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
                            "layout": "stripe-major [stripe][unit][cell] in HBM"}
             self._step = lambda: enc.encode_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n)
@@ -117,7 +117,7 @@ class Workload:
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + len(self.erased)) * n
             self.kernel = "gf_code_vec<10,4>"
-            self.config = {"workload": "rs-10-4-1024k decode, 2048 stripes, 4 erased {0,1,2,3}, device-resident",
+            self.config = {"workload": f"rs-10-4-1024k decode, {S} stripes, 4 erased {{0,1,2,3}}, device-resident",
                            "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S}
             self._step = lambda: self.dec.decode_batch(self.units, stride, n, present, self.erased, self.out, 4 * n,
                                                        n, S, n)

@@ -193,6 +193,7 @@ int plan_decode(ozec_coder *dec, const bool *present, const int *erased, int n_e
 }
 
 void fill_coef(CodeArgs &a, int rows, int k, const uint8_t *coef) {
+  a.unit_map = ozec::g_tune.unit_map;
   a.k = k;
   a.rows = rows;
   std::memcpy(a.coef, coef, static_cast<size_t>(rows) * k);
@@ -526,6 +527,7 @@ static int make_crc_args(DevCtx *ctx, int checksum_type, const uint8_t *d_base, 
   a->init_last = cm.shift(0xffffffffu, len - (a->nwin ? (a->nwin - 1) * bpc : 0));
   a->big_endian = big_endian;
   a->raw = raw;
+  a->unit_map = ozec::g_tune.unit_map;
   return OZEC_OK;
 }
 
@@ -857,6 +859,7 @@ int ozec_set_tuning(const char *key, int64_t value) {
   else if (k == "gf_variant") ozec::g_tune.gf_variant = static_cast<int>(value);
   else if (k == "crc_variant") ozec::g_tune.crc_variant = static_cast<int>(value);
   else if (k == "crc_grid") ozec::g_tune.crc_grid = value;
+  else if (k == "unit_map") ozec::g_tune.unit_map = static_cast<int>(value);
   else return fail(OZEC_EINVAL, "unknown tuning key " + k);
   return OZEC_OK;
 }

@@ -136,6 +136,15 @@ struct TabArgs {
   uint32_t w[N][5];  // per coefficient: lo0, lo1, mid0, mid1, top
 };
 
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (b and b+8 share one), so map
+// block b to work item (b % 8) * (n / 8) + b / 8: every XCD streams one contiguous eighth of the batch instead of
+// all eight interleaving at 4 KiB granularity.  Bijective on [0, n) (the n % 8 tail keeps its own index).
+// Measured on C2 (scripts/tune_map.py): 75.6 % -> 78.7 % of the HBM roofline.  Placement is a speed hint only.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
+  const uint32_t q = n >> 3;
+  return b < (q << 3) ? (b & 7) * q + (b >> 3) : b;
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
   // raw buffer (stride 0), full 4 GiB range; bounds are checked explicitly by the kernels
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0xffffffff, 0x00020000);
@@ -169,10 +178,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
   constexpr uint32_t kChunk = kBlock * VPT;
   const uint32_t cpc = (nvec + kChunk - 1) / kChunk;  // units per cell
   const uint32_t units = static_cast<uint32_t>(a.nstripes) * cpc;
-  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+  const uint32_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  for (uint32_t u = bid; u < units; u += gridDim.x) {
     if constexpr (!SREG) asm volatile("" ::: "memory");  // keep the LDS table reads inside the loop
     const uint32_t s = u / cpc;
-    const uint32_t v0 = (u - s * cpc) * kChunk + threadIdx.x;
+    const uint32_t c = u - s * cpc;
+    const uint32_t v0 = c * kChunk + threadIdx.x;
     const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + static_cast<int64_t>(s) * a.in_stripe_stride);
     const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + static_cast<int64_t>(s) * a.out_stripe_stride);
     uint4 x[VPT][K];
@@ -402,8 +413,8 @@ __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t units = a.ncells * a.nwin;
-  for (int64_t u = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + wave; u < units;
-       u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  for (int64_t u = bid * (kBlock / 64) + wave; u < units; u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
     const int64_t c = u / a.nwin;
     const int64_t w = u - c * a.nwin;
     const bool last = w == a.nwin - 1;
@@ -494,8 +505,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
   const int wave = threadIdx.x >> 6;
   const int64_t nwin = cr.nwin;
   const int64_t units = a.nstripes * nwin;
-  for (int64_t u = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + wave; u < units;
-       u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  for (int64_t u = bid * (kBlock / 64) + wave; u < units; u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
     const int64_t s = u / nwin;
     const int64_t w = u - s * nwin;
     const bool last = w == nwin - 1;
@@ -727,10 +738,10 @@ hipError_t launch_krv(const CodeArgs &a, hipStream_t st, int64_t default_grid) {
   return hipGetLastError();
 }
 
-// Defaults measured on MI355X (scripts/tune.py, profiles/r01/tune_*.log): register-table kernels run best as
-// one 4 KiB chunk per block (a non-persistent grid keeps the in-flight chunks contiguous in HBM) with
-// non-temporal loads and stores; LDS-table kernels (K*R > 18) prefer 2 chunks per lane and a 8192-block
-// grid.  ozec_set_tuning("gf_variant", 1..6) pins one (VPT, load policy, store policy) combination.
+// Defaults measured on MI355X (scripts/tune.py, scripts/tune_all.py, profiles/r01/tune_*.log): one 4 KiB chunk
+// per block on a non-persistent grid (XCD-contiguous block order, xcd_remap) with non-temporal loads and stores,
+// for register-table and LDS-table kernels alike (C2 77.9 %, C3 77.9 % of the HBM roofline).
+// ozec_set_tuning("gf_variant", 1..6) pins one (VPT, load policy, store policy) combination.
 template <int K, int R>
 hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
   constexpr int64_t kAll = int64_t{1} << 40;
@@ -743,8 +754,7 @@ hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
     case 6: return launch_krv<K, R, 2, 2, 2>(a, st, 8192);
     default: break;
   }
-  if constexpr (K * R <= 18) return launch_krv<K, R, 1, 2, 2>(a, st, kAll);
-  else return launch_krv<K, R, 2, 2, 2>(a, st, 8192);
+  return launch_krv<K, R, 1, 2, 2>(a, st, kAll);
 }
 
 template <int K>

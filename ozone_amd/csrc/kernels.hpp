@@ -22,7 +22,7 @@ struct CodeArgs {
   int32_t k;
   int32_t rows;
   int32_t all_ones;  // every coefficient is 1 (XOR codec): pure XOR kernel
-  int32_t pad_;
+  int32_t unit_map;  // block order: 0 XCD-contiguous (default, see xcd_remap), 1 plain blockIdx order
   int64_t in_off[OZEC_MAX_K];
   int64_t out_off[OZEC_MAX_ROWS];
   uint8_t coef[OZEC_MAX_ROWS * OZEC_MAX_K];  // row-major rows x k
@@ -49,6 +49,7 @@ struct CrcArgs {
   int32_t *mismatch;
   int32_t expected_be;
   int32_t mismatch_base;
+  int32_t unit_map;        // as CodeArgs::unit_map
 };
 
 // Fused encode + CRC (bpc % 16 == 0, len % 16 == 0, 16-B aligned).
@@ -85,6 +86,7 @@ struct TuneKnobs {
   int crc_variant = 0;    // CRC kernel: 1/4 = B (default 2); fused: 3 SGPR tables, 5 prefetch, 6 B = 2, 7 both,
                           //   8/9/10 = at least 5/6/8 waves per SIMD
   int64_t crc_grid = 0;   // blocks for the CRC / fused kernels
+  int unit_map = 0;       // CodeArgs::unit_map for the coding kernels
 };
 extern TuneKnobs g_tune;
 

@@ -40,10 +40,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3r", "c4", "c5", "crc", "e2e"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3r", "c4", "c5", "crc", "e2e", "host"])
     ap.add_argument("--stripes", type=int, default=0, help="override the stripe count (profiling only)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--threads", type=int, default=1, help="host workload: caller threads sharing one coder")
     return ap.parse_args()
 
 
@@ -53,13 +54,42 @@ def parse():
 class Workload:
     """Allocates device-resident inputs once; step() launches one batch on the current stream."""
 
-    def __init__(self, name, rank, stripes_override):
+    def __init__(self, name, rank, stripes_override, threads=1):
         from ozone_amd import checksum as ck
         from ozone_amd import rawcoder as rc
         self.name = name
         dev = torch.device("cuda", torch.cuda.current_device())
         n = MIB
         self.n = n
+        if name == "host":
+            k, p, S = 6, 3, stripes_override or 64
+            T = max(1, threads)
+            rng = np.random.default_rng(rank)
+            self.hd = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for _ in range(T)]
+            self.hp = [[np.empty(n, np.uint8) for _ in range(p)] for _ in range(T)]
+            self.k, self.p, self.S = k, p, S
+            enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * (k + p) * n
+            self.kernel = "gf_code_vec<6,3> (+pageable->pinned staging, H2D, D2H, per stripe)"
+            self.config = {"workload": f"rs-6-3-1024k encode through the host-pointer ABI (ozec_encode: the JNI "
+                                       f"drop-in path), {S} single-stripe calls from {T} threads sharing one coder",
+                           "stripes": S, "threads": T}
+
+            def run(t):
+                for _ in range(t, S, T):
+                    enc.encode(self.hd[t], self.hp[t])
+
+            def step():
+                if T == 1:
+                    return run(0)
+                ts = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+                for th in ts:
+                    th.start()
+                for th in ts:
+                    th.join()
+            self._step = step
+            return
         if name in ("c2", "c5", "e2e"):
             k, p, S = 6, 3, stripes_override or (4096 if name != "e2e" else 1024)
         elif name in ("c3", "c3r"):
@@ -235,7 +265,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
             dist.init_process_group(backend)
-    wl = Workload(args.workload, rank, args.stripes)
+    wl = Workload(args.workload, rank, args.stripes, args.threads)
 
     def barrier():
         if dist is not None:
@@ -283,7 +313,7 @@ def main():
                      "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": wl.alg_bytes},
     }
-    if rank == 0 and world == 1 and not args.no_cpu and args.workload in ("c2", "e2e"):
+    if rank == 0 and world == 1 and not args.no_cpu and args.workload in ("c2", "e2e", "host"):
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)

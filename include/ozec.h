@@ -60,6 +60,7 @@ int ozec_version(void);
 int ozec_device_count(void);
 /* select the GPU used by subsequently created coders and host calls on this thread */
 int ozec_set_device(int device);
+/* wait for all work queued on the calling thread's current device (host-buffer calls are already synchronous) */
 int ozec_synchronize(void);
 
 /* ---- coder lifecycle: RawErasureCoderFactory.createEncoder/createDecoder
@@ -186,7 +187,8 @@ int ozec_parse_replication(const char *s, int *codec, int *num_data, int *num_pa
 uint32_t ozec_crc_combine(int checksum_type, uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
 /* ---- harness utilities ------------------------------------------------------------------------------- */
-/* process-wide kernel tuning knobs for benchmarking ("grid", "gf_variant", "crc_variant"; 0 = default) */
+/* process-wide tuning knobs for benchmarking: kernels ("grid", "gf_variant", "crc_variant", "crc_grid",
+ * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_slots") */
 int ozec_set_tuning(const char *key, int64_t value);
 /* fill n bytes with splitmix64 stream `stream_id` of `seed` (tests/golden/synth.py is the CPU twin) */
 int ozec_fill_splitmix64(uint8_t *d_dst, size_t n, uint64_t seed, uint64_t stream_id, void *stream);

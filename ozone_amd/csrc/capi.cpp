@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -44,17 +45,18 @@ int fail(int code, const std::string &msg) {
 // ------------------------------------------------------------------------------------------------
 // per-GPU context
 
-struct DevCtx {
-  int device = -1;
+// One staging slot = a private stream + pinned host buffer + device buffer. Host-pointer calls (the JNI
+// drop-in path) take a slot from the pool for the duration of the call, so calls from different threads
+// overlap on the GPU and on the copy engines instead of serialising on one buffer.
+struct Slot {
   hipStream_t stream = nullptr;
-  std::mutex mu;  // guards the staging buffers below
   uint8_t *pinned = nullptr;
   size_t pinned_cap = 0;
   uint8_t *dbuf = nullptr;
   size_t dbuf_cap = 0;
-  uint32_t *crc_tables[2][3] = {};  // [type][B = 1, 2, 4]
+  std::vector<hipEvent_t> events;
 
-  int reserve(size_t bytes) {
+  int reserve(size_t bytes, size_t nevents) {
     if (bytes > pinned_cap) {
       if (pinned) (void)hipHostFree(pinned);
       pinned = nullptr;
@@ -71,7 +73,53 @@ struct DevCtx {
       OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&dbuf), cap));
       dbuf_cap = cap;
     }
+    while (events.size() < nevents) {
+      hipEvent_t e;
+      OZEC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      events.push_back(e);
+    }
     return OZEC_OK;
+  }
+};
+
+struct DevCtx {
+  int device = -1;
+  std::mutex pool_mu;  // guards the slot pool
+  std::condition_variable pool_cv;
+  std::vector<std::unique_ptr<Slot>> slots;
+  std::vector<Slot *> free_slots;
+  uint32_t *crc_tables[2][3] = {};  // [type][B = 1, 2, 4]
+
+  int acquire(Slot **out) {
+    std::unique_lock<std::mutex> lk(pool_mu);
+    const size_t max_slots = static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.host_slots));
+    pool_cv.wait(lk, [&] { return !free_slots.empty() || slots.size() < max_slots; });
+    if (free_slots.empty()) {
+      auto s = std::make_unique<Slot>();
+      OZEC_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+      free_slots.push_back(s.get());
+      slots.push_back(std::move(s));
+    }
+    *out = free_slots.back();
+    free_slots.pop_back();
+    return OZEC_OK;
+  }
+
+  void release(Slot *s) {
+    {
+      std::lock_guard<std::mutex> lk(pool_mu);
+      free_slots.push_back(s);
+    }
+    pool_cv.notify_one();
+  }
+};
+
+struct SlotLease {
+  DevCtx *ctx;
+  Slot *slot = nullptr;
+  explicit SlotLease(DevCtx *c) : ctx(c) {}
+  ~SlotLease() {
+    if (slot) ctx->release(slot);
   }
 };
 
@@ -89,7 +137,6 @@ int get_ctx(DevCtx **out) {
   if (!g_ctx[dev]) {
     auto c = std::make_unique<DevCtx>();
     c->device = dev;
-    OZEC_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int t = 0; t < 2; ++t)
       for (int b = 0; b < 3; ++b) {
         const auto &blob = CrcMath::get(static_cast<CrcType>(t)).device_tables(1 << b);
@@ -216,6 +263,64 @@ void encode_rows(const ozec_coder *enc, std::vector<uint8_t> &rows) {
 
 int out_rows(const ozec_coder *enc) { return enc->codec == OZEC_CODEC_XOR ? 1 : enc->p; }
 
+
+// Host-buffer job through one staging slot, pipelined in chunks: while the GPU copies / codes / copies back
+// chunk c, this thread stages chunk c+1 (pageable -> pinned) and unstages chunk c-1 (pinned -> pageable).
+// Chunk-major staging layout, chunk c at c * per_chunk: [nin inputs x Cp][nout outputs x Op].
+//   launch(d_in, in_stride, d_out, out_stride, off, cl, stream) enqueues the kernel for bytes [off, off+cl)
+//   out_bytes(cl) / out_pos(off) give the output bytes a chunk produces and where they go in each output
+template <class Launch, class OutBytes, class OutPos>
+int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, size_t gran, int nout,
+                    uint8_t *const *out, OutBytes out_bytes, OutPos out_pos, Launch launch) {
+  constexpr size_t kMaxChunks = 64;
+  size_t chunk = static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.host_chunk));
+  chunk = std::max(chunk, (len + kMaxChunks - 1) / kMaxChunks);
+  chunk = std::max(gran, chunk / gran * gran);
+  if (chunk >= len) chunk = len;
+  const size_t nch = (len + chunk - 1) / chunk;
+  const size_t cp = round_up(chunk, kStageAlign), op = round_up(out_bytes(chunk), kStageAlign);
+  const size_t per_chunk = nin * cp + nout * op;
+  SlotLease lease(ctx);
+  if (int rc = ctx->acquire(&lease.slot)) return rc;
+  Slot *s = lease.slot;
+  if (int rc = s->reserve(per_chunk * nch, nch)) return rc;
+  auto unstage = [&](size_t c) -> int {
+    OZEC_HIP(hipEventSynchronize(s->events[c]));
+    const size_t off = c * chunk, cl = std::min(chunk, len - off);
+    const uint8_t *src = s->pinned + c * per_chunk + nin * cp;
+    for (int r = 0; r < nout; ++r) std::memcpy(out[r] + out_pos(off), src + r * op, out_bytes(cl));
+    return OZEC_OK;
+  };
+  for (size_t c = 0; c < nch; ++c) {
+    const size_t off = c * chunk, cl = std::min(chunk, len - off);
+    uint8_t *h = s->pinned + c * per_chunk, *d = s->dbuf + c * per_chunk;
+    for (int j = 0; j < nin; ++j) std::memcpy(h + j * cp, in[j] + off, cl);
+    OZEC_HIP(hipMemcpyAsync(d, h, nin * cp, hipMemcpyHostToDevice, s->stream));
+    OZEC_HIP(launch(d, static_cast<int64_t>(cp), d + nin * cp, static_cast<int64_t>(op), off, cl, s->stream));
+    OZEC_HIP(hipMemcpyAsync(h + nin * cp, d + nin * cp, nout * op, hipMemcpyDeviceToHost, s->stream));
+    OZEC_HIP(hipEventRecord(s->events[c], s->stream));
+    if (c > 0)
+      if (int rc = unstage(c - 1)) return rc;
+  }
+  return unstage(nch - 1);
+}
+
+// host-buffer coding job (encode / decode): rows outputs from nin inputs
+int staged_code(DevCtx *ctx, const CodeArgs &tmpl, const uint8_t *const *in, uint8_t *const *out, size_t len) {
+  return staged_pipeline(
+      ctx, tmpl.k, in, len, 4096, tmpl.rows, out, [](size_t cl) { return cl; }, [](size_t off) { return off; },
+      [&](uint8_t *d_in, int64_t in_stride, uint8_t *d_out, int64_t out_stride, size_t, size_t cl, hipStream_t st) {
+        CodeArgs a = tmpl;
+        a.in = d_in;
+        a.out = d_out;
+        a.nstripes = 1;
+        a.len = static_cast<int64_t>(cl);
+        for (int j = 0; j < a.k; ++j) a.in_off[j] = j * in_stride;
+        for (int r = 0; r < a.rows; ++r) a.out_off[r] = r * out_stride;
+        return ozec::launch_code(a, st);
+      });
+}
+
 }  // namespace
 
 extern "C" {
@@ -236,9 +341,7 @@ int ozec_set_device(int device) {
 }
 
 int ozec_synchronize(void) {
-  DevCtx *ctx;
-  if (int rc = get_ctx(&ctx)) return rc;
-  OZEC_HIP(hipStreamSynchronize(ctx->stream));
+  OZEC_HIP(hipDeviceSynchronize());
   return OZEC_OK;
 }
 
@@ -303,25 +406,11 @@ int ozec_encode(ozec_coder *enc, const uint8_t *const *inputs, uint8_t *const *o
   if (len == 0) return OZEC_OK;  // RawErasureEncoder.java:73-75
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
-  const size_t lp = round_up(len, kStageAlign);
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (int rc = ctx->reserve(lp * (k + rows))) return rc;
-  for (int j = 0; j < k; ++j) std::memcpy(ctx->pinned + j * lp, inputs[j], len);
-  OZEC_HIP(hipMemcpyAsync(ctx->dbuf, ctx->pinned, lp * k, hipMemcpyHostToDevice, ctx->stream));
   CodeArgs a{};
-  a.in = ctx->dbuf;
-  a.out = ctx->dbuf + lp * k;
-  a.nstripes = 1;
-  a.len = static_cast<int64_t>(len);
   std::vector<uint8_t> coef;
   encode_rows(enc, coef);
   fill_coef(a, rows, k, coef.data());
-  for (int j = 0; j < k; ++j) a.in_off[j] = static_cast<int64_t>(j * lp);
-  for (int r = 0; r < rows; ++r) a.out_off[r] = static_cast<int64_t>(r * lp);
-  OZEC_HIP(ozec::launch_code(a, ctx->stream));
-  OZEC_HIP(hipMemcpyAsync(ctx->pinned + lp * k, a.out, lp * rows, hipMemcpyDeviceToHost, ctx->stream));
-  OZEC_HIP(hipStreamSynchronize(ctx->stream));
-  for (int r = 0; r < rows; ++r) std::memcpy(outputs[r], ctx->pinned + lp * (k + r), len);
+  if (int rc = staged_code(ctx, a, inputs, outputs, len)) return rc;
   // XOR with p > 1: the reference zero-fills every output and writes only outputs[0] (XORRawEncoder.java:67-85)
   for (int r = rows; r < enc->p; ++r)
     if (outputs[r]) std::memset(outputs[r], 0, len);
@@ -406,29 +495,15 @@ int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased
   const int nin = static_cast<int>(units.size());
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
-  const size_t lp = round_up(len, kStageAlign);
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (int rc = ctx->reserve(lp * (nin + n_erased))) return rc;
-  for (int j = 0; j < nin; ++j) std::memcpy(ctx->pinned + j * lp, inputs[units[j]], len);
-  OZEC_HIP(hipMemcpyAsync(ctx->dbuf, ctx->pinned, lp * nin, hipMemcpyHostToDevice, ctx->stream));
   CodeArgs a{};
-  a.in = ctx->dbuf;
-  a.out = ctx->dbuf + lp * nin;
-  a.nstripes = 1;
-  a.len = static_cast<int64_t>(len);
   if (dec->codec == OZEC_CODEC_XOR) fill_coef(a, 1, nin, rows.data());
   else fill_coef(a, n_erased, nin, rows.data());
   if (int rc = check_limits(a.k, a.rows)) return rc;
-  for (int j = 0; j < nin; ++j) a.in_off[j] = static_cast<int64_t>(j * lp);
-  for (int r = 0; r < a.rows; ++r) a.out_off[r] = static_cast<int64_t>(r * lp);
-  OZEC_HIP(ozec::launch_code(a, ctx->stream));
-  OZEC_HIP(hipMemcpyAsync(ctx->pinned + lp * nin, a.out, lp * a.rows, hipMemcpyDeviceToHost, ctx->stream));
-  OZEC_HIP(hipStreamSynchronize(ctx->stream));
-  for (int r = 0; r < n_erased; ++r) {
-    // XOR decode: only erasedIndexes[0] is recovered, further outputs stay zero-filled (XORRawDecoder.java:45-61)
-    if (r < a.rows) std::memcpy(outputs[r], ctx->pinned + lp * (nin + r), len);
-    else std::memset(outputs[r], 0, len);
-  }
+  std::vector<const uint8_t *> in(nin);
+  for (int j = 0; j < nin; ++j) in[j] = inputs[units[j]];
+  if (int rc = staged_code(ctx, a, in.data(), outputs, len)) return rc;
+  // XOR decode: only erasedIndexes[0] is recovered, further outputs stay zero-filled (XORRawDecoder.java:45-61)
+  for (int r = a.rows; r < n_erased; ++r) std::memset(outputs[r], 0, len);
   return OZEC_OK;
 }
 
@@ -561,22 +636,20 @@ static int checksum_host(int checksum_type, const uint8_t *data, size_t len, siz
   if (!data || !out) return fail(OZEC_EINVAL, "null buffer");
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
-  const size_t nwin = (len + bpc - 1) / bpc;
-  const size_t lp = round_up(len, kStageAlign);
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  if (int rc = ctx->reserve(lp + nwin * sizeof(uint32_t))) return rc;
-  std::memcpy(ctx->pinned, data, len);
-  OZEC_HIP(hipMemcpyAsync(ctx->dbuf, ctx->pinned, len, hipMemcpyHostToDevice, ctx->stream));
-  CrcArgs a;
-  uint32_t *d_out = reinterpret_cast<uint32_t *>(ctx->dbuf + lp);
-  if (int rc = make_crc_args(ctx, checksum_type, ctx->dbuf, 0, 1, len, bpc, d_out, static_cast<int64_t>(nwin),
-                             big_endian, raw, &a))
-    return rc;
-  OZEC_HIP(ozec::launch_crc_windows(a, ctx->stream));
-  OZEC_HIP(hipMemcpyAsync(ctx->pinned + lp, d_out, nwin * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-  OZEC_HIP(hipStreamSynchronize(ctx->stream));
-  std::memcpy(out, ctx->pinned + lp, nwin * sizeof(uint32_t));
-  return OZEC_OK;
+  uint8_t *outs[1] = {reinterpret_cast<uint8_t *>(out)};
+  // chunks are whole windows, so every chunk's windows are the call's windows
+  const size_t gran = bpc >= 4096 ? bpc : (4096 + bpc - 1) / bpc * bpc;
+  return staged_pipeline(
+      ctx, 1, &data, len, gran, 1, outs, [bpc](size_t cl) { return (cl + bpc - 1) / bpc * sizeof(uint32_t); },
+      [bpc](size_t off) { return off / bpc * sizeof(uint32_t); },
+      [&](uint8_t *d_in, int64_t, uint8_t *d_out, int64_t, size_t, size_t cl, hipStream_t st) {
+        CrcArgs a;
+        const int64_t nw = static_cast<int64_t>((cl + bpc - 1) / bpc);
+        if (make_crc_args(ctx, checksum_type, d_in, 0, 1, cl, bpc, reinterpret_cast<uint32_t *>(d_out), nw,
+                          big_endian, raw, &a))
+          return hipErrorInvalidValue;
+        return ozec::launch_crc_windows(a, st);
+      });
 }
 
 int ozec_checksum_windows(int checksum_type, const uint8_t *data, size_t len, size_t bpc, uint32_t *out,
@@ -860,6 +933,8 @@ int ozec_set_tuning(const char *key, int64_t value) {
   else if (k == "crc_variant") ozec::g_tune.crc_variant = static_cast<int>(value);
   else if (k == "crc_grid") ozec::g_tune.crc_grid = value;
   else if (k == "unit_map") ozec::g_tune.unit_map = static_cast<int>(value);
+  else if (k == "host_chunk" && value > 0) ozec::g_tune.host_chunk = value;
+  else if (k == "host_slots" && value > 0) ozec::g_tune.host_slots = value;
   else return fail(OZEC_EINVAL, "unknown tuning key " + k);
   return OZEC_OK;
 }

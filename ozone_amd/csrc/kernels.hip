@@ -752,6 +752,10 @@ hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
     case 4: return launch_krv<K, R, 1, 2, 2>(a, st, kAll);
     case 5: return launch_krv<K, R, 2, 0, 0>(a, st, 8192);
     case 6: return launch_krv<K, R, 2, 2, 2>(a, st, 8192);
+    case 7: return launch_krv<K, R, 1, 2, 16>(a, st, kAll);   // sc1 (write-through) stores
+    case 8: return launch_krv<K, R, 1, 2, 18>(a, st, kAll);   // sc1 nt stores
+    case 9: return launch_krv<K, R, 1, 18, 18>(a, st, kAll);  // sc1 nt loads and stores
+    case 10: return launch_krv<K, R, 1, 16, 2>(a, st, kAll);  // sc1 loads
     default: break;
   }
   return launch_krv<K, R, 1, 2, 2>(a, st, kAll);

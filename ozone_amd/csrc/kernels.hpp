@@ -87,6 +87,8 @@ struct TuneKnobs {
                           //   8/9/10 = at least 5/6/8 waves per SIMD
   int64_t crc_grid = 0;   // blocks for the CRC / fused kernels
   int unit_map = 0;       // CodeArgs::unit_map for the coding kernels
+  int64_t host_chunk = 256 << 10;  // host-buffer calls: bytes per unit per pipelined chunk
+  int64_t host_slots = 8;          // host-buffer calls: staging slots (concurrent calls) per GPU
 };
 extern TuneKnobs g_tune;
 

@@ -324,3 +324,59 @@ def test_splitmix_fill_matches_cpu_twin():
     got = h(d)
     for c in range(3):
         assert (got[c, :n] == splitmix64_bytes(SEED, 77 + c, n)).all()
+
+
+def test_host_path_concurrent_threads_share_one_coder():
+    """RawErasureCoderBenchmark.java:201-206 shares one coder across threads; encode is not synchronized in the
+    reference, so the host path must be reentrant (ctypes releases the GIL during the call)."""
+    import threading
+    k, p, n = 6, 3, 65536 + 5
+    e = enc("rs", k, p)
+    d = dec("rs", k, p)
+    errors = []
+
+    def worker(tid):
+        try:
+            for it in range(6):
+                data = cells(SEED, 90000 + tid * 100 + it * k, k, n)
+                par = [np.zeros(n, np.uint8) for _ in range(p)]
+                e.encode(data, par)
+                ref = oracle.rs_encode(k, p, data)
+                assert all((a == b).all() for a, b in zip(par, ref))
+                ins = [None, None] + data[2:] + par[:2] + [None]
+                out = [np.zeros(n, np.uint8), np.zeros(n, np.uint8)]
+                d.decode(ins, [0, 1], out)
+                assert (out[0] == data[0]).all() and (out[1] == data[1]).all()
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append(repr(ex))
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join()
+    assert not errors, errors
+
+
+@pytest.mark.parametrize("chunk", [4096, 12288, 1 << 18])
+def test_host_path_chunked_pipeline(chunk):
+    """Host-buffer calls are staged in pipelined chunks (ozec_set_tuning "host_chunk"); odd lengths, chunk counts
+    above the 64-chunk cap and CRC windows that straddle the nominal chunk size must not change any byte."""
+    assert L.lib().ozec_set_tuning(b"host_chunk", chunk) == 0
+    try:
+        k, p, n = 6, 3, 700_001
+        data = cells(SEED, 95000, k, n)
+        par = [np.zeros(n, np.uint8) for _ in range(p)]
+        enc("rs", k, p).encode(data, par)
+        ref = oracle.rs_encode(k, p, data)
+        assert all((a == b).all() for a, b in zip(par, ref))
+        ins = [None] + data[1:] + [ref[0], None, ref[2]]
+        out = [np.zeros(n, np.uint8), np.zeros(n, np.uint8)]
+        dec("rs", k, p).decode(ins, [0, 7], out)
+        assert (out[0] == data[0]).all() and (out[1] == ref[1]).all()
+        for bpc in (1000, 16384, 5000):
+            cd = ck.Checksum(ck.ChecksumType.CRC32C, bpc).compute_checksum(data[2])
+            got = [int.from_bytes(b, "big") for b in cd.get_checksums()]
+            assert got == [int(x) for x in oracle.crc_windows(oracle.CRC32C, data[2], bpc)]
+    finally:
+        L.lib().ozec_set_tuning(b"host_chunk", 256 << 10)

@@ -688,10 +688,16 @@ int ozec_crc_update(int checksum_type, uint32_t *state, const uint8_t *data, siz
   if (int rc = crc_type_of(checksum_type, &t)) return rc;
   if (!state) return fail(OZEC_EINVAL, "null state");
   if (len == 0) return OZEC_OK;
-  uint32_t raw = 0;
-  if (int rc = checksum_host(checksum_type, data, len, len, &raw, 0, 1)) return rc;
-  // register after (state, data) = shift(state, len) ^ f(data)
-  *state = CrcMath::get(t).shift(*state, len) ^ raw;
+  // raw (zero-init, no final xor) CRCs of 16 KiB windows computed in parallel on the GPU, folded on the host:
+  // register after (reg, w) = shift(reg, |w|) ^ f(w)
+  constexpr size_t kWin = 16384;
+  const size_t nwin = (len + kWin - 1) / kWin;
+  std::vector<uint32_t> raw(nwin);
+  if (int rc = checksum_host(checksum_type, data, len, kWin, raw.data(), 0, 1)) return rc;
+  const CrcMath &cm = CrcMath::get(t);
+  uint32_t reg = *state;
+  for (size_t i = 0; i < nwin; ++i) reg = cm.shift(reg, std::min(kWin, len - i * kWin)) ^ raw[i];
+  *state = reg;
   return OZEC_OK;
 }
 

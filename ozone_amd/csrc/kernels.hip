@@ -411,7 +411,7 @@ __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
   load_tables(s_t, a.tables[g5_slot(B)], kG5Words);
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: unit index lives in SGPRs
   const int64_t units = a.ncells * a.nwin;
   const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   for (int64_t u = bid * (kBlock / 64) + wave; u < units; u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
@@ -424,32 +424,40 @@ __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
     const int64_t P = T * 64 * B - m;  // virtual zero blocks in front
     const uint8_t *win = a.base + c * a.cell_stride + w * a.bpc;
     uint32_t S = 0;
-    uint4 cur[B], nxt[B];
-    auto load_step = [&](int64_t t, uint4 (&dst)[B]) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    // step t's blocks; only step 0 holds virtual (front-padding) blocks, so only it needs the lane predicate
+    auto load_step = [&](int64_t t, uint4 (&dst)[B], bool pad) {
 #pragma unroll
       for (int q = 0; q < B; ++q) {
         const int64_t vb = t * 64 * B + lane * B + q - P;
-        dst[q] = make_uint4(0, 0, 0, 0);
-        if (t < T && vb >= 0) {
-          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        if (!pad || vb >= 0) {
           const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(win + vb * 16));
           dst[q] = make_uint4(d[0], d[1], d[2], d[3]);
+        } else {
+          dst[q] = make_uint4(0, 0, 0, 0);
         }
       }
     };
-    load_step(0, cur);
-    for (int64_t t = 0; t < T; ++t) {
-      load_step(t + 1, nxt);
+    auto fold_step = [&](int64_t t, const uint4 (&src)[B]) {
       if (t > 0) S = g5_shift(s_t + kG5Step, S);
 #pragma unroll
       for (int q = 0; q < B; ++q) {
-        uint4 b = cur[q];
+        uint4 b = src[q];
         b.x ^= S;
         S = g5_block(s_t, b);
       }
-#pragma unroll
-      for (int q = 0; q < B; ++q) cur[q] = nxt[q];
+    };
+    // two register sets used alternately (no copies between steps), next step's loads in flight
+    uint4 xa[B], xb[B];
+    load_step(0, xa, true);
+    int64_t t = 0;
+    for (; t + 1 < T; t += 2) {
+      load_step(t + 1, xb, false);
+      fold_step(t, xa);
+      if (t + 2 < T) load_step(t + 2, xa, false);
+      fold_step(t + 1, xb);
     }
+    if (t < T) fold_step(t, xa);
     S = g5_lane_tree(s_t, S, lane);
     for (int64_t i = m * 16; i < N; ++i) S = (S >> 8) ^ s_t[kG5T0 + ((S ^ win[i]) & 0xff)];
     if (lane == 0) crc_emit(a, c, w, S, last);
@@ -502,7 +510,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
   }
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: unit index lives in SGPRs
   const int64_t nwin = cr.nwin;
   const int64_t units = a.nstripes * nwin;
   const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
@@ -521,12 +529,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     for (int q = 0; q < K + R; ++q) S[q] = 0;
     uint4 x[B][K], xn[PF ? B : 1][K];
     auto load = [&](int64_t t, uint4 (&dst)[B][K]) {
+      const bool pad = t == 0 && P > 0;  // wave-uniform: only step 0 holds virtual front blocks
 #pragma unroll
       for (int q = 0; q < B; ++q) {
         const int64_t vb = t * 64 * B + lane * B + q - P;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          if (t < T && vb >= 0) {
+          if (t < T && (!pad || vb >= 0)) {
             const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<uint32_t>(vb) * 16u,
                                                                  static_cast<int>(a.in_off[j]), 2);
             dst[q][j] = make_uint4(d[0], d[1], d[2], d[3]);

@@ -228,6 +228,20 @@ def test_streaming_checksum_prefixes():
         assert s.get_value() == oracle.crc(otype, data[:1])
 
 
+def test_streaming_checksum_large_updates():
+    """Multi-window streaming updates (the GPU computes 16 KiB window registers, the host folds them): random
+    split points across window boundaries must equal the one-shot CRC."""
+    n = 3 * 16384 + 4321
+    data = cells(SEED, 42100, 1, n)[0]
+    rng = np.random.default_rng(5)
+    cuts = sorted(set([0, n] + rng.integers(1, n, 6).tolist() + [16384, 16385, 2 * 16384 - 1]))
+    for ctype, otype in ((ck.ChecksumType.CRC32, oracle.CRC32), (ck.ChecksumType.CRC32C, oracle.CRC32C)):
+        s = ck.ChecksumByteBuffer(ctype)
+        for a, b in zip(cuts, cuts[1:]):
+            s.update(data, a, b - a)
+            assert s.get_value() == oracle.crc(otype, data[:b]), (ctype, b)
+
+
 def test_checksum_impls_compute_same_values_64mib():
     """TestChecksumImplsComputeSameValues.java:39-101 scale: 64 MiB random, several bpc."""
     n = 64 << 20

@@ -488,7 +488,10 @@ __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
 // every data unit (lanes interleaved, 64*B blocks per step), produces the parity blocks and folds all K+R
 // units into their CRC registers while the bytes are in VGPRs.  PF: issue the next step's loads before
 // computing the current one.  Coefficient tables as in gf_code_vec (SREG: SGPR/VGPR split, else LDS).
-template <int K, int R, bool SREG, int B, bool PF, int WAVES = 1>
+// XORC (all-ones single row: the XOR codec): the output is the XOR of the inputs, and since the raw CRC
+// register recursion is GF(2)-linear in (register, data), the output's register is the XOR of the inputs'
+// registers at every step -- its CRC costs no table lookups.
+template <int K, int R, bool SREG, int B, bool PF, int WAVES = 1, bool XORC = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_vec(
     const EncCrcArgs e, const TabArgs<K * R> tabs) {
   __shared__ __attribute__((aligned(16))) uint32_t s_t[kG5Words];
@@ -561,6 +564,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int j = 0; j < K; ++j) {
+          if constexpr (XORC) {
+            acc[0].x ^= x[q][j].x;
+            acc[0].y ^= x[q][j].y;
+            acc[0].z ^= x[q][j].z;
+            acc[0].w ^= x[q][j].w;
+            continue;
+          }
           const Sel sx = make_sel(x[q][j].x), sy = make_sel(x[q][j].y), sz = make_sel(x[q][j].z),
                     sw = make_sel(x[q][j].w);
 #pragma unroll
@@ -596,7 +606,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         }
         // CRC: the first block of a step jumps the register (63*B)*16 bytes, then every block folds in
 #pragma unroll
-        for (int j = 0; j < K + R; ++j) {
+        for (int j = 0; j < (XORC ? K : K + R); ++j) {
           uint4 b = j < K ? x[q][j] : acc[j - K];
           if (q == 0) b.x ^= t > 0 ? g5_shift(s_t + kG5Step, S[j]) : 0u;
           else b.x ^= S[j];
@@ -610,6 +620,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 #pragma unroll
           for (int j = 0; j < K; ++j) x[q][j] = xn[q][j];
       }
+    }
+    if constexpr (XORC) {
+      S[K] = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) S[K] ^= S[j];
     }
     const uint32_t init = last ? cr.init_last : cr.init_full;
 #pragma unroll
@@ -860,6 +875,12 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
   const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : (units + 3) / 4;
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
   constexpr bool kS = K * R <= 18;
+  if constexpr (R == 1) {
+    if (e.code.all_ones && g_tune.crc_variant != 2) {
+      hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 1, true>), grid, block, 0, st, e, tabs);
+      return hipGetLastError();
+    }
+  }
   if constexpr (K == 6 && R == 3) {  // the headline shape carries the tuning variants (scripts/tune_crc.py)
     switch (g_tune.crc_variant) {
       case 3: hipLaunchKernelGGL((encode_crc_vec<K, R, kS, 1, false>), grid, block, 0, st, e, tabs); break;

@@ -83,8 +83,8 @@ constexpr int g5_slot(int B) { return B == 1 ? 0 : B == 2 ? 1 : 2; }
 struct TuneKnobs {
   int64_t grid = 0;       // blocks for the coding kernels
   int gf_variant = 0;     // coding-kernel variant 1..6 (VPT / cache policy), see launch_kr
-  int crc_variant = 0;    // CRC kernel: 1/4 = B (default 2); fused: 3 SGPR tables, 5 prefetch, 6 B = 2, 7 both,
-                          //   8/9/10 = at least 5/6/8 waves per SIMD
+  int crc_variant = 0;    // CRC kernel: 1/4 = B (default 2); fused: 2 no XOR-codec register shortcut,
+                          //   3 SGPR tables, 5 prefetch, 6 B = 2, 7 both, 8 = at least 5 waves per SIMD
   int64_t crc_grid = 0;   // blocks for the CRC / fused kernels
   int unit_map = 0;       // CodeArgs::unit_map for the coding kernels
   int64_t host_chunk = 256 << 10;  // host-buffer calls: bytes per unit per pipelined chunk

@@ -266,7 +266,9 @@ def test_checksum_impls_compute_same_values_64mib():
 @pytest.mark.parametrize("k,p,codec,n,bpc,S", [(6, 3, "rs", 1 << 20, 16384, 4), (3, 2, "rs", 1 << 20, 16384, 2),
                                                (10, 4, "rs", 1 << 18, 16384, 3), (2, 1, "xor", 1 << 20, 16384, 3),
                                                (6, 3, "rs", 65536, 4096, 3), (6, 3, "rs", 1040 * 16, 1040, 2),
-                                               (6, 3, "rs", 50000, 16384, 2), (5, 2, "rs", 65536, 16384, 2)])
+                                               (6, 3, "rs", 50000, 16384, 2), (5, 2, "rs", 65536, 16384, 2),
+                                               (6, 1, "xor", 65536, 4096, 2), (3, 1, "xor", 50000, 16384, 2),
+                                               (10, 1, "xor", 1 << 17, 16384, 2), (6, 1, "rs", 65536, 16384, 2)])
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
 def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
     data = np.stack([np.stack(cells(SEED, 50000 + s * k, k, n)) for s in range(S)])

@@ -1,24 +1,41 @@
-"""Copy the last gpu_check.sh outputs from gpurun_out/ into profiles/<tag>/ and refresh profiles/traffic_c2.json."""
+"""Copy a scripts/gpu_full.sh session from gpurun_out/full/ into profiles/<tag>/ and refresh
+profiles/traffic_<workload>.json (HBM bytes per launch of each workload's dominant kernel, from PMC)."""
 import csv, json, os, shutil, sys
+
 tag = sys.argv[1]
-G, P = "gpurun_out", os.path.join("profiles", tag)
+G, P = os.path.join("gpurun_out", "full"), os.path.join("profiles", tag)
 os.makedirs(P, exist_ok=True)
-for w in ("c2", "c3", "c3r", "c4", "c5", "crc", "e2e"):
+KERNEL = {"c2": "gf_code_vec", "c3": "gf_code_vec", "c3r": "encode_crc_vec", "c4": "encode_crc_vec",
+          "c5": "encode_crc_vec", "crc": "crc_windows_vec"}
+for w in ("c2", "c3", "c3r", "c4", "c5", "crc", "e2e", "host"):
     if os.path.exists(f"{G}/bench_{w}.json"):
         shutil.copy(f"{G}/bench_{w}.json", f"{P}/bench_{w}.json")
-shutil.copy(f"{G}/prof_c2/run_kernel_stats.csv", f"{P}/c2_kernel_stats.csv")
-for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    shutil.copy(f"{G}/pmc_c2_{c}/run_counter_collection.csv", f"{P}/c2_pmc_{c}.csv")
 shutil.copy(f"{G}/pytest_gpu.log", f"{P}/pytest_gpu.log")
-def mean(path, ctr):
-    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if "gf_code_vec" in r["Kernel_Name"] and r["Counter_Name"] == ctr]
-    return sum(v) / len(v)
-f, w = mean(f"{P}/c2_pmc_FETCH_SIZE.csv", "FETCH_SIZE"), mean(f"{P}/c2_pmc_WRITE_SIZE.csv", "WRITE_SIZE")
-kname = [r["Name"] for r in csv.DictReader(open(f"{P}/c2_kernel_stats.csv")) if "gf_code_vec" in r["Name"]][0]
-avg = [float(r["AverageNs"]) for r in csv.DictReader(open(f"{P}/c2_kernel_stats.csv")) if "gf_code_vec" in r["Name"]][0]
-out = {"workload": "c2", "kernel": kname, "rocprof_average_ns": avg, "FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w,
-       "correction": "gfx950 FETCH_SIZE reports 1/2 of wide coalesced streaming reads (MI355X_MICROARCH.md HBM): bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
-       "hbm_bytes_per_launch": int(round((2 * f + w) * 1024)),
-       "source": f"profiles/{tag}/c2_pmc_{{FETCH,WRITE}}_SIZE.csv (rocprofv3 --pmc, separate passes, bench.py --steps 3)"}
-json.dump(out, open("profiles/traffic_c2.json", "w"), indent=1)
-print(json.dumps(out))
+
+
+def rows(path):
+    return list(csv.DictReader(open(path)))
+
+
+for w, pat in KERNEL.items():
+    stats = f"{G}/prof_{w}/run_kernel_stats.csv"
+    if not os.path.exists(stats):
+        continue
+    shutil.copy(stats, f"{P}/{w}_kernel_stats.csv")
+    ctr = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        src = f"{G}/pmc_{w}_{c}/run_counter_collection.csv"
+        shutil.copy(src, f"{P}/{w}_pmc_{c}.csv")
+        v = [float(r["Counter_Value"]) for r in rows(src) if pat in r["Kernel_Name"] and r["Counter_Name"] == c]
+        ctr[c] = sum(v) / len(v)
+    k = [r for r in rows(stats) if pat in r["Name"]][0]
+    bench = json.loads(open(f"{P}/bench_{w}.json").read().strip().splitlines()[-1])
+    out = {"workload": w, "kernel": k["Name"], "rocprof_average_ns": float(k["AverageNs"]),
+           "bench_kernel_ms": bench["roofline"]["kernel_ms"], "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+           "FETCH_SIZE_KiB": ctr["FETCH_SIZE"], "WRITE_SIZE_KiB": ctr["WRITE_SIZE"],
+           "correction": "gfx950 FETCH_SIZE reports 1/2 of wide coalesced streaming reads (MI355X_MICROARCH.md HBM): "
+                         "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
+           "hbm_bytes_per_launch": int(round((2 * ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024)),
+           "source": f"profiles/{tag}/{w}_pmc_{{FETCH,WRITE}}_SIZE.csv (rocprofv3 --pmc, separate passes)"}
+    json.dump(out, open(f"profiles/traffic_{w}.json", "w"), indent=1)
+    print(json.dumps({x: out[x] for x in ("workload", "rocprof_average_ns", "bench_kernel_ms", "alg_bytes_per_launch", "hbm_bytes_per_launch")}))

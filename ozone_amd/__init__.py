@@ -8,7 +8,8 @@ mirror of the reference's plugin interfaces:
 from . import _lib  # noqa: F401
 from .bytebuffer import ByteBuffer, ECChunk  # noqa: F401
 from .checksum import Checksum, ChecksumByteBuffer, ChecksumData, ChecksumType, OzoneChecksumException  # noqa: F401
-from .rawcoder import (CodecRegistry, CodecUtil, ECReplicationConfig, HadoopIllegalArgumentException,  # noqa: F401
+from .rawcoder import (CodecRegistry, CodecUtil, DummyRawDecoder, DummyRawEncoder,  # noqa: F401
+                       DummyRawErasureCoderFactory, ECReplicationConfig, HadoopIllegalArgumentException,
                        HipRSRawErasureCoderFactory, HipXORRawErasureCoderFactory, IllegalArgumentException,
                        IOException, RawErasureDecoder, RawErasureEncoder)
 

@@ -397,6 +397,39 @@ class RawErasureDecoder(_Coder):
             _raise_for(rc)
 
 
+# ---------------------------------------------------------------- dummy coder ----------------------------
+
+class DummyRawEncoder(RawErasureEncoder):
+    """DummyRawEncoder (EC/rawcoder/DummyRawEncoder.java:30-45): the inherited validation and position
+    bookkeeping run, the coding step does nothing -- the framework-overhead floor of the benchmark.
+    Host-only: it never touches the GPU library."""
+
+    def __init__(self, config):  # no native handle
+        self._config = config
+        self._handle = None
+
+    def _run(self, in_addrs, out_addrs, n):
+        pass  # "Nothing to do. Output buffers have already been reset"
+
+    def release(self):
+        pass  # RawErasureEncoder.release: "Nothing to do here."
+
+
+class DummyRawDecoder(RawErasureDecoder):
+    """DummyRawDecoder (EC/rawcoder/DummyRawDecoder.java): validation only, no decoding."""
+
+    def __init__(self, config):
+        self._config = config
+        self._handle = None
+        self._lock = threading.Lock()
+
+    def _run(self, in_addrs, erased, out_addrs, n):
+        pass
+
+    def release(self):
+        pass
+
+
 # ---------------------------------------------------------------- factories / registry -------------------
 
 class RawErasureCoderFactory:
@@ -416,6 +449,18 @@ class RawErasureCoderFactory:
 
     def get_codec_name(self):
         return self.codec_name
+
+
+class DummyRawErasureCoderFactory(RawErasureCoderFactory):
+    """DummyRawErasureCoderFactory (EC/rawcoder/DummyRawErasureCoderFactory.java:27-52)."""
+    coder_name = "dummy_dummy"
+    codec_name = "dummy"
+
+    def create_encoder(self, config):
+        return DummyRawEncoder(config)
+
+    def create_decoder(self, config):
+        return DummyRawDecoder(config)
 
 
 class HipRSRawErasureCoderFactory(RawErasureCoderFactory):

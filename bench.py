@@ -13,7 +13,7 @@ value      = data bytes of all ranks / max-over-ranks wall time of the K timed s
 roofline   = algorithmic bytes per launch (9 x 1 MiB per stripe x 4096) / mean kernel time measured with
              HIP events on the launch stream, against 8.0 TB/s; traffic = rocprofv3 PMC bytes per launch
              read from profiles/traffic_<workload>.json when it has been measured, else null
-cpu_baseline (rank 0, N = 1): the oracle/ C port of RSUtil.encodeData timed on this host's cores on a
+cpu_baseline (rank 0, N = 1): the oracle/ C restatement of the same work timed on this host's cores on a
              bounded sample (threads share one coder, as RawErasureCoderBenchmark.java:201-206 does)
 """
 import argparse
@@ -216,20 +216,50 @@ class Workload:
 # ------------------------------------------------------------------------------------------ CPU baseline
 
 
-def cpu_baseline(budget_s):
-    """oracle/ (C port of RSUtil.encodeData) on this host: T threads share one coder; bounded sample."""
+def cpu_baseline(workload, budget_s):
+    """oracle/ (C restatement of the reference path, gcc -O3) timed on this host's cores on a bounded sample of
+    the workload: T threads share one coder (RawErasureCoderBenchmark.java:201-206), each repeating one unit of
+    work (a stripe, a decode, a cell's windows) until the wall budget is spent."""
     import oracle
     from synth import cells
     threads = min(16, os.cpu_count() or 1)
-    k, p, n = 6, 3, MIB
-    data = cells(SEED, 900, k, n)
-    oracle.rs_encode(k, p, data)  # warm the tables
+    n = MIB
+    if workload == "c3":
+        k, p, erased = 10, 4, [0, 1, 2, 3]
+        d = cells(SEED, 900, k, n)
+        units = d + oracle.rs_encode(k, p, d)
+        ins = [None if u in erased else units[u] for u in range(k + p)]
+        job, data_bytes = (lambda: oracle.rs_decode(k, p, ins, erased)), k * n
+        what = "rs-10-4-1024k decodes of 4 erased units (oracle rs_decode: RSRawDecoder + RSUtil.encodeData)"
+    elif workload == "crc":
+        cell = cells(SEED, 900, 1, n)[0]
+        job, data_bytes = (lambda: oracle.crc_windows(oracle.CRC32C, cell, 16384)), n
+        what = "1 MiB cells checksummed as CRC32C/16 KiB windows (oracle crc_windows: CrcIntTable slice-by-8)"
+    elif workload in ("c4", "c5", "c3r"):
+        k, p = (2, 1) if workload == "c4" else (10, 4) if workload == "c3r" else (6, 3)
+        d = cells(SEED, 900, k, n)
+
+        def job():
+            par = oracle.rs_encode(k, p, d) if workload != "c4" else [oracle.xor_encode(d)]
+            for u in d + par:
+                oracle.crc_windows(oracle.CRC32C, u, 16384)
+        data_bytes = k * n
+        what = {"c4": "xor-2-1-1024k stripes coded + CRC32C/16 KiB of all 3 units",
+                "c5": "rs-6-3-1024k stripes coded + CRC32C/16 KiB of all 9 units",
+                "c3r": "rs-10-4-1024k stripes, 10 units -> 4 rebuilt + CRC32C/16 KiB of all 14 units (the "
+                       "reconstruction's work)"}[workload] + " (oracle coder + crc_windows)"
+    else:
+        k, p = 6, 3
+        d = cells(SEED, 900, k, n)
+        job, data_bytes = (lambda: oracle.rs_encode(k, p, d)), k * n
+        what = "rs-6-3-1024k stripes encoded (oracle rs_encode: C restatement of RSUtil.encodeData)"
+    job()  # warm the tables
     done = [0] * threads
     stop = time.perf_counter() + budget_s
 
     def worker(i):
         while time.perf_counter() < stop:
-            oracle.rs_encode(k, p, data)
+            job()
             done[i] += 1
 
     ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
@@ -239,10 +269,9 @@ def cpu_baseline(budget_s):
     for t in ts:
         t.join()
     el = time.perf_counter() - t0
-    stripes = sum(done)
-    return {"value": round(stripes * k * n / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"{stripes} rs-6-3-1024k stripes encoded by {threads} threads sharing one coder in "
-                      f"{el:.1f} s wall (oracle/ozec_oracle.c, C restatement of RSUtil.encodeData, gcc -O3)"}
+    units = sum(done)
+    return {"value": round(units * data_bytes / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{units} {what}, {threads} threads sharing one coder, {el:.1f} s wall (gcc -O3)"}
 
 
 # ------------------------------------------------------------------------------------------ main
@@ -313,8 +342,8 @@ def main():
                      "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": wl.alg_bytes},
     }
-    if rank == 0 and world == 1 and not args.no_cpu and args.workload in ("c2", "e2e", "host"):
-        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

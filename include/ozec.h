@@ -186,6 +186,39 @@ int ozec_parse_replication(const char *s, int *codec, int *num_data, int *num_pa
 /* crc(A||B) from crc(A), crc(B), |B| -- the combine primitive behind streaming update and stripe checksums */
 uint32_t ozec_crc_combine(int checksum_type, uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
+/* ---- COMPOSITE_CRC: CrcUtil / CrcComposer ------------------------------------------
+ * OC/ = hadoop-ozone/common/src/main/java/org/apache/hadoop/ozone/client/checksum/.  CRC values are the stored
+ * ints ((int)getValue()) in CrcUtil's reversed representation; checksum_type is OZEC_CHECKSUM_CRC32/CRC32C
+ * (CrcUtil.getCrcPolynomialForType, OC/CrcUtil.java:53-64). */
+/* CrcUtil.getMonomial (OC/CrcUtil.java:74-98): x^(8*len) mod P; OZEC_EINVAL for len < 0 */
+int ozec_crc_monomial(int checksum_type, int64_t len_bytes, uint32_t *out);
+/* CrcUtil.compose (OC/CrcUtil.java:124-127): crc_a * x^(8*len_b) xor crc_b; OZEC_EINVAL for len_b < 0 */
+int ozec_crc_compose(int checksum_type, uint32_t crc_a, uint32_t crc_b, int64_t len_b, uint32_t *out);
+/* CrcComposer (OC/CrcComposer.java:44-215).  stripe_length <= 0 means unstriped (newCrcComposer, :61-66);
+ * otherwise newStripedCrcComposer (:84-95): one 4-byte big-endian CRC is emitted per stripe_length bytes. */
+typedef struct ozec_crc_composer ozec_crc_composer;
+int ozec_crc_composer_create(int checksum_type, int64_t bytes_per_crc_hint, int64_t stripe_length,
+                             ozec_crc_composer **out);
+/* update(int crcB, long bytesPerCrc) (:168-199): OZEC_EINVAL for a negative length, OZEC_EMISMATCH when the
+ * position passes stripe_length without landing on it (the reference's IOException) */
+int ozec_crc_composer_update(ozec_crc_composer *c, uint32_t crc, int64_t bytes_per_crc);
+/* update(byte[] crcBuffer, int offset, int length, long bytesPerCrc) (:124-139): big-endian 4-byte CRCs,
+ * OZEC_EINVAL unless len % 4 == 0 */
+int ozec_crc_composer_update_bytes(ozec_crc_composer *c, const uint8_t *crc_bytes, size_t len, int64_t bytes_per_crc);
+/* bytes the next digest returns */
+size_t ozec_crc_composer_pending(const ozec_crc_composer *c);
+/* digest() (:205-214): flush a partial stripe, copy the digest into out (OZEC_EINVAL if cap is too small,
+ * nothing is consumed then), reset */
+int ozec_crc_composer_digest(ozec_crc_composer *c, uint8_t *out, size_t cap, size_t *len);
+void ozec_crc_composer_free(ozec_crc_composer *c);
+/* Device batch: CrcComposer over each cell's window CRCs, in order: d_crcs[cell * crc_cell_stride + w] for
+ * w < num_windows, every window bpc bytes long except the last (last_len bytes) -> d_out[cell].  This is the
+ * chunk/block composite CRC of ECBlockChecksumComputer.computeCompositeCrc (client/checksum/
+ * ECBlockChecksumComputer.java:105-195) over GPU-produced window CRCs; it equals the CRC of the whole cell. */
+int ozec_crc_compose_windows_batch(int checksum_type, const uint32_t *d_crcs, int64_t crc_cell_stride,
+                                   size_t num_cells, size_t num_windows, size_t bpc, size_t last_len,
+                                   int crcs_big_endian, uint32_t *d_out, int out_big_endian, void *stream);
+
 /* ---- harness utilities ------------------------------------------------------------------------------- */
 /* process-wide tuning knobs for benchmarking: kernels ("grid", "gf_variant", "crc_variant", "crc_grid",
  * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_slots") */

@@ -156,3 +156,109 @@ def crc_windows(ctype, data, bpc):
     out = np.zeros(max(1, nw), np.uint32)
     lib().oracle_crc_windows(ctype, _ptr(a), a.size, bpc, _ptr(out))
     return out[:nw]
+
+
+# ---------------------------------------------------------------- COMPOSITE_CRC (ozec_oracle.c) ---------------
+
+def _composite_lib():
+    L = lib()
+    if not getattr(L, "_composite_ready", False):
+        L.oracle_crc_poly.restype = ctypes.c_uint32
+        L.oracle_gf32_multiply.restype = ctypes.c_uint32
+        L.oracle_gf32_multiply.argtypes = [ctypes.c_uint32] * 3
+        L.oracle_crc_monomial.argtypes = [ctypes.c_int64, ctypes.c_uint32, _u32p]
+        L.oracle_crc_compose.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64, ctypes.c_uint32, _u32p]
+        L.oracle_composer_new.restype = ctypes.c_void_p
+        L.oracle_composer_new.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
+        L.oracle_composer_update.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64]
+        L.oracle_composer_digest.restype = ctypes.c_size_t
+        L.oracle_composer_digest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_composer_free.argtypes = [ctypes.c_void_p]
+        L.oracle_composer_pending.restype = ctypes.c_size_t
+        L.oracle_composer_pending.argtypes = [ctypes.c_void_p]
+        L._composite_ready = True
+    return L
+
+
+def crc_monomial(ctype, length):
+    out = ctypes.c_uint32()
+    L = _composite_lib()
+    if L.oracle_crc_monomial(length, L.oracle_crc_poly(ctype), ctypes.byref(out)):
+        raise ValueError(f"lengthBytes must be positive, got {length}")
+    return out.value
+
+
+def crc_compose(ctype, crc_a, crc_b, len_b):
+    """CrcUtil.compose (OC/CrcUtil.java:124-127)."""
+    out = ctypes.c_uint32()
+    L = _composite_lib()
+    if L.oracle_crc_compose(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b, L.oracle_crc_poly(ctype), ctypes.byref(out)):
+        raise ValueError(f"lengthBytes must be positive, got {len_b}")
+    return out.value
+
+
+class Composer:
+    """CrcComposer (OC/CrcComposer.java:44-215) through ozec_oracle.c."""
+
+    def __init__(self, ctype, bytes_per_crc_hint, stripe_length=(1 << 63) - 1):
+        self._L = _composite_lib()
+        self._c = self._L.oracle_composer_new(ctype, bytes_per_crc_hint, stripe_length)
+
+    def update(self, crc, bytes_per_crc):
+        rc = self._L.oracle_composer_update(self._c, crc & 0xFFFFFFFF, bytes_per_crc)
+        if rc == -1:
+            raise ValueError(f"lengthBytes must be positive, got {bytes_per_crc}")
+        if rc == -2:
+            raise OSError("Current position in stripe exceeds stripeLength without stripe alignment.")
+
+    def digest(self):
+        buf = ctypes.create_string_buffer(max(4, self._L.oracle_composer_pending(self._c)))
+        n = self._L.oracle_composer_digest(self._c, buf, len(buf))
+        return buf.raw[:n]
+
+    def __del__(self):
+        if getattr(self, "_c", None):
+            self._L.oracle_composer_free(self._c)
+            self._c = None
+
+
+def read_int(b, off=0):
+    v = int.from_bytes(bytes(b[off:off + 4]), "big")
+    return v
+
+
+def replicated_block_composite_crc(ctype, chunks, bytes_per_crc):
+    """ReplicatedBlockChecksumComputer.computeCompositeCrc (client/checksum/ReplicatedBlockChecksumComputer.java:
+    94-148). chunks: list of (chunk_len, [window crc ints]); the first chunk's length is the block hint."""
+    block = Composer(ctype, chunks[0][0])
+    for chunk_len, crcs in chunks:
+        cc = Composer(ctype, bytes_per_crc)
+        remaining = chunk_len
+        for c in crcs:
+            cc.update(c, min(bytes_per_crc, remaining))
+            remaining -= bytes_per_crc
+        block.update(read_int(cc.digest()), chunk_len)
+    return block.digest()
+
+
+def ec_block_composite_crc(ctype, stripe_checksums, chunk_size, bytes_per_crc, key_size, num_parity):
+    """ECBlockChecksumComputer.computeCompositeCrc (client/checksum/ECBlockChecksumComputer.java:105-195).
+    stripe_checksums: list of bytes (the concatenated 4-B BE window CRCs of a stripe, parity units last)."""
+    offset = chunk_size % bytes_per_crc
+    parity_bytes = -(-chunk_size // bytes_per_crc) * 4 * num_parity
+    per_chunk = -(-chunk_size // bytes_per_crc)
+    block = Composer(ctype, bytes_per_crc)
+    for sc in stripe_checksums:
+        assert len(sc) % 4 == 0
+        body = sc[:len(sc) - parity_bytes]
+        idx = 1
+        for off in range(0, len(body), 4):
+            cur_off = offset if (idx % per_chunk == 0 and offset > 0) else (1 << 63) - 1
+            crc = read_int(body, off)
+            size = min(min(key_size, bytes_per_crc), cur_off)
+            cc = Composer(ctype, bytes_per_crc)
+            cc.update(crc, size)
+            block.update(read_int(cc.digest()), size)
+            key_size -= min(bytes_per_crc, cur_off)
+            idx += 1
+    return block.digest()

@@ -318,3 +318,122 @@ size_t oracle_crc_windows(int type, const uint8_t *data, size_t n, size_t bpc, u
   }
   return w;
 }
+
+/* ---------------------------------------------------------------- COMPOSITE_CRC ---------------- */
+/* OC/ = hadoop-ozone/common/src/main/java/org/apache/hadoop/ozone/client/checksum/
+ * CRC values here are the stored ints ((int)getValue()), in the reference's "reversed" representation:
+ * bit 31 is the x^0 coefficient, bit 0 the x^31 one; MULTIPLICATIVE_IDENTITY = 0x80000000 (OC/CrcUtil.java:34). */
+
+/* CrcUtil.getCrcPolynomialForType, OC/CrcUtil.java:53-64 */
+uint32_t oracle_crc_poly(int type) { return type == 0 ? 0xEDB88320u : 0x82F63B78u; }
+
+/* CrcUtil.galoisFieldMultiply, OC/CrcUtil.java:249-270: p * q mod m, bit-serial */
+uint32_t oracle_gf32_multiply(uint32_t p, uint32_t q, uint32_t m) {
+  uint32_t summation = 0, cur_term = 0x80000000u, px = p;
+  while (cur_term != 0) {
+    if (q & cur_term) summation ^= px;
+    int has_max_degree = (px & 1) != 0;
+    px >>= 1;
+    if (has_max_degree) px ^= m;
+    cur_term >>= 1;
+  }
+  return summation;
+}
+
+/* CrcUtil.getMonomial, OC/CrcUtil.java:74-98: x^(8*len) mod m by square-and-multiply from x^8.
+ * Returns -1 (IllegalArgumentException) for len < 0. */
+int oracle_crc_monomial(int64_t len, uint32_t m, uint32_t *out) {
+  if (len == 0) { *out = 0x80000000u; return 0; }
+  if (len < 0) return -1;
+  uint32_t multiplier = 0x80000000u >> 8, product = 0x80000000u;
+  int64_t degree = len;
+  while (degree > 0) {
+    if (degree & 1) product = product == 0x80000000u ? multiplier : oracle_gf32_multiply(product, multiplier, m);
+    multiplier = oracle_gf32_multiply(multiplier, multiplier, m);
+    degree >>= 1;
+  }
+  *out = product;
+  return 0;
+}
+
+/* CrcUtil.compose / composeWithMonomial, OC/CrcUtil.java:110-127 */
+int oracle_crc_compose(uint32_t crc_a, uint32_t crc_b, int64_t len_b, uint32_t m, uint32_t *out) {
+  uint32_t mono;
+  if (oracle_crc_monomial(len_b, m, &mono)) return -1;
+  *out = oracle_gf32_multiply(crc_a, mono, m) ^ crc_b;
+  return 0;
+}
+
+/* CrcComposer, OC/CrcComposer.java:44-215 */
+typedef struct {
+  uint32_t poly, mono_hint;
+  int64_t hint, stripe_len, pos;
+  uint32_t cur;
+  uint8_t *digest;
+  size_t dlen, dcap;
+} oracle_composer;
+
+static void composer_emit(oracle_composer *c) {
+  if (c->dlen + 4 > c->dcap) {
+    c->dcap = c->dcap ? 2 * c->dcap : 64;
+    c->digest = (uint8_t *)realloc(c->digest, c->dcap);
+  }
+  /* CrcUtil.intToBytes / writeInt, OC/CrcUtil.java:135-175: big-endian */
+  c->digest[c->dlen++] = (uint8_t)(c->cur >> 24);
+  c->digest[c->dlen++] = (uint8_t)(c->cur >> 16);
+  c->digest[c->dlen++] = (uint8_t)(c->cur >> 8);
+  c->digest[c->dlen++] = (uint8_t)c->cur;
+}
+
+/* newStripedCrcComposer, OC/CrcComposer.java:84-95 (newCrcComposer = stripe length Long.MAX_VALUE, :61-66) */
+oracle_composer *oracle_composer_new(int type, int64_t bytes_per_crc_hint, int64_t stripe_length) {
+  oracle_composer *c = (oracle_composer *)calloc(1, sizeof(oracle_composer));
+  c->poly = oracle_crc_poly(type);
+  if (oracle_crc_monomial(bytes_per_crc_hint, c->poly, &c->mono_hint)) { free(c); return NULL; }
+  c->hint = bytes_per_crc_hint;
+  c->stripe_len = stripe_length;
+  return c;
+}
+
+/* update(int crcB, long bytesPerCrc), OC/CrcComposer.java:168-199.
+ * 0 ok, -1 negative length (IllegalArgumentException), -2 stripe overrun (IOException). */
+int oracle_composer_update(oracle_composer *c, uint32_t crc_b, int64_t bytes_per_crc) {
+  if (c->cur == 0) {
+    c->cur = crc_b;
+  } else if (bytes_per_crc == c->hint) {
+    c->cur = oracle_gf32_multiply(c->cur, c->mono_hint, c->poly) ^ crc_b;
+  } else {
+    if (oracle_crc_compose(c->cur, crc_b, bytes_per_crc, c->poly, &c->cur)) return -1;
+  }
+  c->pos += bytes_per_crc;
+  if (c->pos > c->stripe_len) return -2;
+  if (c->pos == c->stripe_len) {
+    composer_emit(c);
+    c->cur = 0;
+    c->pos = 0;
+  }
+  return 0;
+}
+
+/* digest(), OC/CrcComposer.java:205-214: flush a partial stripe, return and reset the digest */
+size_t oracle_composer_digest(oracle_composer *c, uint8_t *out, size_t cap) {
+  if (c->pos > 0) {
+    composer_emit(c);
+    c->cur = 0;
+    c->pos = 0;
+  }
+  size_t n = c->dlen < cap ? c->dlen : cap;
+  if (out && n) memcpy(out, c->digest, n);
+  size_t all = c->dlen;
+  c->dlen = 0;
+  return all;
+}
+
+void oracle_composer_free(oracle_composer *c) {
+  if (!c) return;
+  free(c->digest);
+  free(c);
+}
+
+/* bytes the next digest() returns (test helper) */
+size_t oracle_composer_pending(const oracle_composer *c) { return c->dlen + (c->pos > 0 ? 4 : 0); }

@@ -92,6 +92,17 @@ _SIGS = {
     "ozec_gf_mul": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.c_uint8]),
     "ozec_parse_replication": (ctypes.c_int, [ctypes.c_char_p, c_intp, c_intp, c_intp, c_intp]),
     "ozec_crc_combine": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    "ozec_crc_monomial": (ctypes.c_int, [ctypes.c_int, c_i64, ctypes.POINTER(ctypes.c_uint32)]),
+    "ozec_crc_compose": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, c_i64,
+                                        ctypes.POINTER(ctypes.c_uint32)]),
+    "ozec_crc_composer_create": (ctypes.c_int, [ctypes.c_int, c_i64, c_i64, ctypes.POINTER(c_voidp)]),
+    "ozec_crc_composer_update": (ctypes.c_int, [c_voidp, ctypes.c_uint32, c_i64]),
+    "ozec_crc_composer_update_bytes": (ctypes.c_int, [c_voidp, c_voidp, c_size, c_i64]),
+    "ozec_crc_composer_pending": (c_size, [c_voidp]),
+    "ozec_crc_composer_digest": (ctypes.c_int, [c_voidp, c_voidp, c_size, ctypes.POINTER(c_size)]),
+    "ozec_crc_composer_free": (None, [c_voidp]),
+    "ozec_crc_compose_windows_batch": (ctypes.c_int, [ctypes.c_int, c_voidp, c_i64, c_size, c_size, c_size, c_size,
+                                                      ctypes.c_int, c_voidp, ctypes.c_int, c_voidp]),
     "ozec_set_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
     "ozec_fill_splitmix64": (ctypes.c_int, [c_voidp, c_size, ctypes.c_uint64, ctypes.c_uint64, c_voidp]),
     "ozec_fill_splitmix64_cells": (ctypes.c_int, [c_voidp, c_i64, c_size, c_size, ctypes.c_uint64, ctypes.c_uint64,

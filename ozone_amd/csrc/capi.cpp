@@ -951,6 +951,149 @@ uint32_t ozec_crc_combine(int checksum_type, uint32_t a, uint32_t b, uint64_t le
   return CrcMath::get(t).combine(a, b, len_b);
 }
 
+// ---- COMPOSITE_CRC ------------------------------------------------------------------------------------
+
+int ozec_crc_monomial(int checksum_type, int64_t len, uint32_t *out) {
+  CrcType t;
+  if (int rc = crc_type_of(checksum_type, &t)) return rc;
+  if (!out) return fail(OZEC_EINVAL, "null output");
+  if (len < 0) return fail(OZEC_EINVAL, "lengthBytes must be positive, got " + std::to_string(len));
+  *out = CrcMath::get(t).monomial(static_cast<uint64_t>(len));
+  return OZEC_OK;
+}
+
+int ozec_crc_compose(int checksum_type, uint32_t crc_a, uint32_t crc_b, int64_t len_b, uint32_t *out) {
+  CrcType t;
+  if (int rc = crc_type_of(checksum_type, &t)) return rc;
+  if (!out) return fail(OZEC_EINVAL, "null output");
+  if (len_b < 0) return fail(OZEC_EINVAL, "lengthBytes must be positive, got " + std::to_string(len_b));
+  *out = CrcMath::get(t).combine(crc_a, crc_b, static_cast<uint64_t>(len_b));
+  return OZEC_OK;
+}
+
+}  // extern "C"
+
+// The shift-by-hint operator is built on the first update that needs it (ECBlockChecksumComputer makes a fresh
+// composer per window CRC and only ever takes its `cur == 0` branch, so creation must stay cheap).
+struct ozec_crc_composer {
+  const CrcMath *cm = nullptr;
+  int64_t hint = 0, stripe_len = 0, pos = 0;
+  uint32_t cur = 0;
+  bool hint_ready = false;
+  uint32_t hint_cols[32] = {};
+  std::vector<uint8_t> digest;
+
+  void emit() {
+    for (int s = 24; s >= 0; s -= 8) digest.push_back(static_cast<uint8_t>(cur >> s));  // CrcUtil.intToBytes
+  }
+};
+
+extern "C" {
+
+int ozec_crc_composer_create(int checksum_type, int64_t hint, int64_t stripe_length, ozec_crc_composer **out) {
+  CrcType t;
+  if (int rc = crc_type_of(checksum_type, &t)) return rc;
+  if (!out) return fail(OZEC_EINVAL, "null output handle");
+  if (hint < 0) return fail(OZEC_EINVAL, "lengthBytes must be positive, got " + std::to_string(hint));
+  auto *c = new (std::nothrow) ozec_crc_composer();
+  if (!c) return fail(OZEC_ENOMEM, "out of memory");
+  c->cm = &CrcMath::get(t);
+  c->hint = hint;
+  c->stripe_len = stripe_length > 0 ? stripe_length : INT64_MAX;
+  *out = c;
+  return OZEC_OK;
+}
+
+int ozec_crc_composer_update(ozec_crc_composer *c, uint32_t crc, int64_t bpc) {
+  if (!c) return fail(OZEC_EINVAL, "null composer");
+  if (c->cur == 0) {
+    c->cur = crc;
+  } else if (bpc == c->hint) {
+    if (!c->hint_ready) {
+      c->cm->shift_matrix(static_cast<uint64_t>(c->hint), c->hint_cols);
+      c->hint_ready = true;
+    }
+    c->cur = CrcMath::apply(c->hint_cols, c->cur) ^ crc;
+  } else {
+    if (bpc < 0) return fail(OZEC_EINVAL, "lengthBytes must be positive, got " + std::to_string(bpc));
+    c->cur = c->cm->combine(c->cur, crc, static_cast<uint64_t>(bpc));
+  }
+  c->pos += bpc;
+  if (c->pos > c->stripe_len)
+    return fail(OZEC_EMISMATCH, "Current position in stripe '" + std::to_string(c->pos) +
+                                    "' after advancing by bytesPerCrc '" + std::to_string(bpc) +
+                                    "' exceeds stripeLength '" + std::to_string(c->stripe_len) +
+                                    "' without stripe alignment.");
+  if (c->pos == c->stripe_len) {
+    c->emit();
+    c->cur = 0;
+    c->pos = 0;
+  }
+  return OZEC_OK;
+}
+
+int ozec_crc_composer_update_bytes(ozec_crc_composer *c, const uint8_t *b, size_t len, int64_t bpc) {
+  if (!c) return fail(OZEC_EINVAL, "null composer");
+  if (len % 4 != 0)
+    return fail(OZEC_EINVAL, "Trying to update CRC from byte array with length '" + std::to_string(len) +
+                                 "' which is not a multiple of 4!");
+  for (size_t i = 0; i < len; i += 4) {
+    const uint32_t v = (uint32_t{b[i]} << 24) | (uint32_t{b[i + 1]} << 16) | (uint32_t{b[i + 2]} << 8) | b[i + 3];
+    if (int rc = ozec_crc_composer_update(c, v, bpc)) return rc;
+  }
+  return OZEC_OK;
+}
+
+size_t ozec_crc_composer_pending(const ozec_crc_composer *c) {
+  return c ? c->digest.size() + (c->pos > 0 ? 4 : 0) : 0;
+}
+
+int ozec_crc_composer_digest(ozec_crc_composer *c, uint8_t *out, size_t cap, size_t *len) {
+  if (!c) return fail(OZEC_EINVAL, "null composer");
+  const size_t need = ozec_crc_composer_pending(c);
+  if (len) *len = need;
+  if (need > cap || (need && !out)) return fail(OZEC_EINVAL, "digest buffer too small");
+  if (c->pos > 0) {
+    c->emit();
+    c->cur = 0;
+    c->pos = 0;
+  }
+  if (need) std::memcpy(out, c->digest.data(), need);
+  c->digest.clear();
+  return OZEC_OK;
+}
+
+void ozec_crc_composer_free(ozec_crc_composer *c) { delete c; }
+
+int ozec_crc_compose_windows_batch(int checksum_type, const uint32_t *d_crcs, int64_t crc_cell_stride,
+                                   size_t num_cells, size_t num_windows, size_t bpc, size_t last_len,
+                                   int crcs_big_endian, uint32_t *d_out, int out_big_endian, void *stream) {
+  CrcType t;
+  if (int rc = crc_type_of(checksum_type, &t)) return rc;
+  if (num_cells == 0) return OZEC_OK;
+  if (!d_crcs || !d_out) return fail(OZEC_EINVAL, "null buffer");
+  if (num_windows == 0 || bpc == 0 || last_len == 0 || last_len > bpc)
+    return fail(OZEC_EINVAL, "need num_windows > 0 and 0 < last_len <= bpc");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  const CrcMath &cm = CrcMath::get(t);
+  ozec::ComposeArgs a{};
+  a.crcs = d_crcs;
+  a.cell_stride = crc_cell_stride;
+  a.ncells = static_cast<int64_t>(num_cells);
+  a.nwin = static_cast<int64_t>(num_windows);
+  a.bpc = static_cast<int64_t>(bpc);
+  a.last_len = static_cast<int64_t>(last_len);
+  a.poly = cm.poly();
+  a.mono_bpc = cm.monomial(bpc);
+  a.mono_last = cm.monomial(last_len);
+  a.big_endian_in = crcs_big_endian;
+  a.big_endian_out = out_big_endian;
+  a.out = d_out;
+  OZEC_HIP(ozec::launch_compose_windows(a, pick_stream(ctx, stream)));
+  return OZEC_OK;
+}
+
 // ---- harness utilities ------------------------------------------------------------------------------
 
 int ozec_fill_splitmix64_cells(uint8_t *d_base, int64_t cell_stride, size_t ncells, size_t n, uint64_t seed,

@@ -24,7 +24,7 @@ const CrcMath &CrcMath::get(CrcType t) {
   return t == CrcType::kCrc32 ? crc32 : crc32c;
 }
 
-CrcMath::CrcMath(uint32_t poly) {
+CrcMath::CrcMath(uint32_t poly) : poly_(poly) {
   for (uint32_t i = 0; i < 256; ++i) {
     uint32_t c = i;
     for (int b = 0; b < 8; ++b) c = (c & 1) ? (c >> 1) ^ poly : c >> 1;

@@ -20,9 +20,23 @@ class CrcMath {
   // the device G5 table blob (kernels.hpp kG5* layout) for B = 1 or 4 blocks per lane per step
   const std::vector<uint32_t> &device_tables(int B) const { return B == 1 ? blob_b1_ : B == 2 ? blob_b2_ : blob_b4_; }
   uint32_t byte_table(int v) const { return t0_[v]; }
+  uint32_t poly() const { return poly_; }
+  // x^(8n) mod P in CrcUtil's reversed representation (CrcUtil.getMonomial)
+  uint32_t monomial(uint64_t n) const { return shift(0x80000000u, n); }
+  // the shift-by-n operator as 32 columns (column c = shift(1 << c, n)), for repeated use with apply()
+  void shift_matrix(uint64_t n, uint32_t cols[32]) const {
+    for (int c = 0; c < 32; ++c) cols[c] = shift(1u << c, n);
+  }
+  static uint32_t apply(const uint32_t cols[32], uint32_t v) {
+    uint32_t r = 0;
+    for (int c = 0; v; ++c, v >>= 1)
+      if (v & 1) r ^= cols[c];
+    return r;
+  }
 
  private:
   explicit CrcMath(uint32_t poly);
+  uint32_t poly_;
   uint32_t t0_[256];
   // op_[i] = operator for 2^i zero BYTES as a 32x32 GF(2) matrix (column c = image of bit c)
   uint32_t op_[64][32];

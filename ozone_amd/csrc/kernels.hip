@@ -646,6 +646,62 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// COMPOSITE_CRC (CrcUtil / CrcComposer, hadoop-ozone/common/.../client/checksum/): CRC values in the reversed
+// representation (bit 31 = x^0); composing A then B = A * x^(8|B|) mod P xor B.
+
+// CrcUtil.galoisFieldMultiply (CrcUtil.java:249-270), branch-free
+__device__ __forceinline__ uint32_t gf32_mul(uint32_t p, uint32_t q, uint32_t m) {
+  uint32_t sum = 0, px = p;
+#pragma unroll 8
+  for (int i = 31; i >= 0; --i) {
+    sum ^= px & (0u - ((q >> i) & 1u));
+    px = (px >> 1) ^ (m & (0u - (px & 1u)));
+  }
+  return sum;
+}
+
+// CrcUtil.getMonomial (CrcUtil.java:74-98): x^(8*len) mod m, len >= 0
+__device__ uint32_t gf32_monomial(int64_t len, uint32_t m) {
+  uint32_t mult = 0x80000000u >> 8, prod = 0x80000000u;
+  for (; len > 0; len >>= 1) {
+    if (len & 1) prod = gf32_mul(prod, mult, m);
+    mult = gf32_mul(mult, mult, m);
+  }
+  return prod;
+}
+
+// One wave per cell: lane l composes a contiguous run of windows, then a 6-level shuffle tree composes the
+// 64 runs in order.  Equal to CrcComposer.update over the windows in order (its `cur == 0` shortcut gives the
+// same value as composing onto 0), i.e. to the CRC of the whole cell.
+__global__ __launch_bounds__(kBlock) void compose_windows(const ComposeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t cell = static_cast<int64_t>(blockIdx.x) * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (cell >= a.ncells) return;
+  const uint32_t *c = a.crcs + cell * a.cell_stride;
+  const int64_t per = (a.nwin + 63) / 64;
+  const int64_t w0 = lane * per, w1 = w0 + per < a.nwin ? w0 + per : a.nwin;
+  uint32_t acc = 0;
+  int64_t len = 0;
+  for (int64_t w = w0; w < w1; ++w) {
+    const bool last = w == a.nwin - 1;
+    uint32_t v = c[w];
+    if (a.big_endian_in) v = __builtin_bswap32(v);
+    acc = gf32_mul(acc, last ? a.mono_last : a.mono_bpc, a.poly) ^ v;
+    len += last ? a.last_len : a.bpc;
+  }
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const uint32_t oacc = static_cast<uint32_t>(__shfl_down(static_cast<int>(acc), 1 << m, 64));
+    const int64_t olen = __shfl_down(len, 1 << m, 64);
+    if ((lane & ((2 << m) - 1)) == 0 && olen > 0) {
+      acc = gf32_mul(acc, gf32_monomial(olen, a.poly), a.poly) ^ oacc;
+      len += olen;
+    }
+  }
+  if (lane == 0) a.out[cell] = a.big_endian_out ? __builtin_bswap32(acc) : acc;
+}
+
 __global__ void finish_mismatch(int32_t *m, int64_t n) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i < n && m[i] == 0x7fffffff) m[i] = -1;
@@ -919,6 +975,13 @@ hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   OZEC_FUSED_SHAPES(OZEC_SHAPE_LAUNCH)
 #undef OZEC_SHAPE_LAUNCH
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_compose_windows(const ComposeArgs &a, hipStream_t st) {
+  if (a.ncells <= 0) return hipSuccess;
+  hipLaunchKernelGGL(compose_windows, dim3(static_cast<unsigned>((a.ncells + kBlock / 64 - 1) / (kBlock / 64))),
+                     dim3(kBlock), 0, st, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_finish_mismatch(int32_t *d_mismatch, int64_t n, hipStream_t st) {

@@ -97,6 +97,19 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t stream);
 hipError_t launch_encode_crc(const EncCrcArgs &a, hipStream_t stream);
 // d_mismatch[i] == INT32_MAX (no failure recorded) -> -1
 hipError_t launch_finish_mismatch(int32_t *d_mismatch, int64_t n, hipStream_t stream);
+
+// CrcComposer over each cell's window CRCs: windows of bpc bytes, the last of last_len
+struct ComposeArgs {
+  const uint32_t *crcs;      // [cell][window], stored ints ((int)getValue()), optionally big-endian
+  int64_t cell_stride;       // in CRCs
+  int64_t ncells, nwin;
+  int64_t bpc, last_len;
+  uint32_t poly;             // reversed polynomial (CrcUtil.getCrcPolynomialForType)
+  uint32_t mono_bpc, mono_last;  // x^(8*bpc), x^(8*last_len) mod poly (CrcUtil.getMonomial)
+  int big_endian_in, big_endian_out;
+  uint32_t *out;             // [cell]
+};
+hipError_t launch_compose_windows(const ComposeArgs &a, hipStream_t stream);
 hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t ncells, int64_t n, uint64_t seed,
                                   uint64_t first_stream, hipStream_t stream);
 // true when the fused kernel supports this (k, rows) pair with the given geometry

@@ -92,3 +92,59 @@ def test_reconstruct_crc_batch(codec, k, p, erased, n, bpc):
             assert (crcs[s, i] == stored[s, e]).all(), (s, e)
     for i in range(len(erased)):  # the corrupted stripe's rebuilt CRCs still describe what was written
         assert (crcs[1, i] == oracle.crc_windows(otype, out[1, i], bpc)).all()
+
+
+# ------------------------------------------------------------------ §8(f) row 4: COMPOSITE_CRC
+
+
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
+@pytest.mark.parametrize("n,bpc,big_endian", [(1 << 20, 16384, False), (1 << 20, 16384, True), (100_000, 4096, False),
+                                              (5000, 16384, False), (64 * 512, 512, False), (65 * 512 + 7, 512, True),
+                                              (1000 * 100, 100, False)])
+def test_compose_windows_batch_is_cell_crc(ctype, otype, n, bpc, big_endian):
+    """GPU window CRCs -> GPU CrcComposer per cell == CRC of the whole cell (oracle)."""
+    from ozone_amd import composite as cc
+    C = 5
+    data = np.stack(cells(SEED, 81000, C, n))
+    nwin = (n + bpc - 1) // bpc
+    d_crc = torch.zeros((C, nwin), dtype=torch.int32, device=DEV)
+    ck.checksum_windows_batch(ctype, t(data), n, C, n, bpc, d_crc, big_endian=big_endian)
+    d_out = torch.zeros(C, dtype=torch.int32, device=DEV)
+    cc.compose_windows_batch(ctype, d_crc, nwin, C, nwin, bpc, n - (nwin - 1) * bpc, d_out,
+                             crcs_big_endian=big_endian, out_big_endian=big_endian)
+    got = h(d_out).view(np.uint32)
+    if big_endian:
+        got = got.byteswap()
+    assert got.tolist() == [oracle.crc(otype, data[c]) for c in range(C)]
+
+
+def test_ec_file_composite_crc_from_fused_kernel():
+    """Writer side end to end: fused rs-6-3 encode + CRC32C windows on the GPU, stripe checksums as
+    ECBlockOutputStreamEntry.calculateChecksum builds them, ECBlockChecksumComputer COMPOSITE_CRC == CRC32C of
+    the key bytes (whole stripes) and == the oracle restatement of the computer."""
+    from ozone_amd import composite as cc
+    k, p, n, S, bpc = 6, 3, 1 << 18, 3, 16384
+    key = cells(SEED, 82000, 1, S * k * n)[0]
+    data = key.reshape(S, k, n)
+    nwin = n // bpc
+    d_out = torch.zeros((S, p, n), dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    e.encode_crc_batch(t(data), k * n, n, d_out, p * n, n, S, n, ck.ChecksumType.CRC32C, bpc, d_crc, big_endian=True)
+    crc_bytes = h(d_crc).view(np.uint8).reshape(S, k + p, nwin * 4)
+    infos = []
+    for s in range(S):
+        cds = [ck.ChecksumData(ck.ChecksumType.CRC32C, bpc, [crc_bytes[s, u, 4 * w:4 * w + 4].tobytes()
+                                                              for w in range(nwin)]) for u in range(k + p)]
+        infos.append(cc.ChunkInfo(n, cds[0], cc.stripe_checksum(cds)))
+    comp = cc.ECBlockChecksumComputer(infos, key.size, p)
+    comp.compute(cc.ChecksumCombineMode.COMPOSITE_CRC)
+    assert int.from_bytes(comp.get_out_bytes(), "big") == oracle.crc(oracle.CRC32C, key)
+    assert comp.get_out_bytes() == oracle.ec_block_composite_crc(oracle.CRC32C, [i.stripe_checksum for i in infos],
+                                                                 n, bpc, key.size, p)
+    # per-cell composites on the GPU agree with the host computer's view of each data cell
+    d_cell = torch.zeros((S, k + p), dtype=torch.int32, device=DEV)
+    cc.compose_windows_batch(ck.ChecksumType.CRC32C, d_crc, nwin, S * (k + p), nwin, bpc, bpc, d_cell,
+                             crcs_big_endian=True)
+    cell = h(d_cell).view(np.uint32)
+    assert all(cell[s, u] == oracle.crc(oracle.CRC32C, data[s, u]) for s in range(S) for u in range(k))

@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3r", "c4", "c5", "crc", "e2e", "host"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3r", "c4", "c5", "crc", "e2e", "host", "queue", "queue_pageable"])
     ap.add_argument("--stripes", type=int, default=0, help="override the stripe count (profiling only)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -88,6 +88,48 @@ class Workload:
                     th.start()
                 for th in ts:
                     th.join()
+            self._step = step
+            return
+        if name in ("queue", "queue_pageable"):
+            from ozone_amd.stripe_queue import StripeQueue, host_alloc
+            k, p, S, pool = 6, 3, stripes_override or 1024, 64
+            pinned = name == "queue"
+            self.crc_type, self.bpc = ck.ChecksumType.CRC32C, 16384
+            nwin = n // self.bpc
+            self._pool = []
+
+            def buf(nbytes, dtype=np.uint8):
+                if not pinned:
+                    return np.zeros(nbytes // np.dtype(dtype).itemsize, dtype)
+                pb = host_alloc(nbytes)
+                self._pool.append(pb)
+                return pb.array.view(dtype)
+            rng = np.random.default_rng(rank)
+            # one buffer per stripe with its k data then p parity cells back to back (the layout a writer's
+            # pinned cell pool would use); the queue then moves a stripe in one H2D and one D2H copy
+            slabs = [buf((k + p) * n) for _ in range(pool)]
+            self.qd = [[sl[j * n:(j + 1) * n] for j in range(k)] for sl in slabs]
+            for st in self.qd:
+                for a in st:
+                    a[:] = rng.integers(0, 256, n, dtype=np.uint8)
+            self.qp = [[sl[(k + r) * n:(k + r + 1) * n] for r in range(p)] for sl in slabs]
+            self.qc = [buf((k + p) * nwin * 4, np.uint32) for _ in range(pool)]
+            enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+            self.q = StripeQueue(enc, n, 64, self.crc_type, self.bpc)
+            self.k, self.p, self.S = k, p, S
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * (k + p) * n
+            self.kernel = "encode_crc_vec<6,3> via ozec_stripe_queue (+H2D/D2H per cell)"
+            self.config = {"workload": f"rs-6-3-1024k + CRC32C/16 KiB through the stripe queue (SURVEY 8(f) row 3) "
+                                       f"from {'pinned' if pinned else 'pageable'} host cells, {S} stripes, "
+                                       f"batches of 64", "stripes": S}
+
+            def step():
+                t = 0
+                for i in range(S):
+                    j = i % pool
+                    t = self.q.submit(self.qd[j], self.qp[j], crcs=self.qc[j])
+                self.q.wait(t)
             self._step = step
             return
         if name in ("c2", "c5", "e2e"):

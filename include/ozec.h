@@ -186,6 +186,32 @@ int ozec_parse_replication(const char *s, int *codec, int *num_data, int *num_pa
 /* crc(A||B) from crc(A), crc(B), |B| -- the combine primitive behind streaming update and stripe checksums */
 uint32_t ozec_crc_combine(int checksum_type, uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
+/* ---- writer-side stripe batching -------------------------------------------------------
+ * ECKeyOutputStream encodes one stripe per RawErasureEncoder.encode call (ECKeyOutputStream.java:304; its stripe
+ * queue :114, :501-543).  A stripe queue accepts stripes as they fill and encodes them in batches of
+ * stripes_per_batch on the GPU (one fused encode (+ CRC) launch per batch, three batches in rotation).  Cells are
+ * DMA'd straight from / into the caller's buffers when those are pinned (ozec_host_alloc, or any pinned host
+ * memory), else through pinned staging.  The buffers given to submit must stay valid and unmodified until wait()
+ * has returned for that ticket (or until ozec_stripe_queue_free). */
+/* pinned host memory for cell buffers (the JNI side wraps it with NewDirectByteBuffer) */
+int ozec_host_alloc(size_t bytes, void **out);
+int ozec_host_free(void *p);
+typedef struct ozec_stripe_queue ozec_stripe_queue;
+/* checksum_type OZEC_CHECKSUM_NONE: parity only; CRC32 / CRC32C: also the bpc-window CRCs of all k+p units,
+ * written per stripe as crcs[unit][window] (window count from the stripe's length), big-endian if asked */
+int ozec_stripe_queue_create(ozec_coder *encoder, size_t cell_len, size_t stripes_per_batch, int checksum_type,
+                             size_t bpc, int big_endian, ozec_stripe_queue **out);
+/* queue one stripe (k data cells of len <= cell_len bytes -> p parity cells, optional CRCs); a batch holds one
+ * length, so a stripe of another length first launches the pending batch.  *ticket identifies the stripe. */
+int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, uint8_t *const *parity, size_t len,
+                             uint32_t *crcs, uint64_t *ticket);
+/* launch the partly filled batch now */
+int ozec_stripe_queue_flush(ozec_stripe_queue *q);
+/* block until every stripe up to and including `ticket` has its parity (and CRCs) in the caller's buffers */
+int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket);
+/* drain and destroy */
+int ozec_stripe_queue_free(ozec_stripe_queue *q);
+
 /* ---- COMPOSITE_CRC: CrcUtil / CrcComposer ------------------------------------------
  * OC/ = hadoop-ozone/common/src/main/java/org/apache/hadoop/ozone/client/checksum/.  CRC values are the stored
  * ints ((int)getValue()) in CrcUtil's reversed representation; checksum_type is OZEC_CHECKSUM_CRC32/CRC32C
@@ -221,7 +247,8 @@ int ozec_crc_compose_windows_batch(int checksum_type, const uint32_t *d_crcs, in
 
 /* ---- harness utilities ------------------------------------------------------------------------------- */
 /* process-wide tuning knobs for benchmarking: kernels ("grid", "gf_variant", "crc_variant", "crc_grid",
- * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_slots") */
+ * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_slots",
+ * "copy_threads" = helper threads for pageable <-> pinned copies, 0 = copy on the calling thread) */
 int ozec_set_tuning(const char *key, int64_t value);
 /* fill n bytes with splitmix64 stream `stream_id` of `seed` (tests/golden/synth.py is the CPU twin) */
 int ozec_fill_splitmix64(uint8_t *d_dst, size_t n, uint64_t seed, uint64_t stream_id, void *stream);

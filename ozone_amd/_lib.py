@@ -92,6 +92,15 @@ _SIGS = {
     "ozec_gf_mul": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.c_uint8]),
     "ozec_parse_replication": (ctypes.c_int, [ctypes.c_char_p, c_intp, c_intp, c_intp, c_intp]),
     "ozec_crc_combine": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    "ozec_host_alloc": (ctypes.c_int, [c_size, ctypes.POINTER(c_voidp)]),
+    "ozec_host_free": (ctypes.c_int, [c_voidp]),
+    "ozec_stripe_queue_create": (ctypes.c_int, [c_voidp, c_size, c_size, ctypes.c_int, c_size, ctypes.c_int,
+                                                ctypes.POINTER(c_voidp)]),
+    "ozec_stripe_queue_submit": (ctypes.c_int, [c_voidp, c_ptrs, c_ptrs, c_size, c_voidp,
+                                                ctypes.POINTER(ctypes.c_uint64)]),
+    "ozec_stripe_queue_flush": (ctypes.c_int, [c_voidp]),
+    "ozec_stripe_queue_wait": (ctypes.c_int, [c_voidp, ctypes.c_uint64]),
+    "ozec_stripe_queue_free": (ctypes.c_int, [c_voidp]),
     "ozec_crc_monomial": (ctypes.c_int, [ctypes.c_int, c_i64, ctypes.POINTER(ctypes.c_uint32)]),
     "ozec_crc_compose": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, c_i64,
                                         ctypes.POINTER(ctypes.c_uint32)]),

@@ -19,7 +19,9 @@
 #include "../../include/ozec.h"
 #include "crc_host.hpp"
 #include "gf256.hpp"
+#include "copy_pool.hpp"
 #include "kernels.hpp"
+#include "status.hpp"
 
 namespace {
 
@@ -166,6 +168,8 @@ int crc_type_of(int checksum_type, CrcType *t) {
 
 }  // namespace
 
+int ozec::set_error(int code, const std::string &msg) { return fail(code, msg); }
+
 // ------------------------------------------------------------------------------------------------
 // coder handle
 
@@ -288,13 +292,17 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     OZEC_HIP(hipEventSynchronize(s->events[c]));
     const size_t off = c * chunk, cl = std::min(chunk, len - off);
     const uint8_t *src = s->pinned + c * per_chunk + nin * cp;
-    for (int r = 0; r < nout; ++r) std::memcpy(out[r] + out_pos(off), src + r * op, out_bytes(cl));
+    std::vector<ozec::CopyTask> tasks;
+    for (int r = 0; r < nout; ++r) tasks.push_back({out[r] + out_pos(off), src + r * op, out_bytes(cl)});
+    ozec::parallel_copy(tasks);
     return OZEC_OK;
   };
   for (size_t c = 0; c < nch; ++c) {
     const size_t off = c * chunk, cl = std::min(chunk, len - off);
     uint8_t *h = s->pinned + c * per_chunk, *d = s->dbuf + c * per_chunk;
-    for (int j = 0; j < nin; ++j) std::memcpy(h + j * cp, in[j] + off, cl);
+    std::vector<ozec::CopyTask> tasks;
+    for (int j = 0; j < nin; ++j) tasks.push_back({h + j * cp, in[j] + off, cl});
+    ozec::parallel_copy(tasks);
     OZEC_HIP(hipMemcpyAsync(d, h, nin * cp, hipMemcpyHostToDevice, s->stream));
     OZEC_HIP(launch(d, static_cast<int64_t>(cp), d + nin * cp, static_cast<int64_t>(op), off, cl, s->stream));
     OZEC_HIP(hipMemcpyAsync(h + nin * cp, d + nin * cp, nout * op, hipMemcpyDeviceToHost, s->stream));
@@ -941,6 +949,7 @@ int ozec_set_tuning(const char *key, int64_t value) {
   else if (k == "unit_map") ozec::g_tune.unit_map = static_cast<int>(value);
   else if (k == "host_chunk" && value > 0) ozec::g_tune.host_chunk = value;
   else if (k == "host_slots" && value > 0) ozec::g_tune.host_slots = value;
+  else if (k == "copy_threads" && value >= 0) ozec::set_copy_threads(static_cast<int>(value));
   else return fail(OZEC_EINVAL, "unknown tuning key " + k);
   return OZEC_OK;
 }

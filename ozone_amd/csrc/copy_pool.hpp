@@ -1,0 +1,21 @@
+// Parallel host memcpy for the staging paths (pageable caller buffers <-> pinned staging).  One thread copies
+// ~10-16 GB/s; the host-buffer ABI (the JNI drop-in path) is bound by that copy, so large copies are split into
+// >= 256 KiB pieces over a small process-wide worker pool, the calling thread taking part.
+#pragma once
+#include <cstddef>
+#include <vector>
+
+namespace ozec {
+
+struct CopyTask {
+  void *dst;
+  const void *src;
+  size_t n;
+};
+
+// run every task (in any order) and return when all are done
+void parallel_copy(const std::vector<CopyTask> &tasks);
+// threads used besides the caller (0 = copy inline); set by ozec_set_tuning("copy_threads", n)
+void set_copy_threads(int n);
+
+}  // namespace ozec

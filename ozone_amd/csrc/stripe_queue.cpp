@@ -1,0 +1,304 @@
+// Writer-side stripe batching, built on the public C ABI only.
+//
+// ECKeyOutputStream encodes one stripe per RawErasureEncoder.encode call (ECKeyOutputStream.java:304; stripe
+// queue :114, :501-543).  A stripe queue takes stripes as they fill and runs them in batches: each submitted
+// cell is copied into the batch's device buffer on the batch's stream right away (DMA straight from the
+// caller's buffer when it is pinned, else through pinned staging), a full batch is one fused encode (+ CRC)
+// launch, and parity / CRCs come back by DMA into pinned callers' buffers or through staging.  Several
+// batches rotate, so the copies of batch i+1 overlap the kernel and copies of batch i.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ozec.h"
+#include "copy_pool.hpp"
+#include "status.hpp"
+
+namespace {
+
+using ozec::set_error;
+
+#define SQ_HIP(call)                                                                                      \
+  do {                                                                                                    \
+    hipError_t err_ = (call);                                                                             \
+    if (err_ != hipSuccess)                                                                               \
+      return set_error(OZEC_EDEVICE, std::string("HIP error: ") + hipGetErrorString(err_) + " at " #call); \
+  } while (0)
+
+bool is_pinned(const void *p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+struct Pending {
+  std::vector<uint8_t *> parity;  // caller's parity buffers (p of them)
+  uint32_t *crcs = nullptr;       // caller's CRC buffer or null
+  bool parity_staged = false;     // parity comes back through staging (caller buffer not pinned)
+};
+
+struct Batch {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t *d_units = nullptr;  // [S][k+rows][cell_len]
+  uint32_t *d_crcs = nullptr;  // [S][k+rows][nwin]
+  uint8_t *h_stage = nullptr;  // pinned [S][k+rows][cell_len], allocated on first pageable use
+  uint32_t *h_crcs = nullptr;  // pinned [S][k+rows][nwin]
+  size_t n = 0, len = 0;
+  uint64_t first_ticket = 0;
+  bool in_flight = false;
+  std::vector<Pending> pend;
+};
+
+}  // namespace
+
+struct ozec_stripe_queue {
+  ozec_coder *enc = nullptr;
+  int k = 0, p = 0, rows = 0, ctype = OZEC_CHECKSUM_NONE, big_endian = 0;
+  size_t cell_len = 0, S = 0, bpc = 0, nwin_max = 0;
+  std::vector<Batch> batches;
+  size_t cur = 0;
+  uint64_t next_ticket = 0;
+  std::mutex mu;
+
+  // device layout per stripe: k data + p parity cells (all p, so the XOR codec's zero-filled extra outputs --
+  // ozec_encode_batch writes them -- stay inside the stripe); CRCs cover the k + rows cells that are coded
+  size_t units() const { return static_cast<size_t>(k + rows); }
+  size_t stripe_bytes() const { return static_cast<size_t>(k + p) * cell_len; }
+  size_t stripe_crcs() const { return units() * nwin_max; }
+  size_t nwin(size_t len) const { return bpc ? (len + bpc - 1) / bpc : 0; }
+
+  int launch(Batch &b) {
+    if (b.n == 0 || b.in_flight) return OZEC_OK;
+    const int64_t ss = static_cast<int64_t>(stripe_bytes()), us = static_cast<int64_t>(cell_len);
+    uint8_t *d_par = b.d_units + static_cast<size_t>(k) * cell_len;
+    const size_t nw = nwin(b.len);
+    if (ctype == OZEC_CHECKSUM_NONE) {
+      if (int rc = ozec_encode_batch(enc, b.d_units, ss, us, d_par, ss, us, b.n, b.len, b.stream)) return rc;
+    } else {
+      // CRC layout per stripe [unit][window] with a fixed stride of nw windows per unit
+      if (int rc = ozec_encode_crc_batch(enc, b.d_units, ss, us, d_par, ss, us, b.n, b.len, ctype, bpc, b.d_crcs,
+                                         big_endian, b.stream))
+        return rc;
+    }
+    for (size_t i = 0; i < b.n; ++i) {
+      const Pending &pd = b.pend[i];
+      for (int r = 0; r < rows;) {
+        const size_t off = i * stripe_bytes() + static_cast<size_t>(k + r) * cell_len;
+        uint8_t *dst = pd.parity_staged ? b.h_stage + off : pd.parity[r];
+        int run = 1;
+        while (!pd.parity_staged && b.len == cell_len && r + run < rows && pd.parity[r + run] == dst + run * b.len)
+          ++run;
+        SQ_HIP(hipMemcpyAsync(dst, b.d_units + off, run * b.len, hipMemcpyDeviceToHost, b.stream));
+        r += run;
+      }
+    }
+    if (ctype != OZEC_CHECKSUM_NONE)
+      SQ_HIP(hipMemcpyAsync(b.h_crcs, b.d_crcs, b.n * units() * nw * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                            b.stream));
+    SQ_HIP(hipEventRecord(b.done, b.stream));
+    b.in_flight = true;
+    return OZEC_OK;
+  }
+
+  int complete(Batch &b) {
+    if (!b.in_flight) return OZEC_OK;
+    SQ_HIP(hipEventSynchronize(b.done));
+    const size_t nw = nwin(b.len);
+    std::vector<ozec::CopyTask> tasks;
+    for (size_t i = 0; i < b.n; ++i) {
+      const Pending &pd = b.pend[i];
+      for (int r = 0; r < p; ++r) {
+        if (r >= rows) {  // XOR with p > 1: outputs past the first stay zero (XORRawEncoder.java:67-85)
+          std::memset(pd.parity[r], 0, b.len);
+        } else if (pd.parity_staged) {
+          tasks.push_back({pd.parity[r], b.h_stage + i * stripe_bytes() + static_cast<size_t>(k + r) * cell_len, b.len});
+        }
+      }
+      if (pd.crcs && ctype != OZEC_CHECKSUM_NONE)
+        tasks.push_back({pd.crcs, b.h_crcs + i * units() * nw, units() * nw * sizeof(uint32_t)});
+    }
+    ozec::parallel_copy(tasks);
+    b.in_flight = false;
+    b.n = 0;
+    return OZEC_OK;
+  }
+
+  int stage_pinned(Batch &b) {
+    if (!b.h_stage) SQ_HIP(hipHostMalloc(reinterpret_cast<void **>(&b.h_stage), S * stripe_bytes(), hipHostMallocDefault));
+    return OZEC_OK;
+  }
+};
+
+extern "C" {
+
+int ozec_host_alloc(size_t bytes, void **out) {
+  if (!out) return set_error(OZEC_EINVAL, "null output");
+  *out = nullptr;
+  if (bytes == 0) return OZEC_OK;
+  SQ_HIP(hipHostMalloc(out, bytes, hipHostMallocDefault));
+  return OZEC_OK;
+}
+
+int ozec_host_free(void *p) {
+  if (p) SQ_HIP(hipHostFree(p));
+  return OZEC_OK;
+}
+
+int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_per_batch, int checksum_type,
+                             size_t bpc, int big_endian, ozec_stripe_queue **out) {
+  if (!out) return set_error(OZEC_EINVAL, "null output handle");
+  *out = nullptr;
+  int codec = 0, k = 0, p = 0, is_dec = 0;
+  if (int rc = ozec_coder_info(enc, &codec, &k, &p, &is_dec)) return rc;
+  if (is_dec) return set_error(OZEC_EINVAL, "not an encoder");
+  if (cell_len == 0 || stripes_per_batch == 0) return set_error(OZEC_EINVAL, "cell_len and stripes_per_batch must be > 0");
+  if (checksum_type != OZEC_CHECKSUM_NONE && checksum_type != OZEC_CHECKSUM_CRC32 &&
+      checksum_type != OZEC_CHECKSUM_CRC32C)
+    return set_error(OZEC_EINVAL, "checksum type must be NONE, CRC32 or CRC32C");
+  if (checksum_type != OZEC_CHECKSUM_NONE && bpc == 0) return set_error(OZEC_EINVAL, "bytesPerChecksum must be positive");
+  auto *q = new (std::nothrow) ozec_stripe_queue();
+  if (!q) return set_error(OZEC_ENOMEM, "out of memory");
+  q->enc = enc;
+  q->k = k;
+  q->p = p;
+  q->rows = codec == OZEC_CODEC_XOR ? 1 : p;
+  q->ctype = checksum_type;
+  q->bpc = checksum_type == OZEC_CHECKSUM_NONE ? 0 : bpc;
+  q->big_endian = big_endian;
+  q->cell_len = cell_len;
+  q->S = stripes_per_batch;
+  q->nwin_max = q->nwin(cell_len);
+  q->batches.resize(3);
+  for (Batch &b : q->batches) {
+    b.pend.resize(q->S);
+    hipError_t e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&b.d_units), q->S * q->stripe_bytes());
+    if (e == hipSuccess && q->ctype != OZEC_CHECKSUM_NONE) {
+      e = hipMalloc(reinterpret_cast<void **>(&b.d_crcs), q->S * q->stripe_crcs() * sizeof(uint32_t));
+      if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void **>(&b.h_crcs), q->S * q->stripe_crcs() * sizeof(uint32_t),
+                          hipHostMallocDefault);
+    }
+    if (e != hipSuccess) {
+      ozec_stripe_queue_free(q);
+      return set_error(OZEC_EDEVICE, std::string("HIP error creating the stripe queue: ") + hipGetErrorString(e));
+    }
+  }
+  *out = q;
+  return OZEC_OK;
+}
+
+int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, uint8_t *const *parity, size_t len,
+                             uint32_t *crcs, uint64_t *ticket) {
+  if (!q) return set_error(OZEC_EINVAL, "null queue");
+  if (!data || !parity) return set_error(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  for (int j = 0; j < q->k; ++j)
+    if (!data[j]) return set_error(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  for (int r = 0; r < q->p; ++r)
+    if (!parity[r]) return set_error(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  if (len == 0 || len > q->cell_len)
+    return set_error(OZEC_EINVAL, "stripe length must be in [1, cell_len] (" + std::to_string(q->cell_len) + ")");
+  std::lock_guard<std::mutex> lk(q->mu);
+  Batch *b = &q->batches[q->cur];
+  if (b->n > 0 && (b->in_flight || b->len != len)) {  // a batch holds one cell length; rotate
+    if (int rc = q->launch(*b)) return rc;
+    q->cur = (q->cur + 1) % q->batches.size();
+    b = &q->batches[q->cur];
+  }
+  if (b->in_flight)
+    if (int rc = q->complete(*b)) return rc;  // oldest batch: its callers' outputs land now
+  if (b->n == 0) {
+    b->len = len;
+    b->first_ticket = q->next_ticket;
+  }
+  const size_t i = b->n;
+  Pending &pd = b->pend[i];
+  pd.parity.assign(parity, parity + q->p);
+  pd.crcs = crcs;
+  pd.parity_staged = false;
+  for (int r = 0; r < q->rows; ++r) pd.parity_staged |= !is_pinned(parity[r]);
+  if (pd.parity_staged)
+    if (int rc = q->stage_pinned(*b)) return rc;
+  // pageable cells are staged first (in parallel), then every cell goes over PCIe; cells laid out back to back
+  // in one pinned buffer (or in the staging area) go as one copy
+  std::vector<const uint8_t *> src(data, data + q->k);
+  std::vector<ozec::CopyTask> tasks;
+  for (int j = 0; j < q->k; ++j) {
+    if (is_pinned(src[j])) continue;
+    if (int rc = q->stage_pinned(*b)) return rc;
+    uint8_t *st = b->h_stage + i * q->stripe_bytes() + static_cast<size_t>(j) * q->cell_len;
+    tasks.push_back({st, src[j], len});
+    src[j] = st;
+  }
+  ozec::parallel_copy(tasks);
+  for (int j = 0; j < q->k;) {
+    const size_t off = i * q->stripe_bytes() + static_cast<size_t>(j) * q->cell_len;
+    int run = 1;
+    while (len == q->cell_len && j + run < q->k && src[j + run] == src[j] + run * len) ++run;
+    SQ_HIP(hipMemcpyAsync(b->d_units + off, src[j], run * len, hipMemcpyHostToDevice, b->stream));
+    j += run;
+  }
+  ++b->n;
+  if (ticket) *ticket = q->next_ticket;
+  ++q->next_ticket;
+  if (b->n == q->S) {
+    if (int rc = q->launch(*b)) return rc;
+    q->cur = (q->cur + 1) % q->batches.size();
+  }
+  return OZEC_OK;
+}
+
+int ozec_stripe_queue_flush(ozec_stripe_queue *q) {
+  if (!q) return set_error(OZEC_EINVAL, "null queue");
+  std::lock_guard<std::mutex> lk(q->mu);
+  Batch &b = q->batches[q->cur];
+  if (b.n > 0 && !b.in_flight) {
+    if (int rc = q->launch(b)) return rc;
+    q->cur = (q->cur + 1) % q->batches.size();
+  }
+  return OZEC_OK;
+}
+
+int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket) {
+  if (!q) return set_error(OZEC_EINVAL, "null queue");
+  std::lock_guard<std::mutex> lk(q->mu);
+  if (ticket >= q->next_ticket) return set_error(OZEC_EINVAL, "unknown ticket " + std::to_string(ticket));
+  // complete, oldest first, every batch holding a stripe <= ticket (launching the filling one if needed)
+  for (;;) {
+    Batch *oldest = nullptr;
+    for (Batch &b : q->batches)
+      if (b.n > 0 && b.first_ticket <= ticket && (!oldest || b.first_ticket < oldest->first_ticket)) oldest = &b;
+    if (!oldest) return OZEC_OK;
+    if (!oldest->in_flight) {
+      if (int rc = q->launch(*oldest)) return rc;
+      if (oldest == &q->batches[q->cur]) q->cur = (q->cur + 1) % q->batches.size();
+    }
+    if (int rc = q->complete(*oldest)) return rc;
+  }
+}
+
+int ozec_stripe_queue_free(ozec_stripe_queue *q) {
+  if (!q) return OZEC_OK;
+  int rc = OZEC_OK;
+  for (Batch &b : q->batches) {
+    if (b.in_flight && hipEventSynchronize(b.done) != hipSuccess) rc = OZEC_EDEVICE;
+    if (b.d_units) (void)hipFree(b.d_units);
+    if (b.d_crcs) (void)hipFree(b.d_crcs);
+    if (b.h_stage) (void)hipHostFree(b.h_stage);
+    if (b.h_crcs) (void)hipHostFree(b.h_crcs);
+    if (b.done) (void)hipEventDestroy(b.done);
+    if (b.stream) (void)hipStreamDestroy(b.stream);
+  }
+  delete q;
+  return rc == OZEC_OK ? OZEC_OK : set_error(rc, "device error while draining the stripe queue");
+}
+
+}  // extern "C"

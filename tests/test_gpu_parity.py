@@ -374,11 +374,13 @@ def test_host_path_concurrent_threads_share_one_coder():
     assert not errors, errors
 
 
-@pytest.mark.parametrize("chunk", [4096, 12288, 1 << 18])
-def test_host_path_chunked_pipeline(chunk):
-    """Host-buffer calls are staged in pipelined chunks (ozec_set_tuning "host_chunk"); odd lengths, chunk counts
-    above the 64-chunk cap and CRC windows that straddle the nominal chunk size must not change any byte."""
+@pytest.mark.parametrize("chunk,copy_threads", [(4096, 3), (12288, 0), (1 << 18, 3), (1 << 18, 0), (1 << 20, 7)])
+def test_host_path_chunked_pipeline(chunk, copy_threads):
+    """Host-buffer calls are staged in pipelined chunks (ozec_set_tuning "host_chunk") with the pageable <-> pinned
+    copies split over helper threads ("copy_threads"); odd lengths, chunk counts above the 64-chunk cap and CRC
+    windows that straddle the nominal chunk size must not change any byte."""
     assert L.lib().ozec_set_tuning(b"host_chunk", chunk) == 0
+    assert L.lib().ozec_set_tuning(b"copy_threads", copy_threads) == 0
     try:
         k, p, n = 6, 3, 700_001
         data = cells(SEED, 95000, k, n)
@@ -396,3 +398,4 @@ def test_host_path_chunked_pipeline(chunk):
             assert got == [int(x) for x in oracle.crc_windows(oracle.CRC32C, data[2], bpc)]
     finally:
         L.lib().ozec_set_tuning(b"host_chunk", 256 << 10)
+        L.lib().ozec_set_tuning(b"copy_threads", 3)

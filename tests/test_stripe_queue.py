@@ -1,0 +1,141 @@
+"""writer-side stripe batching (ozec_stripe_queue_*) against the oracle, bit-exact."""
+import numpy as np
+import pytest
+
+import oracle
+from synth import SEED, cells
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from ozone_amd import rawcoder as rc  # noqa: E402
+from ozone_amd.checksum import ChecksumType  # noqa: E402
+from ozone_amd.stripe_queue import StripeQueue, host_alloc  # noqa: E402
+
+
+def _stripe(first, k, n, pinned, keep):
+    d = cells(SEED, first, k, n)
+    if not pinned:
+        return d
+    out = []
+    for x in d:
+        pb = host_alloc(n)
+        pb.array[:] = x
+        keep.append(pb)
+        out.append(pb.array)
+    return out
+
+
+def _parity(p, n, pinned, keep):
+    if not pinned:
+        return [np.full(n, 0xA5, np.uint8) for _ in range(p)]
+    out = []
+    for _ in range(p):
+        pb = host_alloc(n)
+        pb.array[:] = 0xA5
+        keep.append(pb)
+        out.append(pb.array)
+    return out
+
+
+@pytest.mark.parametrize("codec,k,p", [("rs", 6, 3), ("rs", 3, 2), ("rs", 10, 4), ("xor", 2, 1), ("xor", 3, 2)])
+@pytest.mark.parametrize("ctype,otype", [(ChecksumType.NONE, None), (ChecksumType.CRC32C, oracle.CRC32C)])
+def test_queue_matches_oracle(codec, k, p, ctype, otype):
+    n, bpc, S = 65536, 16384, 4
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec))
+    keep, jobs = [], []
+    with StripeQueue(enc, n, S, ctype, bpc, big_endian=True) as q:
+        for s in range(11):  # two full batches + a partial one, pinned and pageable buffers mixed
+            pinned = s % 3 == 1
+            d = _stripe(90000 + 100 * s, k, n, pinned, keep)
+            par = _parity(p, n, pinned and s % 2 == 1, keep)
+            crcs = np.zeros((k + p) * (n // bpc), np.uint32) if otype is not None else None
+            jobs.append((q.submit(d, par, crcs=crcs), d, par, crcs))
+        q.wait(jobs[-1][0])
+    for t, d, par, crcs in jobs:
+        ref = oracle.rs_encode(k, p, d) if codec == "rs" else [oracle.xor_encode(d)] + [np.zeros(n, np.uint8)] * (p - 1)
+        assert all((a == b).all() for a, b in zip(par, ref)), t
+        if otype is not None:
+            exp = np.concatenate([oracle.crc_windows(otype, u, bpc) for u in list(d) + ref[:1 if codec == "xor" else p]])
+            got = crcs.byteswap()[:exp.size]
+            assert (got == exp).all(), t
+
+
+def test_queue_mixed_lengths_and_wait_order():
+    k, p, cell = 6, 3, 1 << 16
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    q = StripeQueue(enc, cell, 8, ChecksumType.CRC32, 4096)
+    jobs = []
+    for s, n in enumerate([cell, cell, 1000, 4096 + 16, cell, 17, cell]):
+        d = cells(SEED, 91000 + 100 * s, k, n)
+        par = [np.zeros(n, np.uint8) for _ in range(p)]
+        crcs = np.zeros((k + p) * ((n + 4095) // 4096), np.uint32)
+        jobs.append((q.submit(d, par, crcs=crcs), d, par, crcs, n))
+    q.wait(jobs[3][0])  # stripes 0..3 are complete now, whatever batch they were in
+    for t, d, par, crcs, n in jobs[:4]:
+        ref = oracle.rs_encode(k, p, d)
+        assert all((a == b).all() for a, b in zip(par, ref)), t
+    q.flush()
+    q.wait(jobs[-1][0])
+    for t, d, par, crcs, n in jobs:
+        ref = oracle.rs_encode(k, p, d)
+        assert all((a == b).all() for a, b in zip(par, ref)), t
+        exp = np.concatenate([oracle.crc_windows(oracle.CRC32, u, 4096) for u in list(d) + ref])
+        assert (crcs == exp).all(), t
+    q.close()
+
+
+def test_queue_many_batches_rotate():
+    k, p, n = 6, 3, 4096
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    jobs = []
+    with StripeQueue(enc, n, 5) as q:
+        for s in range(203):
+            d = cells(SEED, 92000 + 10 * s, k, n)
+            par = [np.zeros(n, np.uint8) for _ in range(p)]
+            jobs.append((q.submit(d, par), d, par))
+            if s % 50 == 49:
+                q.wait(jobs[s - 7][0])
+        q.wait(jobs[-1][0])
+    for t, d, par in jobs:
+        ref = oracle.rs_encode(k, p, d)
+        assert all((a == b).all() for a, b in zip(par, ref)), t
+
+
+def test_queue_errors():
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(6, 3))
+    dec = rc.RawErasureDecoder(rc.ECReplicationConfig(6, 3))
+    with pytest.raises(Exception):
+        StripeQueue(dec, 4096)
+    q = StripeQueue(enc, 4096)
+    with pytest.raises(Exception):
+        q.submit(cells(SEED, 1, 6, 8192), [np.zeros(8192, np.uint8)] * 3)  # longer than cell_len
+    with pytest.raises(Exception):
+        q.wait(5)  # no such ticket yet
+    with pytest.raises(rc.IllegalArgumentException):
+        q.submit(cells(SEED, 1, 5, 4096), [np.zeros(4096, np.uint8)] * 3)
+    q.close()
+
+
+@pytest.mark.parametrize("n", [1 << 16, 5000])
+def test_queue_contiguous_pinned_stripe(n):
+    """Cells back to back in one pinned buffer (one H2D and one D2H copy per stripe when len == cell_len)."""
+    k, p, cell = 6, 3, 1 << 16
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    slabs, jobs = [], []
+    with StripeQueue(enc, cell, 3, ChecksumType.CRC32C, 4096) as q:
+        for s in range(7):
+            sl = host_alloc((k + p) * n)
+            slabs.append(sl)
+            d = [sl.array[j * n:(j + 1) * n] for j in range(k)]
+            for j, x in enumerate(cells(SEED, 93000 + 10 * s, k, n)):
+                d[j][:] = x
+            par = [sl.array[(k + r) * n:(k + r + 1) * n] for r in range(p)]
+            crcs = np.zeros((k + p) * ((n + 4095) // 4096), np.uint32)
+            jobs.append((q.submit(d, par, crcs=crcs), d, par, crcs))
+        q.wait(jobs[-1][0])
+        for t, d, par, crcs in jobs:
+            ref = oracle.rs_encode(k, p, [np.array(x) for x in d])
+            assert all((a == b).all() for a, b in zip(par, ref)), t
+            exp = np.concatenate([oracle.crc_windows(oracle.CRC32C, u, 4096) for u in [np.array(x) for x in d] + ref])
+            assert (crcs == exp).all(), t

@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--threads", type=int, default=1, help="host workload: caller threads sharing one coder")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="ozec_set_tuning knob (A/B and profiling runs only; defaults are the measured best)")
     return ap.parse_args()
 
 
@@ -119,7 +121,7 @@ class Workload:
             self.k, self.p, self.S = k, p, S
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + p) * n
-            self.kernel = "encode_crc_vec<6,3> via ozec_stripe_queue (+H2D/D2H per cell)"
+            self.kernel = "encode_crc_g26<6,3> via ozec_stripe_queue (+H2D/D2H per cell)"
             self.config = {"workload": f"rs-6-3-1024k + CRC32C/16 KiB through the stripe queue (SURVEY 8(f) row 3) "
                                        f"from {'pinned' if pinned else 'pageable'} host cells, {S} stripes, "
                                        f"batches of 64", "stripes": S}
@@ -150,7 +152,7 @@ class Workload:
             self.crcs = torch.empty((S, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * n
             self.alg_bytes = S * n + S * self.nwin * 4
-            self.kernel = "crc_windows_vec"
+            self.kernel = "crc_windows_g26<1,4>"
             self.config = {"workload": "CRC32C per 16 KiB window, device-resident", "cells": S, "cell_bytes": n,
                            "bytes_per_checksum": self.bpc}
             self._step = lambda: ck.checksum_windows_batch(self.crc_type, self.data, n, S, n, self.bpc, self.crcs)
@@ -205,7 +207,7 @@ class Workload:
             self.mism = torch.empty(S, dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + 4) * n + S * (k + 4) * self.nwin * 4
-            self.kernel = "encode_crc_vec<10,4> (reconstruct mode)"
+            self.kernel = "encode_crc_g26<10,4> (reconstruct mode)"
             self.config = {"workload": "rs-10-4-1024k reconstruction: verify CRC32C of 10 read units + decode 4 + "
                                        "CRC32C of rebuilt units, 2048 stripes, fused, device-resident",
                            "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
@@ -217,7 +219,7 @@ class Workload:
             self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * units * n + S * units * self.nwin * 4
-            self.kernel = f"encode_crc_vec<{k},{p}>"
+            self.kernel = f"encode_crc_g26<{k},{p}>"
             wl = ("xor-2-1-1024k + CRC32C/16 KiB, 16 block groups x 256 stripes" if name == "c4"
                   else "rs-6-3-1024k encode + CRC32C/16 KiB, 4096 stripes")
             self.config = {"workload": wl + ", fused, device-resident", "codec": "xor" if name == "c4" else "rs",
@@ -229,7 +231,7 @@ class Workload:
             self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * units * n
-            self.kernel = "encode_crc_vec<6,3> (+H2D/D2H)"
+            self.kernel = "encode_crc_g26<6,3> (+H2D/D2H)"
             self.config = {"workload": "rs-6-3-1024k + CRC32C end-to-end from pinned host buffers", "stripes": S}
             self.streams = [torch.cuda.Stream(), torch.cuda.Stream()]
             self._step = self._e2e_step
@@ -336,6 +338,12 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
             dist.init_process_group(backend)
+    if args.tune:
+        from ozone_amd import _lib
+        for kv in args.tune:
+            key, val = kv.split("=", 1)
+            if _lib.lib().ozec_set_tuning(key.encode(), int(val)) != 0:
+                raise SystemExit(f"unknown tuning knob {kv}")
     wl = Workload(args.workload, rank, args.stripes, args.threads)
 
     def barrier():

@@ -40,6 +40,58 @@ CrcMath::CrcMath(uint32_t poly) : poly_(poly) {
   blob_b1_ = build_blob(1);
   blob_b2_ = build_blob(2);
   blob_b4_ = build_blob(4);
+  for (int i = 0; i < 5; ++i) g26_[i] = build_g26(kG26Cfg[i][0], kG26Cfg[i][1]);
+}
+
+// Block bit (0..127; dword d bit k = 32d + k, i.e. byte p/8 bit p%8) that index bit i of G26 table g reads,
+// -1 past the table's width.  Mirrors the extraction in kernels.hip g26_block:
+//   g = 4d+b   (16 tables): w_d bits 8b+2..8b+6                       ((w_d >> 8b) & 0x7c)
+//   g = 16+4h+b (8 tables): c_h = rotr(w_2h,5) on bits 2..4 of each byte, rotr(w_2h+1,2) on bits 5..6:
+//                            w_2h bits 8b+7..8b+9, then w_2h+1 bits 8b+7..8b+8 (mod 32)
+//   g = 24, 25  (4 bits)  : e = (rotr(w1,7) on bits 8b+2, rotr(w3,6) on bits 8b+3) & 0x0c0c0c0c, e |= e << 10;
+//                            bits 10..13 and 26..29 of e: the w1/w3 bits 8b+9 left over
+int g26_bit(int g, int i) {
+  if (g < 16) return i < 5 ? 32 * (g >> 2) + 8 * (g & 3) + 2 + i : -1;
+  if (g < 24) {
+    const int h = (g - 16) >> 2, b = (g - 16) & 3;
+    if (i < 3) return 64 * h + (8 * b + 7 + i) % 32;
+    if (i < 5) return 64 * h + 32 + (8 * b + 7 + i - 3) % 32;
+    return -1;
+  }
+  static const int k24[4] = {32 + 17, 96 + 17, 32 + 9, 96 + 9};
+  static const int k25[4] = {32 + 1, 96 + 1, 32 + 25, 96 + 25};
+  if (i >= 4) return -1;
+  return g == 24 ? k24[i] : k25[i];
+}
+
+std::vector<uint32_t> CrcMath::build_g26(int B, int D) const {
+  const int E = B * D;
+  std::vector<uint32_t> blob(g26_words(E), 0);
+  uint32_t bit[128];
+  for (int p = 0; p < 128; ++p) bit[p] = shift(t0_[1u << (p & 7)], 15 - (p >> 3));
+  for (int e = 0; e < E; ++e) {
+    const int r = e / B, s = e % B;
+    const uint64_t dist = (static_cast<uint64_t>(r) * 64 * B + s) * 16;
+    uint32_t sb[128];
+    for (int p = 0; p < 128; ++p) sb[p] = shift(bit[p], dist);
+    for (int g = 0; g < 26; ++g)
+      for (uint32_t v = 0; v < 32; ++v) {
+        uint32_t acc = 0;
+        for (int i = 0; i < 5; ++i) {
+          const int p = g26_bit(g, i);
+          if (p >= 0 && ((v >> i) & 1)) acc ^= sb[p];
+        }
+        blob[e * kG26Set + g * 32 + v] = acc;
+      }
+  }
+  auto fill_shift = [&](int off, uint64_t n) {
+    for (int g = 0; g < 7; ++g)
+      for (uint32_t v = 0; v < 32; ++v) blob[off + g * 32 + v] = shift(static_cast<uint32_t>(uint64_t{v} << (5 * g)), n);
+  };
+  fill_shift(g26_gshift(E), static_cast<uint64_t>(D) * 64 * B * 16);
+  for (int m = 0; m < 6; ++m) fill_shift(g26_tree(E) + m * 224, static_cast<uint64_t>(16) * B << m);
+  for (int v = 0; v < 256; ++v) blob[g26_t0(E) + v] = t0_[v];
+  return blob;
 }
 
 std::vector<uint32_t> CrcMath::build_blob(int B) const {

@@ -19,6 +19,8 @@ class CrcMath {
   uint32_t combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) const { return shift(crc_a, len_b) ^ crc_b; }
   // the device G5 table blob (kernels.hpp kG5* layout) for B = 1 or 4 blocks per lane per step
   const std::vector<uint32_t> &device_tables(int B) const { return B == 1 ? blob_b1_ : B == 2 ? blob_b2_ : blob_b4_; }
+  // the device G26 table blob (kernels.hpp kG26*) for slot `slot` of kG26Cfg
+  const std::vector<uint32_t> &g26_tables(int slot) const { return g26_[slot]; }
   uint32_t byte_table(int v) const { return t0_[v]; }
   uint32_t poly() const { return poly_; }
   // x^(8n) mod P in CrcUtil's reversed representation (CrcUtil.getMonomial)
@@ -41,7 +43,9 @@ class CrcMath {
   // op_[i] = operator for 2^i zero BYTES as a 32x32 GF(2) matrix (column c = image of bit c)
   uint32_t op_[64][32];
   std::vector<uint32_t> blob_b1_, blob_b2_, blob_b4_;
+  std::vector<uint32_t> g26_[5];
   std::vector<uint32_t> build_blob(int B) const;
+  std::vector<uint32_t> build_g26(int B, int D) const;
 };
 
 }  // namespace ozec

@@ -110,6 +110,26 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return d;
 }
 
+// XOR of a sequence of values with three-input XORs: (n-1)/2 ops for n values (every branch folds away
+// once the pushing loops are unrolled)
+struct XorChain {
+  uint32_t acc = 0, spare = 0;
+  int n = 0;
+  bool has_spare = false;
+  __device__ __forceinline__ void push(uint32_t v) {
+    if (n++ == 0) {
+      acc = v;
+    } else if (!has_spare) {
+      spare = v;
+      has_spare = true;
+    } else {
+      acc = xor3(acc, spare, v);
+      has_spare = false;
+    }
+  }
+  __device__ __forceinline__ uint32_t get() const { return has_spare ? acc ^ spare : acc; }
+};
+
 struct RegTab {
   uint32_t lo0, mid0;      // VGPR
   uint32_t lo1, mid1, top; // SGPR (wave-uniform)
@@ -464,6 +484,143 @@ __global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
   }
 }
 
+// ---- G26: step-grouped CRC with SDWA-friendly bit groups (table layout: kernels.hpp kG26*) ----------
+// A table lookup needs its 5-bit index times 4 (the byte offset of a dword entry).  Bits 8b+2..8b+6 of a
+// dword come out as exactly that with ONE op, `(w >> 8b) & 0x7c` (v_and_b32 with an SDWA byte select), so
+// 16 of the 26 groups of a 16-B block are read straight from the data dwords.  The 48 bits left over (bits
+// 8b+7..8b+9 of every byte boundary) are gathered by two rotate-and-merge registers (3 ops, 4 groups each)
+// and one register of 4-bit groups (5 ops, 2 groups): 36 VALU for 26 lookups, against 52 for 5-bit groups
+// cut at fixed offsets (shift + mask each).  Table g reads block bits crc_host.cpp g26_bit(g, *).
+
+__device__ __forceinline__ uint32_t lds_at(const uint32_t *T, uint32_t byte_off) {
+  return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(T) + byte_off);
+}
+__device__ __forceinline__ uint32_t rotr32(uint32_t w, int k) { return __builtin_amdgcn_alignbit(w, w, k); }
+// (a & m) | (b & ~m) in one v_bfi_b32 (the compiler splits the plain-C form into 3-4 ops here)
+__device__ __forceinline__ uint32_t bsel(uint32_t a, uint32_t b, uint32_t m) {
+  uint32_t d;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(d) : "s"(m), "v"(a), "v"(b));
+  return d;
+}
+// ((w >> 8q) & mask) in one op: v_and_b32 with an SDWA byte select (q = 0: plain AND; the compiler finds the
+// WORD_1 / BYTE_3 forms itself but not BYTE_1)
+template <int Q>
+__device__ __forceinline__ uint32_t byte_and(uint32_t w, uint32_t mask) {
+  if constexpr (Q == 1) {
+    uint32_t d;
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+        : "=v"(d) : "v"(w), "s"(mask));
+    return d;
+  } else {
+    return (w >> (8 * Q)) & mask;
+  }
+}
+
+// XOR of the 26 lookups of block b in the table set at T (26 x 32 words)
+__device__ __forceinline__ uint32_t g26_block(const uint32_t *T, const uint4 b) {
+  const uint32_t w[4] = {b.x, b.y, b.z, b.w};
+  uint32_t t[26];
+  auto four = [&](uint32_t v, int g0) {
+    t[g0] = lds_at(T, g0 * 128 + byte_and<0>(v, 0x7cu));
+    t[g0 + 1] = lds_at(T, (g0 + 1) * 128 + byte_and<1>(v, 0x7cu));
+    t[g0 + 2] = lds_at(T, (g0 + 2) * 128 + byte_and<2>(v, 0x7cu));
+    t[g0 + 3] = lds_at(T, (g0 + 3) * 128 + byte_and<3>(v, 0x7cu));
+  };
+#pragma unroll
+  for (int d = 0; d < 4; ++d) four(w[d], 4 * d);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) four(bsel(rotr32(w[2 * h], 5), rotr32(w[2 * h + 1], 2), 0x1c1c1c1cu), 16 + 4 * h);
+  uint32_t e = bsel(rotr32(w[1], 7), rotr32(w[3], 6), 0x04040404u) & 0x0c0c0c0cu;
+  e |= e << 10;
+  t[24] = lds_at(T, 24 * 128 + ((e >> 8) & 0x3cu));
+  t[25] = lds_at(T, 25 * 128 + ((e >> 24) & 0x3cu));
+  uint32_t r = xor3(t[0], t[1], t[2]);
+#pragma unroll
+  for (int g = 3; g + 1 < 26; g += 2) r = xor3(r, t[g], t[g + 1]);
+  return r ^ t[25];
+}
+
+// One wave per (cell, window), as crc_windows_vec, but lane l folds every block of its group of D steps
+// into its register through the table set of the block's distance to the group end (no per-step register
+// shift): S = shift_group(S) ^ XOR_{steps r, blocks s} G26[r*B+s](block).  Windows are front-padded with
+// virtual zero blocks to whole groups; virtual blocks are not loaded and add nothing.
+template <int B, int D, int PD = 1>
+__global__ __launch_bounds__(kBlock) void crc_windows_g26(const CrcArgs a) {
+  constexpr int E = B * D;
+  static_assert(D % 2 == 0, "two register sets alternate across steps");
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(E)];
+  load_tables(s_t, a.g26[g26_slot(B, D)], g26_words(E));
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t units = a.ncells * a.nwin;
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  for (int64_t u = bid * (kBlock / 64) + wave; u < units; u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
+    const int64_t c = u / a.nwin;
+    const int64_t w = u - c * a.nwin;
+    const bool last = w == a.nwin - 1;
+    const int64_t N = last ? a.len - w * a.bpc : a.bpc;
+    const int64_t m = N >> 4;
+    const int64_t G = (m + 64 * E - 1) / (64 * E);  // groups
+    const int64_t P = G * 64 * E - m;               // virtual zero blocks in front
+    const uint8_t *win = a.base + c * a.cell_stride + w * a.bpc;
+    uint32_t S = 0;
+    auto load_step = [&](int64_t t, uint4 (&dst)[B]) {
+      const bool pad = t * 64 * B < P;  // wave-uniform
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        const int64_t vb = t * 64 * B + lane * B + q - P;
+        if (!pad || vb >= 0) {
+          const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(win + vb * 16));
+          dst[q] = make_uint4(d[0], d[1], d[2], d[3]);
+        } else {
+          dst[q] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    };
+    if constexpr (PD == 1) {
+      uint4 xa[B], xb[B];
+      if (G > 0) load_step(0, xa);
+      for (int64_t g = 0; g < G; ++g) {
+#pragma unroll
+        for (int rr = 0; rr < D; ++rr) {
+          const int64_t t = g * D + rr;
+          uint4(&cur)[B] = (rr & 1) ? xb : xa;
+          uint4(&nxt)[B] = (rr & 1) ? xa : xb;
+          if (rr + 1 < D || g + 1 < G) load_step(t + 1, nxt);
+#pragma unroll
+          for (int q = 0; q < B; ++q) S ^= g26_block(s_t + ((D - 1 - rr) * B + (B - 1 - q)) * kG26Set, cur[q]);
+        }
+        if (g + 1 < G) S = g5_shift(s_t + g26_gshift(E), S);
+      }
+    } else {  // two steps in flight: three register sets rotated by copies
+      uint4 x0[B], x1[B], x2[B];
+      const int64_t T = G * D;
+      if (T > 0) load_step(0, x0);
+      if (T > 1) load_step(1, x1);
+      for (int64_t g = 0; g < G; ++g) {
+#pragma unroll
+        for (int rr = 0; rr < D; ++rr) {
+          const int64_t t = g * D + rr;
+          if (t + 2 < T) load_step(t + 2, x2);
+#pragma unroll
+          for (int q = 0; q < B; ++q) S ^= g26_block(s_t + ((D - 1 - rr) * B + (B - 1 - q)) * kG26Set, x0[q]);
+#pragma unroll
+          for (int q = 0; q < B; ++q) {
+            x0[q] = x1[q];
+            x1[q] = x2[q];
+          }
+        }
+        if (g + 1 < G) S = g5_shift(s_t + g26_gshift(E), S);
+      }
+    }
+    S = g5_lane_tree(s_t + g26_tree(E) - kG5Tree, S, lane);
+    for (int64_t i = m * 16; i < N; ++i) S = (S >> 8) ^ s_t[g26_t0(E) + ((S ^ win[i]) & 0xff)];
+    if (lane == 0) crc_emit(a, c, w, S, last);
+  }
+}
+
 // Scalar fallback: one thread per window, byte-at-a-time (any alignment, any bpc).
 __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
   __shared__ uint32_t s_t0[256];
@@ -630,6 +787,165 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 #pragma unroll
     for (int q = 0; q < K + R; ++q) {
       const uint32_t v = g5_lane_tree(s_t, S[q], lane);
+      if (lane == q) {
+        if (!e.verify) {
+          cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+        } else if (q >= K) {
+          cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+        } else if (cr.expected) {
+          const int64_t idx = (s * e.exp_units + e.in_unit[q]) * nwin + w;
+          const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
+          if (crc_finish(v, init, 0, 0) != ex)
+            atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
+        }
+      }
+    }
+  }
+}
+
+// Fused encode + CRC on the G26 scheme (B = 1): one wave per (stripe, window), D steps per group, every
+// unit's register updated with S ^= G26[D-1-rr](block) and shifted once per group.  GF coefficient tables
+// (TM): 1 = {lo0, lo1, mid0, mid1} from LDS in one ds_read_b128 broadcast + top as an SGPR operand;
+// 2 = lo1/mid1/top as SGPR operands, {lo0, mid0} from LDS in one ds_read_b64 broadcast; 3 = as 1 with top from
+// LDS too (ds_read_b32 broadcast).
+template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_g26(const EncCrcArgs e, const TabArgs<K * R> tabs) {
+  constexpr int E = D;
+  static_assert(D >= 1, "group of at least one step");
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(E)];
+  __shared__ __attribute__((aligned(16))) uint4 s_q[K * R];
+  __shared__ __attribute__((aligned(16))) uint2 s_d[K * R];
+  __shared__ uint32_t s_top[K * R];
+  const CodeArgs &a = e.code;
+  const CrcArgs &cr = e.crc;
+  load_tables(s_t, cr.g26[g26_slot(1, D)], g26_words(E));
+  for (int t = threadIdx.x; t < K * R; t += blockDim.x) {
+    s_q[t] = make_uint4(tabs.w[t][0], tabs.w[t][1], tabs.w[t][2], tabs.w[t][3]);
+    s_d[t] = make_uint2(tabs.w[t][0], tabs.w[t][2]);
+    s_top[t] = tabs.w[t][4];
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwin = cr.nwin;
+  const int64_t units = a.nstripes * nwin;
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  for (int64_t u = bid * (kBlock / 64) + wave; u < units; u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
+    const int64_t s = u / nwin;
+    const int64_t w = u - s * nwin;
+    const bool last = w == nwin - 1;
+    const int64_t N = last ? a.len - w * cr.bpc : cr.bpc;
+    const int64_t m = N >> 4;
+    const int32_t G = static_cast<int32_t>((m + 64 * D - 1) / (64 * D));
+    const int32_t P = G * 64 * D - static_cast<int32_t>(m);  // window <= 2 GiB: 32-bit block indices
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + s * a.in_stripe_stride + w * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + s * a.out_stripe_stride + w * cr.bpc);
+    uint32_t S[K + R];
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) S[q] = 0;
+    auto load_x = [&](int32_t t, uint4 (&dst)[K]) {
+      const int32_t vb = t * 64 + lane - P;
+      auto ld = [&](int j) {
+        const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<uint32_t>(vb) * 16u,
+                                                             static_cast<int>(a.in_off[j]), 2);
+        return make_uint4(d[0], d[1], d[2], d[3]);
+      };
+      if (__builtin_expect(t * 64 >= P, 1)) {  // wave-uniform: only the first steps hold virtual blocks
+#pragma unroll
+        for (int j = 0; j < K; ++j) dst[j] = ld(j);
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) dst[j] = vb >= 0 ? ld(j) : make_uint4(0, 0, 0, 0);
+      }
+    };
+    static_assert(!PF || D % 2 == 0, "prefetch alternates two register sets");
+    uint4 xa[K], xb[K];
+    if (PF && G > 0) load_x(0, xa);
+    for (int32_t g = 0; g < G; ++g) {
+#pragma unroll
+      for (int rr = 0; rr < D; ++rr) {
+        asm volatile("" ::: "memory");  // keep the LDS coefficient reads inside the step
+        const int32_t t = g * D + rr;
+        const int32_t vb = t * 64 + lane - P;
+        uint4(&x)[K] = (PF && (rr & 1)) ? xb : xa;
+        if constexpr (PF) {
+          if (rr + 1 < D || g + 1 < G) load_x(t + 1, (rr & 1) ? xa : xb);
+        } else {
+          load_x(t, x);
+        }
+        uint4 acc[R];
+        if constexpr (XORC) {
+          acc[0] = x[0];
+#pragma unroll
+          for (int j = 1; j < K; ++j) {
+            acc[0].x ^= x[j].x;
+            acc[0].y ^= x[j].y;
+            acc[0].z ^= x[j].z;
+            acc[0].w ^= x[j].w;
+          }
+        } else {
+          // parity dword = XOR of 3K permute results, reduced by chained three-input XORs (1.5 ops per
+          // coefficient instead of 2 for xor3-then-accumulate)
+          XorChain ch[R][4];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const uint32_t xw[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+            Sel sl[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) sl[c] = make_sel(xw[c]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const int tt = r * K + j;
+              uint32_t lo0, lo1, mid0, mid1, top;
+              if constexpr (TM == 1 || TM == 3) {
+                const uint4 q4 = s_q[tt];
+                lo0 = q4.x, lo1 = q4.y, mid0 = q4.z, mid1 = q4.w;
+                top = TM == 1 ? tabs.w[tt][4] : s_top[tt];
+              } else {
+                const uint2 d2 = s_d[tt];
+                lo0 = d2.x, mid0 = d2.y, lo1 = tabs.w[tt][1], mid1 = tabs.w[tt][3], top = tabs.w[tt][4];
+              }
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {
+                ch[r][c].push(TM == 2 ? perm_sv(lo1, lo0, sl[c].s0) : perm_vv(lo1, lo0, sl[c].s0));
+                ch[r][c].push(TM == 2 ? perm_sv(mid1, mid0, sl[c].s1) : perm_vv(mid1, mid0, sl[c].s1));
+                ch[r][c].push(TM == 3 ? perm_vv(top, top, sl[c].s2) : perm_top_s(top, sl[c].s2));
+              }
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            acc[r] = make_uint4(ch[r][0].get(), ch[r][1].get(), ch[r][2].get(), ch[r][3].get());
+        }
+        if (vb >= 0) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+            __builtin_amdgcn_raw_buffer_store_b128(d, rout, static_cast<uint32_t>(vb) * 16u,
+                                                   static_cast<int>(a.out_off[r]), 2);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < (XORC ? K : K + R); ++j) {
+          S[j] ^= g26_block(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (g + 1 < G) {
+#pragma unroll
+        for (int j = 0; j < (XORC ? K : K + R); ++j) S[j] = g5_shift(s_t + g26_gshift(E), S[j]);
+      }
+    }
+    if constexpr (XORC) {
+      S[K] = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) S[K] ^= S[j];
+    }
+    const uint32_t init = last ? cr.init_last : cr.init_full;
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) {
+      const uint32_t v = g5_lane_tree(s_t + g26_tree(E) - kG5Tree, S[q], lane);
       if (lane == q) {
         if (!e.verify) {
           cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
@@ -909,12 +1225,16 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
   const bool vec = aligned16(reinterpret_cast<intptr_t>(a.base)) && (a.ncells == 1 || aligned16(a.cell_stride)) &&
                    aligned16(a.bpc);
   if (vec) {
-    // defaults measured on MI355X: B = 2 (32-B lane chunks), 16384 blocks
+    // defaults measured on MI355X (scripts/tune_crc.py): G26 tables, B = 1 block per lane per step, groups of
+    // D = 4 steps, two steps of loads in flight, 16384 blocks
     const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : 16384;
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
-    if (g_tune.crc_variant == 4) hipLaunchKernelGGL(crc_windows_vec<4>, grid, block, 0, st, a);
-    else if (g_tune.crc_variant == 1) hipLaunchKernelGGL(crc_windows_vec<1>, grid, block, 0, st, a);
-    else hipLaunchKernelGGL(crc_windows_vec<2>, grid, block, 0, st, a);
+    switch (g_tune.crc_variant) {
+      case 1: hipLaunchKernelGGL(crc_windows_vec<2>, grid, block, 0, st, a); break;  // round-1 kernel, for A/B
+      case 11: hipLaunchKernelGGL((crc_windows_g26<1, 4, 1>), grid, block, 0, st, a); break;
+      case 12: hipLaunchKernelGGL((crc_windows_g26<2, 2, 1>), grid, block, 0, st, a); break;
+      default: hipLaunchKernelGGL((crc_windows_g26<1, 4, 2>), grid, block, 0, st, a); break;
+    }
   } else {
     hipLaunchKernelGGL(crc_windows_bytes, dim3(grid_for(units, kBlock)), dim3(kBlock), 0, st, a);
   }
@@ -927,27 +1247,40 @@ template <int K, int R>
 hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
   const int64_t units = e.code.nstripes * e.crc.nwin;
   const TabArgs<K * R> tabs = host_tabs<K * R>(e.code);
-  // defaults measured on MI355X: one wave per window with no grid-stride, LDS coefficient tables
+  // defaults measured on MI355X (scripts/tune_crc.py, profiles/r01/session2/tune_g26*.log): one wave per window
+  // with no grid-stride, G26 tables in groups of D = 2 steps, coefficient tables {lo0,lo1,mid0,mid1} by one
+  // ds_read_b128 broadcast and `top` as an SGPR operand (all from LDS past 18 coefficients: SGPR budget)
   const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : (units + 3) / 4;
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
-  constexpr bool kS = K * R <= 18;
+  constexpr int kTM = K * R <= 18 ? 1 : 3;
+  constexpr int kW = K + R >= 12 ? 3 : 4;  // rs-10-x: 14 unit registers and operands do not fit 128 VGPRs
+  const int v = g_tune.crc_variant;
+  if (v == 1) {  // round-1 kernel (5-bit groups at fixed offsets, register shift every step), kept for A/B
+    if constexpr (R == 1) {
+      if (e.code.all_ones) {
+        hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 1, true>), grid, block, 0, st, e, tabs);
+        return hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs);
+    return hipGetLastError();
+  }
   if constexpr (R == 1) {
-    if (e.code.all_ones && g_tune.crc_variant != 2) {
-      hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 1, true>), grid, block, 0, st, e, tabs);
+    if (e.code.all_ones && v != 2) {
+      hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1>), grid, block, 0, st, e, tabs);
       return hipGetLastError();
     }
   }
   if constexpr (K == 6 && R == 3) {  // the headline shape carries the tuning variants (scripts/tune_crc.py)
-    switch (g_tune.crc_variant) {
-      case 3: hipLaunchKernelGGL((encode_crc_vec<K, R, kS, 1, false>), grid, block, 0, st, e, tabs); break;
-      case 5: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, true>), grid, block, 0, st, e, tabs); break;
-      case 6: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 2, false>), grid, block, 0, st, e, tabs); break;
-      case 7: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 2, true>), grid, block, 0, st, e, tabs); break;
-      case 8: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 5>), grid, block, 0, st, e, tabs); break;
-      default: hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs); break;
+    switch (v) {
+      case 11: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, 1>), grid, block, 0, st, e, tabs); break;
+      case 12: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 1, 4, true>), grid, block, 0, st, e, tabs); break;
+      case 13: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 3>), grid, block, 0, st, e, tabs); break;
+      case 14: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 2>), grid, block, 0, st, e, tabs); break;
+      default: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM>), grid, block, 0, st, e, tabs); break;
     }
   } else {
-    hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs);
+    hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW>), grid, block, 0, st, e, tabs);
   }
   return hipGetLastError();
 }

@@ -39,6 +39,7 @@ struct CrcArgs {
   uint32_t *out;           // out[c * out_cell_stride + w]
   int64_t out_cell_stride; // in uint32 elements
   const uint32_t *tables[3];  // device G5 table blobs for this CRC type, B = 1, 2, 4 blocks per lane per step
+  const uint32_t *g26[5];     // device G26 table blobs for this CRC type, one per kG26Cfg entry
   uint32_t init_full;      // shift(0xFFFFFFFF, bpc bytes)
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
@@ -78,6 +79,28 @@ constexpr int kG5Tree = 1056;
 constexpr int kG5T0 = 2400;
 constexpr int kG5Words = 2656;
 constexpr int g5_slot(int B) { return B == 1 ? 0 : B == 2 ? 1 : 2; }
+
+// Device CRC "G26" table blob for the step-grouped kernels: a lane folds B blocks per step, D steps per
+// group, and every block is looked up in a table set that already includes its distance to the end of the
+// group, so the lane register is shifted once per group instead of once per step.  E = B*D sets:
+//   [0, E*kG26Set)          set e = r*B + s: block -> raw CRC advanced by (r*64*B + s)*16 zero bytes, i.e.
+//                           the block is s blocks before the end of its step and r steps before the end of
+//                           its group.  26 tables of 32 entries; table g is indexed by the 5 (or 4) block bits
+//                           g26 extraction g places at bits 2..6 of a byte (kernels.hip g26_block, host
+//                           crc_host.cpp g26_bit) -- one SDWA byte-select AND per lookup for 16 of them
+//   [g26_gshift(E), +224)   register shift by D*64*B*16 bytes (one group), 7 tables of 5-bit groups
+//   [g26_tree(E), +1344)    lane-tree shifts by 16*B*2^m bytes, m = 0..5 (as kG5Tree)
+//   [g26_t0(E), +256)       classic byte table T0
+constexpr int kG26Set = 26 * 32;
+constexpr int g26_gshift(int E) { return E * kG26Set; }
+constexpr int g26_tree(int E) { return E * kG26Set + 224; }
+constexpr int g26_t0(int E) { return E * kG26Set + 224 + 1344; }
+constexpr int g26_words(int E) { return E * kG26Set + 224 + 1344 + 256; }
+// (B, D) of each G26 blob slot
+constexpr int kG26Cfg[5][2] = {{1, 4}, {2, 2}, {1, 2}, {2, 4}, {1, 8}};
+constexpr int g26_slot(int B, int D) {
+  return B == 1 && D == 4 ? 0 : B == 2 && D == 2 ? 1 : B == 1 && D == 2 ? 2 : B == 2 && D == 4 ? 3 : 4;
+}
 
 // Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.
 struct TuneKnobs {

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X EC + checksum hot path (driver contract: one JSON line on rank 0).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5|crc|e2e]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c3r|c4|c5|crc|verify|e2e|host|queue]
 
 Default workload = BASELINE.json configs[1]: rs-6-3-1024k encode of 4096 stripes, device-resident on one
 MI355X.  A "step" is one ozec_encode_batch over the whole 4096-stripe batch (24 GiB of data cells read,
@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3r", "c4", "c5", "crc", "e2e", "host", "queue", "queue_pageable"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3r", "c4", "c5", "crc", "verify", "e2e", "host", "queue", "queue_pageable"])
     ap.add_argument("--stripes", type=int, default=0, help="override the stripe count (profiling only)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -146,16 +146,28 @@ class Workload:
         self.bpc = 16384
         self.nwin = n // self.bpc
         self.crc_type = ck.ChecksumType.CRC32C
-        if name == "crc":
+        if name in ("crc", "verify"):
             self.data = torch.empty((S, n), dtype=torch.uint8, device=dev)
             rc.fill_splitmix64_cells(self.data, n, S, n, SEED, rank * 10_000_000)
             self.crcs = torch.empty((S, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * n
-            self.alg_bytes = S * n + S * self.nwin * 4
-            self.kernel = "crc_windows_g26<1,4>"
-            self.config = {"workload": "CRC32C per 16 KiB window, device-resident", "cells": S, "cell_bytes": n,
-                           "bytes_per_checksum": self.bpc}
-            self._step = lambda: ck.checksum_windows_batch(self.crc_type, self.data, n, S, n, self.bpc, self.crcs)
+            if name == "crc":
+                self.alg_bytes = S * n + S * self.nwin * 4
+                self.kernel = "crc_windows_g26s<4,4>"
+                self.config = {"workload": "CRC32C per 16 KiB window, device-resident", "cells": S, "cell_bytes": n,
+                               "bytes_per_checksum": self.bpc}
+                self._step = lambda: ck.checksum_windows_batch(self.crc_type, self.data, n, S, n, self.bpc, self.crcs)
+            else:
+                ck.checksum_windows_batch(self.crc_type, self.data, n, S, n, self.bpc, self.crcs)
+                self.mism = torch.empty(S, dtype=torch.int32, device=dev)
+                # every data byte and every stored CRC read, one first-failure index per cell written
+                self.alg_bytes = S * n + S * self.nwin * 4 + S * 4
+                self.kernel = "crc_windows_g26s<4,4> (verify mode)"
+                self.config = {"workload": "CRC32C verify per 16 KiB window against stored CRCs (datanode scanner, "
+                                           "SURVEY 8(f) row 2), device-resident", "cells": S, "cell_bytes": n,
+                               "bytes_per_checksum": self.bpc}
+                self._step = lambda: ck.checksum_verify_batch(self.crc_type, self.data, n, S, n, self.bpc, self.crcs,
+                                                              self.mism)
             torch.cuda.synchronize()
             return
         units = k + p
@@ -275,7 +287,7 @@ def cpu_baseline(workload, budget_s):
         ins = [None if u in erased else units[u] for u in range(k + p)]
         job, data_bytes = (lambda: oracle.rs_decode(k, p, ins, erased)), k * n
         what = "rs-10-4-1024k decodes of 4 erased units (oracle rs_decode: RSRawDecoder + RSUtil.encodeData)"
-    elif workload == "crc":
+    elif workload in ("crc", "verify"):
         cell = cells(SEED, 900, 1, n)[0]
         job, data_bytes = (lambda: oracle.crc_windows(oracle.CRC32C, cell, 16384)), n
         what = "1 MiB cells checksummed as CRC32C/16 KiB windows (oracle crc_windows: CrcIntTable slice-by-8)"

@@ -621,6 +621,87 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26(const CrcArgs a) {
   }
 }
 
+// Streaming form of crc_windows_g26 (B = 1) for full windows of bpc % (1024*D) == 0 bytes: each wave owns a
+// contiguous run of `per_wave` windows (cell-major, so consecutive windows are consecutive in memory) and keeps
+// NS - 1 steps of loads in flight ACROSS window boundaries -- the per-window kernel drains its load pipeline at
+// the end of every window (16 steps of a 16 KiB window) and refills it at the start of the next.  At a window
+// end the 64 lane registers are merged, the CRC is emitted, and the register restarts at 0; no virtual blocks.
+// Window w of cell c is emitted as (c, w) with the full-window init (a short last window, if any, is left to
+// crc_windows_g26).  Persistent grid: one resident set of waves, each streaming its own stretch of HBM.
+// Code shape, from the ISA: the loads are unconditional (past the end of its run the cursor stays on the run's
+// last step, so the NS - 1 surplus loads re-read it) and land in a ring of NS register sets indexed by the
+// unrolled step (NS divides D), so no register copy or branch sits between a load and its use -- either makes
+// the compiler wait for every load in flight (vmcnt(0)) at every step.  For the same reason verify mode reads
+// the stored CRC with a scalar load (lgkmcnt), not a vector one.
+template <int D, int NS>
+__global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int64_t nfull, int64_t per_wave) {
+  static_assert(NS >= 2 && D % NS == 0, "the register ring must divide the unrolled group");
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(D)];
+  load_tables(s_t, a.g26[g26_slot(1, D)], g26_words(D));
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t total = a.ncells * nfull;
+  const int64_t u0 = (bid * (kBlock / 64) + wave) * per_wave;
+  if (u0 >= total) return;
+  const int64_t u1 = u0 + per_wave < total ? u0 + per_wave : total;
+  const int32_t G = static_cast<int32_t>(a.bpc >> 10) / D;  // groups of D steps per window (>= 1)
+  const int32_t T = G * D;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  // load cursor (wave-uniform): window lu = (cell lc, window lw), step lt
+  int64_t lu = u0, lc = u0 / nfull, lw = u0 - lc * nfull;
+  int32_t lt = 0;
+  const uint8_t *lbase = a.base + lc * a.cell_stride + lw * a.bpc + lane * 16;
+  auto load_next = [&](uint4 &dst) {
+    const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(lbase + lt * 1024));
+    dst = make_uint4(d[0], d[1], d[2], d[3]);
+    if (lt + 1 < T) {
+      ++lt;
+    } else if (lu + 1 < u1) {
+      lt = 0;
+      ++lu;
+      if (++lw == nfull) {
+        lw = 0;
+        ++lc;
+      }
+      lbase = a.base + lc * a.cell_stride + lw * a.bpc + lane * 16;
+    }
+  };
+  uint4 x[NS];
+#pragma unroll
+  for (int i = 0; i + 1 < NS; ++i) load_next(x[i]);
+  int64_t cc = u0 / nfull, cw = u0 - cc * nfull;  // compute cursor: (cell, window) of u
+  for (int64_t u = u0; u < u1; ++u) {
+    uint32_t ex = 0;
+    if (a.expected) ex = *(cu32 *)(a.expected + cc * a.out_cell_stride + cw);
+    uint32_t S = 0;
+    int32_t g = 0;
+    do {
+#pragma unroll
+      for (int rr = 0; rr < D; ++rr) {
+        load_next(x[(rr + NS - 1) % NS]);
+        S ^= g26_block(s_t + (D - 1 - rr) * kG26Set, x[rr % NS]);
+      }
+      if (g + 1 < G) S = g5_shift(s_t + g26_gshift(D), S);
+    } while (++g < G);
+    S = g5_lane_tree(s_t + g26_tree(D) - kG5Tree, S, lane);
+    if (lane == 0) {
+      if (a.expected) {
+        if (crc_finish(S, a.init_full, 0, 0) != (a.expected_be ? __builtin_bswap32(ex) : ex))
+          atomicMin(a.mismatch + cc, a.mismatch_base + static_cast<int32_t>(cw));
+      } else {
+        a.out[cc * a.out_cell_stride + cw] = crc_finish(S, a.init_full, a.raw, a.big_endian);
+      }
+    }
+    if (++cw == nfull) {
+      cw = 0;
+      ++cc;
+    }
+  }
+}
+
 // Scalar fallback: one thread per window, byte-at-a-time (any alignment, any bpc).
 __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
   __shared__ uint32_t s_t0[256];
@@ -1219,17 +1300,83 @@ hipError_t launch_code(const CodeArgs &a, hipStream_t st) {
   return hipSuccess;
 }
 
+namespace {
+
+int64_t device_cus() {
+  static const int64_t n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return static_cast<int64_t>(v);
+  }();
+  return n;
+}
+
+// Full windows of every cell through the streaming kernel on a persistent grid (resident blocks per CU x CUs,
+// or crc_grid blocks), the short last window of each cell (len % bpc) through the per-window kernel.
+template <int D, int NS>
+hipError_t launch_crc_stream(const CrcArgs &a, hipStream_t st) {
+  const int64_t nfull = a.len / a.bpc;
+  const int64_t total = a.ncells * nfull;
+  if (total > 0) {
+    static const int per_cu = [] {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&crc_windows_g26s<D, NS>),
+                                                       kBlock, 0) != hipSuccess || nb <= 0)
+        nb = 1;
+      return nb;
+    }();
+    const int64_t blocks = g_tune.crc_grid > 0 ? g_tune.crc_grid : per_cu * device_cus();
+    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(blocks * (kBlock / 64), total));
+    const int64_t per_wave = (total + waves - 1) / waves;
+    const int64_t grid = ((total + per_wave - 1) / per_wave + (kBlock / 64) - 1) / (kBlock / 64);
+    hipLaunchKernelGGL((crc_windows_g26s<D, NS>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, st, a, nfull,
+                       per_wave);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
+  if (nfull < a.nwin) {
+    CrcArgs t = a;
+    const int64_t off = nfull * a.bpc;
+    t.base = a.base + off;
+    t.len = a.len - off;
+    t.nwin = 1;
+    if (a.out) t.out = a.out + nfull;
+    if (a.expected) t.expected = a.expected + nfull;
+    t.mismatch_base = a.mismatch_base + static_cast<int32_t>(nfull);
+    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(16384, (a.ncells + 3) / 4))));
+    hipLaunchKernelGGL((crc_windows_g26<1, 4, 2>), grid, dim3(kBlock), 0, st, t);
+    return hipGetLastError();
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
 hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
   const int64_t units = a.ncells * a.nwin;
   if (units <= 0) return hipSuccess;
   const bool vec = aligned16(reinterpret_cast<intptr_t>(a.base)) && (a.ncells == 1 || aligned16(a.cell_stride)) &&
                    aligned16(a.bpc);
   if (vec) {
-    // defaults measured on MI355X (scripts/tune_crc.py): G26 tables, B = 1 block per lane per step, groups of
-    // D = 4 steps, two steps of loads in flight, 16384 blocks
+    const int v = g_tune.crc_variant;
+    // streaming kernel (D, ring) = (4, 4) for windows of whole 4 KiB groups; variants 20-24 for A/B
+    // (scripts/tune_crc.py): (4, 2), (8, 4), (4, 4), (8, 8), (2, 2)
+    if ((v == 0 || v >= 20) && a.bpc % (v == 21 || v == 23 ? 8192 : v == 24 ? 2048 : 4096) == 0) {
+      switch (v) {
+        case 20: return launch_crc_stream<4, 2>(a, st);
+        case 21: return launch_crc_stream<8, 4>(a, st);
+        case 23: return launch_crc_stream<8, 8>(a, st);
+        case 24: return launch_crc_stream<2, 2>(a, st);
+        default: return launch_crc_stream<4, 4>(a, st);
+      }
+    }
+    // per-window kernel: G26 tables, B = 1 block per lane per step, groups of D = 4 steps, two steps of loads in
+    // flight, 16384 blocks (scripts/tune_crc.py)
     const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : 16384;
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
-    switch (g_tune.crc_variant) {
+    switch (v) {
       case 1: hipLaunchKernelGGL(crc_windows_vec<2>, grid, block, 0, st, a); break;  // round-1 kernel, for A/B
       case 11: hipLaunchKernelGGL((crc_windows_g26<1, 4, 1>), grid, block, 0, st, a); break;
       case 12: hipLaunchKernelGGL((crc_windows_g26<2, 2, 1>), grid, block, 0, st, a); break;

@@ -6,8 +6,8 @@ tag = sys.argv[1]
 G, P = os.path.join("gpurun_out", "full"), os.path.join("profiles", tag)
 os.makedirs(P, exist_ok=True)
 KERNEL = {"c2": "gf_code_vec", "c3": "gf_code_vec", "c3r": "encode_crc_g26", "c4": "encode_crc_g26",
-          "c5": "encode_crc_g26", "crc": "crc_windows_g26"}
-for w in ("c2", "c3", "c3r", "c4", "c5", "crc", "e2e", "host"):
+          "c5": "encode_crc_g26", "crc": "crc_windows_g26", "verify": "crc_windows_g26"}
+for w in ("c2", "c3", "c3r", "c4", "c5", "crc", "verify", "e2e", "host"):
     if os.path.exists(f"{G}/bench_{w}.json"):
         shutil.copy(f"{G}/bench_{w}.json", f"{P}/bench_{w}.json")
 shutil.copy(f"{G}/pytest_gpu.log", f"{P}/pytest_gpu.log")

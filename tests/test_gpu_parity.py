@@ -184,6 +184,65 @@ def test_checksum_batch_vs_oracle(ctype, otype, bpc):
         assert (got[c] == oracle.crc_windows(otype, data[c], bpc)).all(), c
 
 
+@pytest.mark.parametrize("variant", [0, 1, 11, 13, 20, 21, 23, 24])
+def test_checksum_stream_runs_cross_cells(variant):
+    """crc_windows_g26s (the streaming kernel): per-wave runs of full windows that cross cell boundaries
+    (cell_stride > len, crc_grid forced small), the short last window of every cell (the per-window kernel's
+    launch), compute and verify modes -- every CRC kernel variant bit-exact vs the oracle."""
+    lib = L.lib()
+    C, bpc = 7, 16384
+    n = 5 * bpc + 4000
+    stride = n + 4096
+    data = np.stack(cells(SEED, 44000, C, n))
+    buf = np.zeros(C * stride, np.uint8)
+    for c in range(C):
+        buf[c * stride:c * stride + n] = data[c]
+    nwin = (n + bpc - 1) // bpc
+    ref = np.stack([oracle.crc_windows(oracle.CRC32C, data[c], bpc) for c in range(C)]).astype(np.uint32)
+    try:
+        assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+        assert lib.ozec_set_tuning(b"crc_grid", 3) == 0  # 12 waves for 35 full windows: runs of 3 cross cells
+        out = torch.zeros((C, nwin), dtype=torch.int32, device=DEV)
+        ck.checksum_windows_batch(ck.ChecksumType.CRC32C, t(buf), stride, C, n, bpc, out)
+        assert (h(out).view(np.uint32) == ref).all()
+        bad = buf.copy()
+        bad[3 * stride + 4 * bpc + 9] ^= 0x10  # window 4 of cell 3
+        bad[3 * stride + 2 * bpc + 5] ^= 0x04  # window 2 of cell 3: the first failure is the one reported
+        bad[6 * stride + n - 1] ^= 1           # short last window of cell 6
+        bad[0] ^= 0x80                         # window 0 of cell 0
+        mism = torch.zeros(C, dtype=torch.int32, device=DEV)
+        ck.checksum_verify_batch(ck.ChecksumType.CRC32C, t(bad), stride, C, n, bpc, t(ref.view(np.int32)), mism)
+        assert h(mism).tolist() == [0, -1, -1, 2, -1, -1, nwin - 1]
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+        lib.ozec_set_tuning(b"crc_grid", 0)
+
+
+def test_checksum_stream_verify_many_windows_per_wave():
+    """Verify mode with runs longer than 64 windows per wave (the stored CRCs are read 64 at a time)."""
+    lib = L.lib()
+    C, bpc = 3, 4096
+    n = 100 * bpc
+    data = np.stack(cells(SEED, 45000, C, n))
+    ref = np.stack([oracle.crc_windows(oracle.CRC32, data[c], bpc) for c in range(C)]).astype(np.uint32)
+    bad = data.copy()
+    # one block = 4 waves of 75 windows (global window u = 100 * cell + window)
+    bad[0, 74 * bpc + 3] ^= 1   # u = 74: wave 0, window 74 of its run (second group of 64)
+    bad[1, 70 * bpc] ^= 2       # u = 170: wave 2, window 20 of its run (first group)
+    bad[2, 99 * bpc + 7] ^= 4   # u = 299: the last window, wave 3, window 74 of its run
+    try:
+        assert lib.ozec_set_tuning(b"crc_grid", 1) == 0
+        mism = torch.zeros(C, dtype=torch.int32, device=DEV)
+        ck.checksum_verify_batch(ck.ChecksumType.CRC32, t(bad), n, C, n, bpc, t(ref.byteswap().view(np.int32)), mism,
+                                 expected_big_endian=True)
+        assert h(mism).tolist() == [74, 70, 99]
+        out = torch.zeros((C, n // bpc), dtype=torch.int32, device=DEV)
+        ck.checksum_windows_batch(ck.ChecksumType.CRC32, t(data), n, C, n, bpc, out)
+        assert (h(out).view(np.uint32) == ref).all()
+    finally:
+        lib.ozec_set_tuning(b"crc_grid", 0)
+
+
 def test_checksum_unaligned_and_big_endian():
     n, bpc = 70000, 16384
     data = cells(SEED, 41000, 1, n + 3)[0]

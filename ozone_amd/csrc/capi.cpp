@@ -954,6 +954,7 @@ int ozec_set_tuning(const char *key, int64_t value) {
   else if (k == "gf_variant") ozec::g_tune.gf_variant = static_cast<int>(value);
   else if (k == "crc_variant") ozec::g_tune.crc_variant = static_cast<int>(value);
   else if (k == "crc_grid") ozec::g_tune.crc_grid = value;
+  else if (k == "crc_run") ozec::g_tune.crc_run = value;
   else if (k == "unit_map") ozec::g_tune.unit_map = static_cast<int>(value);
   else if (k == "host_chunk" && value > 0) ozec::g_tune.host_chunk = value;
   else if (k == "host_slots" && value > 0) ozec::g_tune.host_slots = value;

@@ -103,6 +103,15 @@ __device__ __forceinline__ uint32_t perm_vv(uint32_t hi, uint32_t lo, uint32_t s
   asm("v_perm_b32 %0, %1, %2, %3" : "=v"(d) : "v"(hi), "v"(lo), "v"(sel));
   return d;
 }
+// A VALU write to the data VGPRs of a 16-B VMEM store issued just before it can corrupt the stored bytes on
+// MI355X: seen as a few wrong bytes per 16-lane group in the fused XOR kernels under load (scripts/diag_c4.py),
+// while hipcc inserts no wait states for this case.  Call right after the store(s): the data registers stay
+// allocated until two wait states after the store, so the next writer of those VGPRs cannot come sooner.
+__device__ __forceinline__ void store_data_hold(const uint4 &v) {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+}
+
 // gfx950 3-input bitwise op; truth table 0x96 = a ^ b ^ c
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t d;
@@ -296,6 +305,8 @@ __global__ __launch_bounds__(kBlock) void gf_code_vec_generic(const CodeArgs a, 
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) *reinterpret_cast<uint4 *>(ob + a.out_off[row0 + r]) = acc[r];
+#pragma unroll
+    for (int r = 0; r < R; ++r) store_data_hold(acc[r]);
   }
 }
 
@@ -1007,6 +1018,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
                                                    static_cast<int>(a.out_off[r]), 2);
           }
         }
+        if constexpr (XORC) store_data_hold(acc[0]);
 #pragma unroll
         for (int j = 0; j < (XORC ? K : K + R); ++j) {
           S[j] ^= g26_block(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K]);
@@ -1039,6 +1051,105 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
             atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
         }
       }
+    }
+  }
+}
+
+// Streaming fused XOR encode + CRC (the XOR codec: one all-ones row) for stripes whose windows are all full
+// (len % bpc == 0, bpc % (1024*D) == 0).  As crc_windows_g26s: each wave owns a contiguous run of (stripe,
+// window) units on a persistent grid and keeps NS - 1 steps of the K input loads in flight across window and
+// stripe ends; loads and parity stores are unconditional (no virtual blocks in full windows; past the end of
+// its run the load cursor stays on the run's last step), so no step waits for the whole pipeline.  The
+// per-window kernel above masks its loads and stores per lane for virtual blocks, and the compiler then waits
+// with vmcnt(0) at every step (ISA of encode_crc_g26<2, 1, 4, true, 1, 4, true>).  Encode mode only.
+template <int K, int D, int NS>
+__global__ __launch_bounds__(kBlock) void encode_xor_crc_g26s(const EncCrcArgs e, int64_t per_wave) {
+  static_assert(NS >= 2 && D % NS == 0, "the register ring must divide the unrolled group");
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(D)];
+  const CodeArgs &a = e.code;
+  const CrcArgs &cr = e.crc;
+  load_tables(s_t, cr.g26[g26_slot(1, D)], g26_words(D));
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwin = cr.nwin;
+  const int64_t total = a.nstripes * nwin;
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t u0 = (bid * (kBlock / 64) + wave) * per_wave;
+  if (u0 >= total) return;
+  const int64_t u1 = u0 + per_wave < total ? u0 + per_wave : total;
+  const int32_t G = static_cast<int32_t>(cr.bpc >> 10) / D;  // groups of D steps per window (>= 1)
+  const int32_t T = G * D;
+  const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
+  // load cursor (wave-uniform): unit lu = (stripe ls, window lw), step lt
+  int64_t lu = u0, ls = u0 / nwin, lw = u0 - ls * nwin;
+  int32_t lt = 0;
+  __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + ls * a.in_stripe_stride + lw * cr.bpc);
+  auto load_next = [&](uint4 (&dst)[K]) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, static_cast<int>(a.in_off[j]) + lt * 1024, 2);
+      dst[j] = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+    if (lt + 1 < T) {
+      ++lt;
+    } else if (lu + 1 < u1) {
+      lt = 0;
+      ++lu;
+      if (++lw == nwin) {
+        lw = 0;
+        ++ls;
+      }
+      rin = make_rsrc(a.in + ls * a.in_stripe_stride + lw * cr.bpc);
+    }
+  };
+  uint4 x[NS][K];
+#pragma unroll
+  for (int i = 0; i + 1 < NS; ++i) load_next(x[i]);
+  int64_t cs = u0 / nwin, cw = u0 - cs * nwin;  // compute cursor
+  for (int64_t u = u0; u < u1; ++u) {
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + cs * a.out_stripe_stride + cw * cr.bpc);
+    uint32_t S[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) S[j] = 0;
+    int32_t g = 0;
+    do {
+#pragma unroll
+      for (int rr = 0; rr < D; ++rr) {
+        load_next(x[(rr + NS - 1) % NS]);
+        const uint4(&cur)[K] = x[rr % NS];
+        uint4 par = cur[0];
+#pragma unroll
+        for (int j = 1; j < K; ++j) {
+          par.x ^= cur[j].x;
+          par.y ^= cur[j].y;
+          par.z ^= cur[j].z;
+          par.w ^= cur[j].w;
+        }
+        __attribute__((ext_vector_type(4))) unsigned int pd = {par.x, par.y, par.z, par.w};
+        __builtin_amdgcn_raw_buffer_store_b128(pd, rout, voff, static_cast<int>(a.out_off[0]) + (g * D + rr) * 1024,
+                                               2);
+        store_data_hold(par);
+#pragma unroll
+        for (int j = 0; j < K; ++j) S[j] ^= g26_block(s_t + (D - 1 - rr) * kG26Set, cur[j]);
+      }
+      if (g + 1 < G) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) S[j] = g5_shift(s_t + g26_gshift(D), S[j]);
+      }
+    } while (++g < G);
+    // the parity's register is the XOR of the inputs' registers (the raw CRC is GF(2)-linear)
+    uint32_t Sp = S[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) Sp ^= S[j];
+#pragma unroll
+    for (int q = 0; q <= K; ++q) {
+      const uint32_t v = g5_lane_tree(s_t + g26_tree(D) - kG5Tree, q < K ? S[q] : Sp, lane);
+      if (lane == q) cr.out[(cs * (K + 1) + q) * nwin + cw] = crc_finish(v, cr.init_full, cr.raw, cr.big_endian);
+    }
+    if (++cw == nwin) {
+      cw = 0;
+      ++cs;
     }
   }
 }
@@ -1302,37 +1413,33 @@ hipError_t launch_code(const CodeArgs &a, hipStream_t st) {
 
 namespace {
 
-int64_t device_cus() {
-  static const int64_t n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-      v = 256;
-    return static_cast<int64_t>(v);
-  }();
-  return n;
+// Windows per wave of the streaming kernels: runs of about crc_run bytes (256 KiB: measured best against
+// persistent grids and one-window runs, profiles/r01/session3/tune_grid.log), or an even split over crc_grid
+// blocks when that knob is set.  The grid is not persistent: blocks start in order, so the waves in flight
+// stream neighbouring stretches of HBM.
+int64_t stream_per_wave(int64_t total, int64_t bpc) {
+  if (g_tune.crc_grid > 0) {
+    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(g_tune.crc_grid * (kBlock / 64), total));
+    return (total + waves - 1) / waves;
+  }
+  const int64_t run = g_tune.crc_run > 0 ? g_tune.crc_run : int64_t{256} << 10;
+  return std::max<int64_t>(1, run / bpc);
 }
 
-// Full windows of every cell through the streaming kernel on a persistent grid (resident blocks per CU x CUs,
-// or crc_grid blocks), the short last window of each cell (len % bpc) through the per-window kernel.
+int64_t stream_grid(int64_t total, int64_t per_wave) {
+  return ((total + per_wave - 1) / per_wave + (kBlock / 64) - 1) / (kBlock / 64);
+}
+
+// Full windows of every cell through the streaming kernel, the short last window of each cell (len % bpc)
+// through the per-window kernel.
 template <int D, int NS>
 hipError_t launch_crc_stream(const CrcArgs &a, hipStream_t st) {
   const int64_t nfull = a.len / a.bpc;
   const int64_t total = a.ncells * nfull;
   if (total > 0) {
-    static const int per_cu = [] {
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&crc_windows_g26s<D, NS>),
-                                                       kBlock, 0) != hipSuccess || nb <= 0)
-        nb = 1;
-      return nb;
-    }();
-    const int64_t blocks = g_tune.crc_grid > 0 ? g_tune.crc_grid : per_cu * device_cus();
-    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(blocks * (kBlock / 64), total));
-    const int64_t per_wave = (total + waves - 1) / waves;
-    const int64_t grid = ((total + per_wave - 1) / per_wave + (kBlock / 64) - 1) / (kBlock / 64);
-    hipLaunchKernelGGL((crc_windows_g26s<D, NS>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, st, a, nfull,
-                       per_wave);
+    const int64_t per_wave = stream_per_wave(total, a.bpc);
+    hipLaunchKernelGGL((crc_windows_g26s<D, NS>), dim3(static_cast<unsigned>(stream_grid(total, per_wave))),
+                       dim3(kBlock), 0, st, a, nfull, per_wave);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
   }
@@ -1390,6 +1497,15 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
 
 namespace {
 
+template <int K, int D, int NS>
+hipError_t launch_xor_stream(const EncCrcArgs &e, hipStream_t st) {
+  const int64_t total = e.code.nstripes * e.crc.nwin;
+  const int64_t per_wave = stream_per_wave(total, e.crc.bpc);
+  hipLaunchKernelGGL((encode_xor_crc_g26s<K, D, NS>), dim3(static_cast<unsigned>(stream_grid(total, per_wave))),
+                     dim3(kBlock), 0, st, e, per_wave);
+  return hipGetLastError();
+}
+
 template <int K, int R>
 hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
   const int64_t units = e.code.nstripes * e.crc.nwin;
@@ -1411,6 +1527,16 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
     }
     hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs);
     return hipGetLastError();
+  }
+  if constexpr (R == 1 && K <= 6) {
+    // XOR codec, every window full: the streaming kernel, for A/B only (variants 20 / 21: ring of 2 / 4 steps).
+    // On C4 it reaches 62-71 % of the HBM roofline against 72-73 % for the per-window kernel below at every grid
+    // and run length tried (profiles/r01/session3/tune_grid.log).
+    if (e.code.all_ones && !e.verify && (v == 20 || v == 21) && e.code.len % e.crc.bpc == 0 &&
+        e.crc.bpc % 4096 == 0) {
+      if (v == 20) return launch_xor_stream<K, 4, 2>(e, st);
+      return launch_xor_stream<K, 4, K <= 3 ? 4 : 2>(e, st);
+    }
   }
   if constexpr (R == 1) {
     if (e.code.all_ones && v != 2) {

@@ -109,6 +109,7 @@ struct TuneKnobs {
   int crc_variant = 0;    // CRC kernel: 1/4 = B (default 2); fused: 2 no XOR-codec register shortcut,
                           //   3 SGPR tables, 5 prefetch, 6 B = 2, 7 both, 8 = at least 5 waves per SIMD
   int64_t crc_grid = 0;   // blocks for the CRC / fused kernels
+  int64_t crc_run = 0;    // streaming CRC kernels: bytes of consecutive windows per wave (default 256 KiB)
   int unit_map = 0;       // CodeArgs::unit_map for the coding kernels
   int64_t host_chunk = 256 << 10;  // host-buffer calls: bytes per unit per pipelined chunk
   int64_t host_slots = 8;          // host-buffer calls: staging slots (concurrent calls) per GPU

@@ -347,6 +347,34 @@ def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
             assert (crcs[s, u] == oracle.crc_windows(otype, units[u], bpc)).all(), (s, u)
 
 
+@pytest.mark.parametrize("variant", [0, 13, 20, 21])
+@pytest.mark.parametrize("k,n,bpc,S", [(2, 1 << 18, 16384, 5), (3, 65536, 4096, 7), (6, 1 << 17, 8192, 3)])
+def test_encode_xor_crc_stream_runs_cross_stripes(variant, k, n, bpc, S):
+    """encode_xor_crc_g26s (XOR codec, all windows full): per-wave runs of (stripe, window) units that cross
+    stripe boundaries (crc_grid forced to one block), block-major input layout and a separate parity block, parity
+    fully overwritten, every unit's window CRCs -- vs the oracle, for the streaming and per-window variants."""
+    lib = L.lib()
+    data = np.stack([np.stack(cells(SEED, 51000 + s * k, k, n)) for s in range(S)])  # [S][k][n]
+    nwin = n // bpc
+    d_in = t(np.ascontiguousarray(data.transpose(1, 0, 2)))  # block-major: [unit][stripe][cell]
+    d_out = torch.full((S, n), 0xA5, dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, k + 1, nwin), dtype=torch.int32, device=DEV)
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, 1, "xor"))
+    try:
+        assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+        assert lib.ozec_set_tuning(b"crc_grid", 1) == 0
+        e.encode_crc_batch(d_in, n, S * n, d_out, n, n, S, n, ck.ChecksumType.CRC32C, bpc, d_crc)
+        par, crcs = h(d_out), h(d_crc).view(np.uint32)
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+        lib.ozec_set_tuning(b"crc_grid", 0)
+    for s in range(S):
+        ref = oracle.xor_encode(list(data[s]))
+        assert (par[s] == ref).all(), s
+        for u, cell in enumerate(list(data[s]) + [ref]):
+            assert (crcs[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (s, u)
+
+
 # ------------------------------------------------------------------------------------------ full size
 
 
@@ -389,6 +417,55 @@ def test_full_size_rs_10_4_decode_4_erased():
         for i, u in enumerate(erased):
             assert torch.equal(out[:, i], units[:, u]), (erased, u)
     del units, out
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("variant", [0, 13])
+def test_full_size_xor_2_1_crc_4096_stripes(variant):
+    """BASELINE config C4 shape (4096 stripes of xor-2-1-1024k + CRC32C/16 KiB): parity equals torch's XOR of the
+    inputs and every window CRC equals the CRC-only kernel's, for the streaming (0) and per-window (13) fused
+    kernels.  At this size, under full load, a 16-B store whose data VGPRs are rewritten right after issue
+    corrupts bytes (kernels.hip store_data_hold); small cases do not show it."""
+    lib = L.lib()
+    n, S, bpc = 1 << 20, 4096, 16384
+    X = torch.empty((S, 3, n), dtype=torch.uint8, device=DEV)
+    for u in range(2):
+        rc.fill_splitmix64_cells(X[:, u], 3 * n, S, n, SEED, 300000 + u * S)
+    X[:, 2].fill_(0x5A)
+    crcs = torch.zeros((S, 3, n // bpc), dtype=torch.int32, device=DEV)
+    try:
+        assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+        enc("xor", 2, 1).encode_crc_batch(X, 3 * n, n, X[:, 2:], 3 * n, n, S, n, ck.ChecksumType.CRC32C, bpc, crcs)
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+    assert torch.equal(X[:, 2], torch.bitwise_xor(X[:, 0], X[:, 1]))
+    ref = torch.zeros_like(crcs)
+    ck.checksum_windows_batch(ck.ChecksumType.CRC32C, X, n, 3 * S, n, bpc, ref)
+    assert torch.equal(crcs, ref)
+    host = h(X[S - 1, 2, :bpc])
+    assert int(h(crcs[S - 1, 2, 0]).view(np.uint32)) == int(oracle.crc_windows(oracle.CRC32C, host, bpc)[0])
+    del X, crcs, ref
+    torch.cuda.empty_cache()
+
+
+def test_full_size_rs_6_3_crc_fused_matches_unfused():
+    """C5 shape at full size (4096 stripes): the fused encode + CRC32C kernel's parity equals the coding kernel's
+    and its window CRCs equal the CRC-only kernel's over all 9 units."""
+    k, p, n, S, bpc = 6, 3, 1 << 20, 4096, 16384
+    units = torch.empty((S, k + p, n), dtype=torch.uint8, device=DEV)
+    for u in range(k):
+        rc.fill_splitmix64_cells(units[:, u], (k + p) * n, S, n, SEED, 400000 + u * S)
+    e = enc("rs", k, p)
+    crcs = torch.zeros((S, k + p, n // bpc), dtype=torch.int32, device=DEV)
+    e.encode_crc_batch(units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n, ck.ChecksumType.CRC32C, bpc, crcs)
+    fused = units[:, k:].clone()
+    e.encode_batch(units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n)
+    assert torch.equal(fused, units[:, k:])
+    del fused
+    ref = torch.zeros_like(crcs)
+    ck.checksum_windows_batch(ck.ChecksumType.CRC32C, units, n, (k + p) * S, n, bpc, ref)
+    assert torch.equal(crcs, ref)
+    del units, crcs, ref
     torch.cuda.empty_cache()
 
 

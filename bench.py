@@ -269,6 +269,38 @@ class Workload:
         self._step()
 
 
+def pcie_ceiling(h2d_bytes, d2h_bytes, reps=5):
+    """Plain pinned<->HBM DMA rates of the e2e byte volumes: H2D alone, D2H alone, and both at once on two
+    streams (full duplex). The e2e/queue paths move 6 MiB in and 3 MiB out per rs-6-3 stripe, so the H2D rate
+    under duplex traffic is the ceiling for their data GB/s."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    hin = torch.empty(h2d_bytes, dtype=torch.uint8).pin_memory()
+    hout = torch.empty(d2h_bytes, dtype=torch.uint8).pin_memory()
+    din = torch.empty(h2d_bytes, dtype=torch.uint8, device=dev)
+    dout = torch.empty(d2h_bytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def timed(h2d, d2h):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if h2d:
+                with torch.cuda.stream(s1):
+                    din.copy_(hin, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s2):
+                    hout.copy_(dout, non_blocking=True)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+    timed(True, True)
+    t_h2d, t_d2h, t_both = timed(True, False), timed(False, True), timed(True, True)
+    return {"h2d_GBps": round(reps * h2d_bytes / t_h2d / 1e9, 2), "d2h_GBps": round(reps * d2h_bytes / t_d2h / 1e9, 2),
+            "duplex_h2d_GBps": round(reps * h2d_bytes / t_both / 1e9, 2),
+            "duplex_d2h_GBps": round(reps * d2h_bytes / t_both / 1e9, 2),
+            "bytes": {"h2d": h2d_bytes, "d2h": d2h_bytes},
+            "note": "contiguous pinned DMA copies of the same volumes, one H2D and one D2H stream"}
+
+
 # ------------------------------------------------------------------------------------------ CPU baseline
 
 
@@ -404,6 +436,13 @@ def main():
                      "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4),
                      "alg_bytes_per_launch": wl.alg_bytes},
     }
+    if args.workload in ("e2e", "queue", "queue_pageable"):
+        # the kernel is not the bound here: report the PCIe ceiling beside the value (never the value itself)
+        pc = pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
+        pc["value_frac_of_duplex_h2d"] = round(value / world / pc["duplex_h2d_GBps"], 4)
+        result["pcie"] = pc
+        result["roofline"]["note"] = ("e2e: kernel_ms is the whole PCIe-inclusive step; the bound is the link "
+                                      "(see pcie), not HBM")
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
     if rank == 0:

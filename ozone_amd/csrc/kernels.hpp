@@ -113,6 +113,7 @@ struct TuneKnobs {
   int unit_map = 0;       // CodeArgs::unit_map for the coding kernels
   int64_t host_chunk = 256 << 10;  // host-buffer calls: bytes per unit per pipelined chunk
   int64_t host_slots = 8;          // host-buffer calls: staging slots (concurrent calls) per GPU
+  int64_t queue_batches = 0;       // stripe queue: batches in the ring (0 = default), read at queue creation
 };
 extern TuneKnobs g_tune;
 

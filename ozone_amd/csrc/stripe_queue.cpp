@@ -6,6 +6,12 @@
 // caller's buffer when it is pinned, else through pinned staging), a full batch is one fused encode (+ CRC)
 // launch, and parity / CRCs come back by DMA into pinned callers' buffers or through staging.  Several
 // batches rotate, so the copies of batch i+1 overlap the kernel and copies of batch i.
+//
+// All H2D copies go in submission order on ONE stream; a batch's kernel and D2H copies follow on its own
+// stream behind an event.  With one H2D stream per batch instead, the H2D copies of all batches in the ring
+// shared the link at once, finished together, and their D2H copies then ran with the link's H2D direction
+// idle while the submitting thread waited for the oldest batch (rocprofv3 copy trace: H2D busy 119 of
+// 147 ms per 1024 stripes; 41 GB/s against a 57 GB/s link).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -15,11 +21,15 @@
 
 #include "../../include/ozec.h"
 #include "copy_pool.hpp"
+#include "kernels.hpp"
 #include "status.hpp"
 
 namespace {
 
 using ozec::set_error;
+
+// batches in the ring: copies of the newest batches keep the link busy while the oldest one drains
+constexpr size_t kDefaultBatches = 3;
 
 #define SQ_HIP(call)                                                                                      \
   do {                                                                                                    \
@@ -44,7 +54,8 @@ struct Pending {
 };
 
 struct Batch {
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // kernel + D2H of this batch
+  hipEvent_t copied = nullptr;   // recorded on the queue's H2D stream after this batch's last H2D copy
   hipEvent_t done = nullptr;
   uint8_t *d_units = nullptr;  // [S][k+rows][cell_len]
   uint32_t *d_crcs = nullptr;  // [S][k+rows][nwin]
@@ -63,6 +74,7 @@ struct ozec_stripe_queue {
   int k = 0, p = 0, rows = 0, ctype = OZEC_CHECKSUM_NONE, big_endian = 0;
   size_t cell_len = 0, S = 0, bpc = 0, nwin_max = 0;
   std::vector<Batch> batches;
+  hipStream_t h2d = nullptr;  // every H2D copy, in submission order
   size_t cur = 0;
   uint64_t next_ticket = 0;
   std::mutex mu;
@@ -79,6 +91,8 @@ struct ozec_stripe_queue {
     const int64_t ss = static_cast<int64_t>(stripe_bytes()), us = static_cast<int64_t>(cell_len);
     uint8_t *d_par = b.d_units + static_cast<size_t>(k) * cell_len;
     const size_t nw = nwin(b.len);
+    SQ_HIP(hipEventRecord(b.copied, h2d));
+    SQ_HIP(hipStreamWaitEvent(b.stream, b.copied, 0));
     if (ctype == OZEC_CHECKSUM_NONE) {
       if (int rc = ozec_encode_batch(enc, b.d_units, ss, us, d_par, ss, us, b.n, b.len, b.stream)) return rc;
     } else {
@@ -175,10 +189,12 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
   q->cell_len = cell_len;
   q->S = stripes_per_batch;
   q->nwin_max = q->nwin(cell_len);
-  q->batches.resize(3);
+  q->batches.resize(ozec::g_tune.queue_batches >= 2 ? static_cast<size_t>(ozec::g_tune.queue_batches) : kDefaultBatches);
   for (Batch &b : q->batches) {
     b.pend.resize(q->S);
-    hipError_t e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
+    hipError_t e = q->h2d ? hipSuccess : hipStreamCreateWithFlags(&q->h2d, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&b.copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&b.d_units), q->S * q->stripe_bytes());
     if (e == hipSuccess && q->ctype != OZEC_CHECKSUM_NONE) {
@@ -243,7 +259,7 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
     const size_t off = i * q->stripe_bytes() + static_cast<size_t>(j) * q->cell_len;
     int run = 1;
     while (len == q->cell_len && j + run < q->k && src[j + run] == src[j] + run * len) ++run;
-    SQ_HIP(hipMemcpyAsync(b->d_units + off, src[j], run * len, hipMemcpyHostToDevice, b->stream));
+    SQ_HIP(hipMemcpyAsync(b->d_units + off, src[j], run * len, hipMemcpyHostToDevice, q->h2d));
     j += run;
   }
   ++b->n;
@@ -288,6 +304,8 @@ int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket) {
 int ozec_stripe_queue_free(ozec_stripe_queue *q) {
   if (!q) return OZEC_OK;
   int rc = OZEC_OK;
+  // H2D copies of a batch never launched (submitted, then freed without flush) still write its device buffer
+  if (q->h2d && hipStreamSynchronize(q->h2d) != hipSuccess) rc = OZEC_EDEVICE;
   for (Batch &b : q->batches) {
     if (b.in_flight && hipEventSynchronize(b.done) != hipSuccess) rc = OZEC_EDEVICE;
     if (b.d_units) (void)hipFree(b.d_units);
@@ -295,8 +313,10 @@ int ozec_stripe_queue_free(ozec_stripe_queue *q) {
     if (b.h_stage) (void)hipHostFree(b.h_stage);
     if (b.h_crcs) (void)hipHostFree(b.h_crcs);
     if (b.done) (void)hipEventDestroy(b.done);
+    if (b.copied) (void)hipEventDestroy(b.copied);
     if (b.stream) (void)hipStreamDestroy(b.stream);
   }
+  if (q->h2d) (void)hipStreamDestroy(q->h2d);
   delete q;
   return rc == OZEC_OK ? OZEC_OK : set_error(rc, "device error while draining the stripe queue");
 }

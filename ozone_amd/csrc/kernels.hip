@@ -507,10 +507,12 @@ __device__ __forceinline__ uint32_t lds_at(const uint32_t *T, uint32_t byte_off)
   return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(T) + byte_off);
 }
 __device__ __forceinline__ uint32_t rotr32(uint32_t w, int k) { return __builtin_amdgcn_alignbit(w, w, k); }
-// (a & m) | (b & ~m) in one v_bfi_b32 (the compiler splits the plain-C form into 3-4 ops here)
+// (a & m) | (b & ~m) in one v_bitop3_b32 (truth table 0xca) with the mask in a VGPR: on gfx950 it issues at
+// the rate of a plain v_and_b32, while v_bfi_b32 (and any VALU op with an SGPR or literal operand) takes
+// ~1.7x as long per wave-instruction (scripts/valu_rate.hip, profiles/r01/session4/valu_rate.log)
 __device__ __forceinline__ uint32_t bsel(uint32_t a, uint32_t b, uint32_t m) {
   uint32_t d;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(d) : "s"(m), "v"(a), "v"(b));
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(d) : "v"(m), "v"(a), "v"(b));
   return d;
 }
 // ((w >> 8q) & mask) in one op: v_and_b32 with an SDWA byte select (q = 0: plain AND; the compiler finds the

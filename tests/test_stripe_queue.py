@@ -139,3 +139,46 @@ def test_queue_contiguous_pinned_stripe(n):
             assert all((a == b).all() for a, b in zip(par, ref)), t
             exp = np.concatenate([oracle.crc_windows(oracle.CRC32C, u, 4096) for u in [np.array(x) for x in d] + ref])
             assert (crcs == exp).all(), t
+
+
+@pytest.mark.parametrize("batches", [2, 5])
+def test_queue_ring_depth_and_ordered_h2d(batches):
+    """Every H2D copy runs on one queue-wide stream and each batch's kernel waits on its event: parity stays
+    bit-exact for any ring depth while the submitting thread keeps refilling the oldest batch."""
+    from ozone_amd import _lib
+    k, p, n = 6, 3, 1 << 15
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    assert _lib.lib().ozec_set_tuning(b"queue_batches", batches) == 0
+    try:
+        keep, jobs = [], []
+        with StripeQueue(enc, n, 3, ChecksumType.CRC32C, 8192) as q:
+            for s in range(3 * batches * 3 + 2):
+                pinned = s % 2 == 0
+                d = _stripe(93000 + 10 * s, k, n, pinned, keep)
+                par = _parity(p, n, pinned, keep)
+                crcs = np.zeros((k + p) * (n // 8192), np.uint32)
+                jobs.append((q.submit(d, par, crcs=crcs), d, par, crcs))
+            q.wait(jobs[-1][0])
+    finally:
+        _lib.lib().ozec_set_tuning(b"queue_batches", 0)
+    for t, d, par, crcs in jobs:
+        ref = oracle.rs_encode(k, p, d)
+        assert all((a == b).all() for a, b in zip(par, ref)), t
+        exp = np.concatenate([oracle.crc_windows(oracle.CRC32C, u, 8192) for u in list(d) + ref])
+        assert (crcs == exp).all(), t
+
+
+def test_queue_close_with_unlaunched_batch_drains():
+    """Closing a queue whose current batch was submitted but never launched waits for its H2D copies."""
+    k, p, n = 6, 3, 1 << 16
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    keep = []
+    q = StripeQueue(enc, n, 8)
+    for s in range(3):
+        q.submit(_stripe(94000 + 10 * s, k, n, True, keep), _parity(p, n, True, keep))
+    q.close()
+    with StripeQueue(enc, n, 8) as q2:  # the device is still usable
+        d = cells(SEED, 94100, k, n)
+        par = [np.zeros(n, np.uint8) for _ in range(p)]
+        q2.wait(q2.submit(d, par))
+    assert all((a == b).all() for a, b in zip(par, oracle.rs_encode(k, p, d)))

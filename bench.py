@@ -40,8 +40,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c3r", "c4", "c5", "crc", "verify", "e2e", "host", "queue", "queue_pageable"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3r", "c4", "c5", "crc", "verify", "e2e", "host", "queue", "queue_pageable"])
     ap.add_argument("--stripes", type=int, default=0, help="override the stripe count (profiling only)")
+    ap.add_argument("--erased", default="0,1,2,3",
+                    help="c3/c3r: erased unit indexes of rs-10-4 (SURVEY 8(d): 0,1,2,3 all data; 1,4,10,13 mixed)")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--threads", type=int, default=1, help="host workload: caller threads sharing one coder")
@@ -56,7 +58,7 @@ def parse():
 class Workload:
     """Allocates device-resident inputs once; step() launches one batch on the current stream."""
 
-    def __init__(self, name, rank, stripes_override, threads=1):
+    def __init__(self, name, rank, stripes_override, threads=1, erased=(0, 1, 2, 3)):
         from ozone_amd import checksum as ck
         from ozone_amd import rawcoder as rc
         self.name = name
@@ -134,7 +136,9 @@ class Workload:
                 self.q.wait(t)
             self._step = step
             return
-        if name in ("c2", "c5", "e2e"):
+        if name == "c1":
+            k, p, S = 3, 2, stripes_override or 1024
+        elif name in ("c2", "c5", "e2e"):
             k, p, S = 6, 3, stripes_override or (4096 if name != "e2e" else 1024)
         elif name in ("c3", "c3r"):
             k, p, S = 10, 4, stripes_override or 2048
@@ -186,7 +190,15 @@ class Workload:
         enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, "rs" if name != "c4" else "xor"))
         self.enc = enc
         stride = units * n
-        if name == "c2":
+        if name == "c1":
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * units * n
+            self.kernel = "gf_code_vec<3,2>"
+            self.config = {"workload": f"rs-3-2-1024k encode, {S} stripes, device-resident (BASELINE configs[0] shape; "
+                                       f"the reference runs it on the CPU)", "codec": "rs", "data_units": k,
+                           "parity_units": p, "cell_bytes": n, "stripes": S}
+            self._step = lambda: enc.encode_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n)
+        elif name == "c2":
             self.data_bytes = S * k * n
             self.alg_bytes = S * units * n
             self.kernel = "gf_code_vec<6,3>"
@@ -197,20 +209,21 @@ class Workload:
         elif name == "c3":
             enc.encode_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n)
             self.dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
-            self.erased = [0, 1, 2, 3]
+            self.erased = sorted(erased)
             present = [u for u in range(units) if u not in self.erased]
             self.out = torch.empty((S, 4, n), dtype=torch.uint8, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + len(self.erased)) * n
             self.kernel = "gf_code_vec<10,4>"
-            self.config = {"workload": f"rs-10-4-1024k decode, {S} stripes, 4 erased {{0,1,2,3}}, device-resident",
+            pat = ",".join(map(str, self.erased))
+            self.config = {"workload": f"rs-10-4-1024k decode, {S} stripes, 4 erased {{{pat}}}, device-resident",
                            "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S}
             self._step = lambda: self.dec.decode_batch(self.units, stride, n, present, self.erased, self.out, 4 * n,
                                                        n, S, n)
         elif name == "c3r":
             enc.encode_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n)
             self.dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
-            self.erased = [0, 1, 2, 3]
+            self.erased = sorted(erased)
             present = [u for u in range(units) if u not in self.erased]
             self.stored = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
             ck.checksum_windows_batch(self.crc_type, self.units, n, S * units, n, self.bpc, self.stored)
@@ -221,7 +234,8 @@ class Workload:
             self.alg_bytes = S * (k + 4) * n + S * (k + 4) * self.nwin * 4
             self.kernel = "encode_crc_g26<10,4> (reconstruct mode)"
             self.config = {"workload": "rs-10-4-1024k reconstruction: verify CRC32C of 10 read units + decode 4 + "
-                                       "CRC32C of rebuilt units, 2048 stripes, fused, device-resident",
+                                       f"CRC32C of rebuilt units {{{','.join(map(str, self.erased))}}}, 2048 stripes, "
+                                       "fused, device-resident",
                            "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
                            "bytes_per_checksum": self.bpc}
             self._step = lambda: self.dec.reconstruct_crc_batch(
@@ -337,10 +351,10 @@ def cpu_baseline(workload, budget_s):
                 "c3r": "rs-10-4-1024k stripes, 10 units -> 4 rebuilt + CRC32C/16 KiB of all 14 units (the "
                        "reconstruction's work)"}[workload] + " (oracle coder + crc_windows)"
     else:
-        k, p = 6, 3
+        k, p = (3, 2) if workload == "c1" else (6, 3)
         d = cells(SEED, 900, k, n)
         job, data_bytes = (lambda: oracle.rs_encode(k, p, d)), k * n
-        what = "rs-6-3-1024k stripes encoded (oracle rs_encode: C restatement of RSUtil.encodeData)"
+        what = f"rs-{k}-{p}-1024k stripes encoded (oracle rs_encode: C restatement of RSUtil.encodeData)"
     job()  # warm the tables
     done = [0] * threads
     stop = time.perf_counter() + budget_s
@@ -388,7 +402,10 @@ def main():
             key, val = kv.split("=", 1)
             if _lib.lib().ozec_set_tuning(key.encode(), int(val)) != 0:
                 raise SystemExit(f"unknown tuning knob {kv}")
-    wl = Workload(args.workload, rank, args.stripes, args.threads)
+    erased = [int(e) for e in args.erased.split(",")]
+    if len(erased) != 4 or len(set(erased)) != 4 or not all(0 <= e < 14 for e in erased):
+        raise SystemExit("--erased: four distinct unit indexes of rs-10-4 (0..13)")
+    wl = Workload(args.workload, rank, args.stripes, args.threads, erased)
 
     def barrier():
         if dist is not None:

@@ -7,7 +7,7 @@ O=$R/gpurun_out
 mkdir -p $O
 timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
-for w in ${WORKLOADS:-c2 c3 c4 c5 crc e2e}; do
+for w in ${WORKLOADS:-c1 c2 c3 c3r c4 c5 crc verify e2e queue}; do
   timeout -k 10 240 python bench.py --workload $w --steps 20 --warmup 5 > $O/bench_$w.json 2> $O/bench_$w.err || { echo "bench $w failed"; tail $O/bench_$w.err; exit 1; }
   cat $O/bench_$w.json
 done

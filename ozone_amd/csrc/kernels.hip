@@ -530,6 +530,7 @@ __device__ __forceinline__ uint32_t byte_and(uint32_t w, uint32_t mask) {
 }
 
 // XOR of the 26 lookups of block b in the table set at T (26 x 32 words)
+template <bool HALVES = false>
 __device__ __forceinline__ uint32_t g26_block(const uint32_t *T, const uint4 b) {
   const uint32_t w[4] = {b.x, b.y, b.z, b.w};
   uint32_t t[26];
@@ -539,6 +540,32 @@ __device__ __forceinline__ uint32_t g26_block(const uint32_t *T, const uint4 b) 
     t[g0 + 2] = lds_at(T, (g0 + 2) * 128 + byte_and<2>(v, 0x7cu));
     t[g0 + 3] = lds_at(T, (g0 + 3) * 128 + byte_and<3>(v, 0x7cu));
   };
+  if constexpr (HALVES) {
+    // two halves of 14 and 12 lookups with a scheduling fence between them: at most 14 lookup results are live
+    four(w[0], 0);
+    four(w[1], 4);
+    four(bsel(rotr32(w[0], 5), rotr32(w[1], 2), 0x1c1c1c1cu), 16);
+    uint32_t e = bsel(rotr32(w[1], 7), rotr32(w[3], 6), 0x04040404u) & 0x0c0c0c0cu;
+    e |= e << 10;
+    t[24] = lds_at(T, 24 * 128 + ((e >> 8) & 0x3cu));
+    t[25] = lds_at(T, 25 * 128 + ((e >> 24) & 0x3cu));
+    uint32_t r = xor3(t[0], t[1], t[2]);
+    r = xor3(r, t[3], t[4]);
+    r = xor3(r, t[5], t[6]);
+    r = xor3(r, t[7], t[16]);
+    r = xor3(r, t[17], t[18]);
+    r = xor3(r, t[19], t[24]);
+    r ^= t[25];
+    __builtin_amdgcn_sched_barrier(0);
+    four(w[2], 8);
+    four(w[3], 12);
+    four(bsel(rotr32(w[2], 5), rotr32(w[3], 2), 0x1c1c1c1cu), 20);
+    r = xor3(r, t[8], t[9]);
+#pragma unroll
+    for (int g = 10; g < 16; g += 2) r = xor3(r, t[g], t[g + 1]);
+    r = xor3(r, t[20], t[21]);
+    return xor3(r, t[22], t[23]);
+  }
 #pragma unroll
   for (int d = 0; d < 4; ++d) four(w[d], 4 * d);
 #pragma unroll
@@ -902,7 +929,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 // (TM): 1 = {lo0, lo1, mid0, mid1} from LDS in one ds_read_b128 broadcast + top as an SGPR operand;
 // 2 = lo1/mid1/top as SGPR operands, {lo0, mid0} from LDS in one ds_read_b64 broadcast; 3 = as 1 with top from
 // LDS too (ds_read_b32 broadcast).
-template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false>
+template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false, bool HV = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_g26(const EncCrcArgs e, const TabArgs<K * R> tabs) {
   constexpr int E = D;
   static_assert(D >= 1, "group of at least one step");
@@ -1023,7 +1050,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         if constexpr (XORC) store_data_hold(acc[0]);
 #pragma unroll
         for (int j = 0; j < (XORC ? K : K + R); ++j) {
-          S[j] ^= g26_block(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K]);
+          S[j] ^= g26_block<HV>(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K]);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -1554,7 +1581,12 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
       case 12: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 1, 4, true>), grid, block, 0, st, e, tabs); break;
       case 13: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 3>), grid, block, 0, st, e, tabs); break;
       case 14: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 2>), grid, block, 0, st, e, tabs); break;
-      default: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM>), grid, block, 0, st, e, tabs); break;
+      // 15: CRC lookups of a block without the fence between halves (the default until session 4); 16: halves at
+      // 5 waves per SIMD (96 VGPRs, 8 spilled).  Halves (default): 105 VGPRs instead of 114 and +0.6 % on C5 in an
+      // interleaved A/B (profiles/r01/session4/ab_c5.log); 5 waves gained nothing over 4.
+      case 15: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM>), grid, block, 0, st, e, tabs); break;
+      case 16: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 5, false, true>), grid, block, 0, st, e, tabs); break;
+      default: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs); break;
     }
   } else {
     switch (v) {

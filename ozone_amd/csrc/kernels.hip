@@ -1581,12 +1581,14 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
       case 12: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 1, 4, true>), grid, block, 0, st, e, tabs); break;
       case 13: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 3>), grid, block, 0, st, e, tabs); break;
       case 14: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 2>), grid, block, 0, st, e, tabs); break;
-      // 15: CRC lookups of a block without the fence between halves (the default until session 4); 16: halves at
-      // 5 waves per SIMD (96 VGPRs, 8 spilled).  Halves (default): 105 VGPRs instead of 114 and +0.6 % on C5 in an
-      // interleaved A/B (profiles/r01/session4/ab_c5.log); 5 waves gained nothing over 4.
+      // CRC lookups of a block in two fenced halves (g26_block<true>: at most 14 results live) and groups of D = 4
+      // steps: 123 VGPRs, 0 spilled.  Interleaved A/Bs (profiles/r01/session4/ab_c5*.log): halves at D = 2 +0.6 %
+      // over the fence-free block (105 instead of 114 VGPRs), D = 4 on top +2.7 %; 5 waves per SIMD gained nothing.
+      // 15: fence-free D = 2 (the default until session 4); 16: halves, D = 2, 5 waves; 17: halves, D = 2.
       case 15: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM>), grid, block, 0, st, e, tabs); break;
       case 16: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 5, false, true>), grid, block, 0, st, e, tabs); break;
-      default: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs); break;
+      case 17: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs); break;
+      default: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs); break;
     }
   } else {
     switch (v) {
@@ -1594,6 +1596,7 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
       case 12: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW, true>), grid, block, 0, st, e, tabs); break;
       case 13: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 1, kW>), grid, block, 0, st, e, tabs); break;
       case 14: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 2>), grid, block, 0, st, e, tabs); break;
+      case 17: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, kW, false, true>), grid, block, 0, st, e, tabs); break;
       default: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW>), grid, block, 0, st, e, tabs); break;
     }
   }

@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 O=$R/gpurun_out/abc5
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "rs63_variants" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_variants.log 2>&1 || { tail -30 $O/pytest_variants.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "variants_vs_oracle" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_variants.log 2>&1 || { tail -30 $O/pytest_variants.log; exit 1; }
 tail -1 $O/pytest_variants.log
 for r in 1 2; do
   for v in ${VARIANTS:-0 15 16}; do

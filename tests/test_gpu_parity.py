@@ -347,7 +347,7 @@ def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
             assert (crcs[s, u] == oracle.crc_windows(otype, units[u], bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [11, 12, 13, 14, 15, 16])
+@pytest.mark.parametrize("variant", [11, 12, 13, 14, 15, 16, 17])
 @pytest.mark.parametrize("n,bpc,S", [(1 << 18, 16384, 3), (50000, 4096, 2)])
 def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
     """Every tuning variant of the rs-6-3 fused encode + CRC32C kernel (D = 4, prefetch, table placements,
@@ -359,6 +359,30 @@ def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
     d_in = t(data)
     d_out = torch.zeros((S, p, n), dtype=torch.uint8, device=DEV)
     d_crc = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    try:
+        assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+        e.encode_crc_batch(d_in, k * n, n, d_out, p * n, n, S, n, ck.ChecksumType.CRC32C, bpc, d_crc)
+        par, crcs = h(d_out), h(d_crc).view(np.uint32)
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+    for s in range(S):
+        ref = oracle.rs_encode(k, p, list(data[s]))
+        assert all((par[s, r] == ref[r]).all() for r in range(p)), s
+        for u, cell in enumerate(list(data[s]) + ref):
+            assert (crcs[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (s, u)
+
+
+@pytest.mark.parametrize("variant", [0, 11, 17])
+@pytest.mark.parametrize("k,p", [(10, 4), (6, 2), (3, 2)])
+def test_encode_crc_other_shapes_variants_vs_oracle(variant, k, p):
+    """Fused encode + CRC32C variants of the other RS shapes (D = 2 default, D = 4, D = 4 with fenced halves)."""
+    lib = L.lib()
+    n, bpc, S = 1 << 17, 16384, 2
+    data = np.stack([np.stack(cells(SEED, 53000 + s * k, k, n)) for s in range(S)])
+    d_in = t(data)
+    d_out = torch.zeros((S, p, n), dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, k + p, n // bpc), dtype=torch.int32, device=DEV)
     e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
     try:
         assert lib.ozec_set_tuning(b"crc_variant", variant) == 0

@@ -1,25 +1,38 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X EC + checksum hot path (driver contract: one JSON line on rank 0).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c3r|c4|c5|crc|verify|e2e|host|queue]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|...]
 
-Default workload = BASELINE.json configs[1]: rs-6-3-1024k encode of 4096 stripes, device-resident on one
-MI355X.  A "step" is one ozec_encode_batch over the whole 4096-stripe batch (24 GiB of data cells read,
-12 GiB of parity written).  For N > 1 (torchrun) every rank encodes its own 4096 stripes on its own GPU
-(stripes are independent: no collective on the data path, "scaling": "weak"); RCCL is used only for the
-start/stop barriers and the max-over-ranks reduction of the elapsed time.
+Default workload = BASELINE.json configs[1]: rs-6-3-1024k encode of 4096 stripes per GPU, device-resident.
+A "step" is one ozec_encode_batch over the GPU's 4096 stripes (24 GiB of data cells read, 12 GiB of parity
+written).
 
-value      = data bytes of all ranks / max-over-ranks wall time of the K timed steps (GB = 1e9 B)
-roofline   = algorithmic bytes per launch (9 x 1 MiB per stripe x 4096) / mean kernel time measured with
-             HIP events on the launch stream, against 8.0 TB/s; traffic = rocprofv3 PMC bytes per launch
-             read from profiles/traffic_<workload>.json when it has been measured, else null
-cpu_baseline (rank 0, N = 1): the oracle/ C restatement of the same work timed on this host's cores on a
-             bounded sample (threads share one coder, as RawErasureCoderBenchmark.java:201-206 does)
+Multi-GPU: one process per GPU.  Under torchrun the ranks come from the environment; with
+`--gpus N` and no WORLD_SIZE this script starts the N rank processes itself (before anything touches a GPU) and
+waits for them.  A global batch of 4096·N stripes is split into contiguous stripe ranges (ozone_amd.shard
+.stripe_range), one per GPU, with no collective on the data path ("scaling": "weak": 4096 stripes per GPU).
+torch.distributed only carries barriers and max-over-ranks reductions of the timings.
+
+value        = data bytes of all ranks / max-over-ranks wall time of the K timed steps (GB = 1e9 B)
+roofline     = algorithmic bytes per launch / mean kernel time from HIP events on the launch stream (max over
+               ranks), against 8.0 TB/s; `traffic` = HBM bytes per launch of the same kernel measured by this run
+               in two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE, gfx950 correction), N = 1 only
+e2e          = BASELINE configs[4] (C5) at the same N: one batch of 8192 rs-6-3-1024k stripes in shared host
+               memory, each GPU encoding + CRC32C'ing its stripe range from NUMA-local pinned pages
+               (ozec_encode_crc_host_batch), parity and CRCs back into the batch
+cpu_baseline = (rank 0, N = 1) oracle/cpu_baseline.c compiled -march=native on this host and run on a bounded
+               sample of the same work with T = the CPUs this process may use and with 1 thread
 """
 import argparse
+import ctypes
 import json
+import mmap
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import threading
 import time
 
@@ -33,23 +46,109 @@ MIB = 1 << 20
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED = 0x00EC5EED
 METRIC = "EC encode GB/s (data bytes) rs-6-3-1024k @1/8 GPUs + % HBM roofline"
+WORKLOADS = ["c1", "c2", "c3", "c3r", "c4", "c4s", "c5", "c5dev", "crc", "verify", "host", "queue", "queue_pageable",
+             "stream"]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c3r", "c4", "c5", "crc", "verify", "e2e", "host", "queue", "queue_pageable"])
-    ap.add_argument("--stripes", type=int, default=0, help="override the stripe count (profiling only)")
+    ap.add_argument("--workload", default="c2", choices=WORKLOADS)
+    ap.add_argument("--stripes", type=int, default=0, help="override the per-GPU stripe count (profiling only)")
     ap.add_argument("--erased", default="0,1,2,3",
                     help="c3/c3r: erased unit indexes of rs-10-4 (SURVEY 8(d): 0,1,2,3 all data; 1,4,10,13 mixed)")
-    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of each CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the C5 end-to-end leg of the default line")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC traffic passes")
+    ap.add_argument("--e2e-stripes", type=int, default=8192, help="C5 batch size (all GPUs together)")
+    ap.add_argument("--e2e-steps", type=int, default=3)
+    ap.add_argument("--chunk", type=int, default=0, help="C5: stripes per pipelined chunk (0 = library default)")
     ap.add_argument("--threads", type=int, default=1, help="host workload: caller threads sharing one coder")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="ozec_set_tuning knob (A/B and profiling runs only; defaults are the measured best)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------------------------------ launch
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_workers(args):
+    """--gpus N without torchrun: start N rank processes (this process never touches a GPU) and wait."""
+    same = os.environ.get("OZEC_BENCH_SAME_DEVICE") == "1"
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if not same and ndev < args.gpus:
+        raise SystemExit(f"--gpus {args.gpus}: only {ndev} visible GPU(s)")
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def node_cpus(node):
+    try:
+        text = open(f"/sys/devices/system/node/node{node}/cpulist").read().strip()
+    except OSError:
+        return set()
+    cpus = set()
+    for part in text.split(","):
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def bind_process_to_gpu_node(dev):
+    """Run this rank on the CPUs of its GPU's NUMA node (the staging copies and DMA descriptors live there)."""
+    from ozone_amd.stripe_queue import device_numa_node
+    node = device_numa_node(dev)
+    if node < 0:
+        return node
+    want = node_cpus(node) & os.sched_getaffinity(0)
+    if want:
+        os.sched_setaffinity(0, want)
+    return node
+
+
+def usable_cpus():
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def host_info():
+    info = {"cpus_usable": usable_cpus(), "cpus_online": os.cpu_count()}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            key, _, val = line.partition(":")
+            if key.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "NUMA node(s)"):
+                info[key.strip()] = val.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
 
 
 # ------------------------------------------------------------------------------------------ workloads
@@ -58,10 +157,12 @@ def parse():
 class Workload:
     """Allocates device-resident inputs once; step() launches one batch on the current stream."""
 
-    def __init__(self, name, rank, stripes_override, threads=1, erased=(0, 1, 2, 3)):
+    def __init__(self, name, rank, world, stripes_override, threads=1, erased=(0, 1, 2, 3)):
         from ozone_amd import checksum as ck
         from ozone_amd import rawcoder as rc
+        from ozone_amd.shard import stripe_range
         self.name = name
+        self.stream = torch.cuda.current_stream()
         dev = torch.device("cuda", torch.cuda.current_device())
         n = MIB
         self.n = n
@@ -138,26 +239,28 @@ class Workload:
             return
         if name == "c1":
             k, p, S = 3, 2, stripes_override or 1024
-        elif name in ("c2", "c5", "e2e"):
-            k, p, S = 6, 3, stripes_override or (4096 if name != "e2e" else 1024)
+        elif name in ("c2", "c5dev"):
+            k, p, S = 6, 3, stripes_override or 4096
         elif name in ("c3", "c3r"):
             k, p, S = 10, 4, stripes_override or 2048
-        elif name == "c4":
+        elif name in ("c4", "c4s"):
             k, p, S = 2, 1, stripes_override or 16 * 256
-        else:  # crc
+        else:  # crc / verify
             k, p, S = 1, 0, stripes_override or 8192
         self.k, self.p, self.S = k, p, S
+        # this rank's share of the global batch (S stripes per GPU, contiguous ranges: SURVEY 8(e))
+        self.lo, self.hi = stripe_range(S * world, rank, world)
         self.bpc = 16384
         self.nwin = n // self.bpc
         self.crc_type = ck.ChecksumType.CRC32C
         if name in ("crc", "verify"):
             self.data = torch.empty((S, n), dtype=torch.uint8, device=dev)
-            rc.fill_splitmix64_cells(self.data, n, S, n, SEED, rank * 10_000_000)
+            rc.fill_splitmix64_cells(self.data, n, S, n, SEED, self.lo)
             self.crcs = torch.empty((S, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * n
             if name == "crc":
                 self.alg_bytes = S * n + S * self.nwin * 4
-                self.kernel = "crc_windows_g26s<4,4>"
+                self.kernel = "crc_windows_g26s"
                 self.config = {"workload": "CRC32C per 16 KiB window, device-resident", "cells": S, "cell_bytes": n,
                                "bytes_per_checksum": self.bpc}
                 self._step = lambda: ck.checksum_windows_batch(self.crc_type, self.data, n, S, n, self.bpc, self.crcs)
@@ -166,7 +269,7 @@ class Workload:
                 self.mism = torch.empty(S, dtype=torch.int32, device=dev)
                 # every data byte and every stored CRC read, one first-failure index per cell written
                 self.alg_bytes = S * n + S * self.nwin * 4 + S * 4
-                self.kernel = "crc_windows_g26s<4,4> (verify mode)"
+                self.kernel = "crc_windows_g26s"
                 self.config = {"workload": "CRC32C verify per 16 KiB window against stored CRCs (datanode scanner, "
                                            "SURVEY 8(f) row 2), device-resident", "cells": S, "cell_bytes": n,
                                "bytes_per_checksum": self.bpc}
@@ -175,20 +278,36 @@ class Workload:
             torch.cuda.synchronize()
             return
         units = k + p
-        if name == "e2e":
-            self.host_in = torch.empty((S, k, n), dtype=torch.uint8).pin_memory()
-            self.host_out = torch.empty((S, p, n), dtype=torch.uint8).pin_memory()
-            self.host_crc = torch.empty((S, units, self.nwin), dtype=torch.int32).pin_memory()
-            tmp = torch.empty((S, k, n), dtype=torch.uint8, device=dev)
-            rc.fill_splitmix64_cells(tmp, n, S * k, n, SEED, rank * 10_000_000)
-            self.host_in.copy_(tmp)
-            del tmp
+        enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, "rs" if k != 2 else "xor"))
+        self.enc = enc
+        if name == "c4":
+            # block-major, as a datanode stores EC block groups: 16 groups of 2 data blocks + 1 parity block of
+            # 256 MiB (one block file per unit), unit stride 256 MiB, stripe s of a group at offset s MiB
+            G, B = S // 256, 256
+            self.blocks = torch.empty((G, units, B * n), dtype=torch.uint8, device=dev)
+            for u in range(k):
+                rc.fill_splitmix64_cells(self.blocks[:, u], units * B * n, G, B * n, SEED, self.lo + u * G * 1000)
+            self.crcs = torch.empty((G, B, units, self.nwin), dtype=torch.int32, device=dev)
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * units * n + S * units * self.nwin * 4
+            self.kernel = "encode_crc_g26<2,1>"
+            self.config = {"workload": "xor-2-1-1024k + CRC32C/16 KiB over 256 MiB blocks, 16 block groups x 256 "
+                                       "stripes, fused, device-resident", "codec": "xor", "data_units": k,
+                           "parity_units": p, "cell_bytes": n, "stripes": S, "bytes_per_checksum": self.bpc,
+                           "layout": "block-major: [group][unit][256 MiB block], unit stride 256 MiB"}
+            us = B * n
+
+            def step():
+                for g in range(G):
+                    base = self.blocks[g]
+                    enc.encode_crc_batch(base, n, us, base[k:], n, us, B, n, self.crc_type, self.bpc, self.crcs[g])
+            self._step = step
+            torch.cuda.synchronize()
+            return
         # HBM layout: stripe-major, units contiguous: unit u of stripe s at s*(k+p)*n + u*n
         self.units = torch.empty((S, units, n), dtype=torch.uint8, device=dev)
         for u in range(k):
-            rc.fill_splitmix64_cells(self.units[:, u], units * n, S, n, SEED, rank * 10_000_000 + u * S)
-        enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, "rs" if name != "c4" else "xor"))
-        self.enc = enc
+            rc.fill_splitmix64_cells(self.units[:, u], units * n, S, n, SEED, u * S * world + self.lo)
         stride = units * n
         if name == "c1":
             self.data_bytes = S * k * n
@@ -202,7 +321,7 @@ class Workload:
             self.data_bytes = S * k * n
             self.alg_bytes = S * units * n
             self.kernel = "gf_code_vec<6,3>"
-            self.config = {"workload": f"rs-6-3-1024k encode, {S} stripes, device-resident (BASELINE configs[1])",
+            self.config = {"workload": f"rs-6-3-1024k encode, {S} stripes per GPU, device-resident (BASELINE configs[1])",
                            "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
                            "layout": "stripe-major [stripe][unit][cell] in HBM"}
             self._step = lambda: enc.encode_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n)
@@ -232,55 +351,206 @@ class Workload:
             self.mism = torch.empty(S, dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + 4) * n + S * (k + 4) * self.nwin * 4
-            self.kernel = "encode_crc_g26<10,4> (reconstruct mode)"
+            self.kernel = "encode_crc_g26<10,4>"
             self.config = {"workload": "rs-10-4-1024k reconstruction: verify CRC32C of 10 read units + decode 4 + "
-                                       f"CRC32C of rebuilt units {{{','.join(map(str, self.erased))}}}, 2048 stripes, "
+                                       f"CRC32C of rebuilt units {{{','.join(map(str, self.erased))}}}, {S} stripes, "
                                        "fused, device-resident",
                            "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
                            "bytes_per_checksum": self.bpc}
             self._step = lambda: self.dec.reconstruct_crc_batch(
                 self.units, stride, n, present, self.erased, self.out, 4 * n, n, S, n, self.crc_type, self.bpc,
                 self.out_crc, d_expected=self.stored, d_mismatch=self.mism)
-        elif name in ("c4", "c5"):
+        else:  # c4s (xor-2-1 stripe-major) / c5dev (rs-6-3): fused encode + CRC, device-resident
             self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * units * n + S * units * self.nwin * 4
             self.kernel = f"encode_crc_g26<{k},{p}>"
-            wl = ("xor-2-1-1024k + CRC32C/16 KiB, 16 block groups x 256 stripes" if name == "c4"
-                  else "rs-6-3-1024k encode + CRC32C/16 KiB, 4096 stripes")
-            self.config = {"workload": wl + ", fused, device-resident", "codec": "xor" if name == "c4" else "rs",
+            wl = ("xor-2-1-1024k + CRC32C/16 KiB, stripe-major" if name == "c4s"
+                  else "rs-6-3-1024k encode + CRC32C/16 KiB (the C5 kernel without PCIe)")
+            self.config = {"workload": f"{wl}, {S} stripes, fused, device-resident", "codec": "xor" if k == 2 else "rs",
                            "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
                            "bytes_per_checksum": self.bpc}
             self._step = lambda: enc.encode_crc_batch(self.units, stride, n, self.units[:, k:], stride, n, S, n,
                                                       self.crc_type, self.bpc, self.crcs)
-        else:  # e2e: pinned host -> HBM -> fused encode+CRC -> host, chunked over 2 streams
-            self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
-            self.data_bytes = S * k * n
-            self.alg_bytes = S * units * n
-            self.kernel = "encode_crc_g26<6,3> (+H2D/D2H)"
-            self.config = {"workload": "rs-6-3-1024k + CRC32C end-to-end from pinned host buffers", "stripes": S}
-            self.streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-            self._step = self._e2e_step
         torch.cuda.synchronize()
-
-    def _e2e_step(self):
-        k, p, n, S = self.k, self.p, self.n, self.S
-        stride = (k + p) * n
-        chunk = 64
-        for i, s0 in enumerate(range(0, S, chunk)):
-            st = self.streams[i % 2]
-            s1 = min(S, s0 + chunk)
-            with torch.cuda.stream(st):
-                self.units[s0:s1, :k].copy_(self.host_in[s0:s1], non_blocking=True)
-                self.enc.encode_crc_batch(self.units[s0:], stride, n, self.units[s0:, k:], stride, n, s1 - s0, n,
-                                          self.crc_type, self.bpc, self.crcs[s0:], stream=st)
-                self.host_out[s0:s1].copy_(self.units[s0:s1, k:], non_blocking=True)
-                self.host_crc[s0:s1].copy_(self.crcs[s0:s1], non_blocking=True)
-        for st in self.streams:
-            torch.cuda.current_stream().wait_stream(st)
 
     def step(self):
         self._step()
+
+    def free(self):
+        for a in ("units", "blocks", "data", "crcs", "stored", "out", "out_crc", "mism"):
+            if hasattr(self, a):
+                delattr(self, a)
+        torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------------------------------ C5 end to end
+
+
+class HostBatch:
+    """One batch of rs-6-3-1024k stripes in host memory shared by every rank ([stripe][9 units][1 MiB], then a
+    CRC area with one page-aligned slot per rank), so the ranks really split ONE batch.  Each rank places its own
+    stripe range on its GPU's NUMA node and pins it (ozec_host_register).  Falls back to a private mapping of
+    the rank's own range when /dev/shm cannot hold the batch."""
+
+    def __init__(self, S, rank, world, dist, dev, k=6, p=3, n=MIB, bpc=16384):
+        from ozone_amd.shard import stripe_range
+        from ozone_amd.stripe_queue import host_register
+        self.k, self.p, self.n, self.S = k, p, n, S
+        self.units, self.nwin = k + p, -(-n // bpc)
+        self.stripe_bytes = self.units * n
+        self.lo, self.hi = stripe_range(S, rank, world)
+        per = -(-S // world)
+        self.crc_slot = -(-(per * self.units * self.nwin * 4) // (2 * MIB)) * (2 * MIB)
+        total = S * self.stripe_bytes + world * self.crc_slot
+        name = None
+        try:
+            free = os.statvfs("/dev/shm").f_bavail * os.statvfs("/dev/shm").f_frsize
+        except OSError:
+            free = 0
+        self.shared = free > total + (8 << 30)
+        if self.shared:
+            name = f"/dev/shm/ozec_c5_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}" if rank == 0 else None
+            if dist is not None:
+                obj = [name]
+                dist.broadcast_object_list(obj, src=0)
+                name = obj[0]
+            if rank == 0:
+                fd = os.open(name, os.O_CREAT | os.O_RDWR | os.O_TRUNC, 0o600)
+                os.ftruncate(fd, total)
+                os.close(fd)
+            if dist is not None:
+                dist.barrier()
+            fd = os.open(name, os.O_RDWR)
+            self.mm = mmap.mmap(fd, total, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+            os.close(fd)
+            # every rank has it mapped: unlink now, so the memory goes away with the last mapping even if a rank dies
+            if dist is not None:
+                dist.barrier()
+            if rank == 0:
+                os.unlink(name)
+            self.name = name
+            self._anchor = ctypes.c_char.from_buffer(self.mm)
+            self.base = ctypes.addressof(self._anchor)
+            self.data_off = self.lo * self.stripe_bytes
+            self.crc_off = S * self.stripe_bytes + rank * self.crc_slot
+        else:
+            self.name = None
+            own = (self.hi - self.lo) * self.stripe_bytes + self.crc_slot
+            self.mm = mmap.mmap(-1, max(own, mmap.PAGESIZE), mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+            self._anchor = ctypes.c_char.from_buffer(self.mm)
+            self.base = ctypes.addressof(self._anchor)
+            self.data_off = 0
+            self.crc_off = (self.hi - self.lo) * self.stripe_bytes
+        self.rank, self.dev = rank, dev
+        self.data_len = (self.hi - self.lo) * self.stripe_bytes
+        self.registered = []
+        t0 = time.perf_counter()
+        for off, ln in ((self.data_off, self.data_len), (self.crc_off, self.crc_slot)):
+            if ln:
+                host_register(self.base + off, ln, dev)
+                self.registered.append(self.base + off)
+        self.register_s = time.perf_counter() - t0
+
+    def fill(self, enc_dev):
+        """Synthetic data cells (splitmix64, stream = global stripe id * k + unit) generated on the GPU and DMA'd
+        into this rank's range; parity and CRC areas are left for the encode."""
+        from ozone_amd import rawcoder as rc
+        k, n, C = self.k, self.n, 64
+        tmp = torch.zeros((C, self.units, n), dtype=torch.uint8, device=enc_dev)  # parity cells stay zero
+        host = np.frombuffer((ctypes.c_uint8 * self.data_len).from_address(self.base + self.data_off), np.uint8)
+        for s0 in range(self.lo, self.hi, C):
+            c = min(C, self.hi - s0)
+            for i in range(c):  # cell (stripe s, unit u) = splitmix64 stream s * k + u
+                rc.fill_splitmix64_cells(tmp[i], n, k, n, SEED, (s0 + i) * k)
+            v = host[(s0 - self.lo) * self.stripe_bytes:(s0 - self.lo + c) * self.stripe_bytes]
+            torch.from_numpy(v).copy_(tmp[:c].reshape(-1))  # one DMA into the registered range
+        torch.cuda.synchronize()
+        del tmp
+
+    def placement(self):
+        """NUMA node of this rank's first and last data page (after the run)."""
+        from ozone_amd.stripe_queue import page_node
+        if not self.data_len:
+            return []
+        return [page_node(self.base + self.data_off), page_node(self.base + self.data_off + self.data_len - 1)]
+
+    def close(self, dist):
+        from ozone_amd.stripe_queue import host_unregister
+        for a in self.registered:
+            host_unregister(a)
+        self.registered = []
+        del self._anchor
+        try:
+            self.mm.close()
+        except BufferError:  # a numpy view still alive: the mapping goes with the process
+            pass
+        if dist is not None:
+            dist.barrier()
+
+
+def e2e_leg(args, rank, world, dist, dev, backend):
+    """BASELINE configs[4] (C5): rs-6-3-1024k encode + CRC32C of one 8192-stripe batch in pinned host memory,
+    sharded across the GPUs by contiguous stripe ranges, end to end (H2D + fused kernel + D2H)."""
+    from ozone_amd import checksum as ck
+    from ozone_amd import rawcoder as rc
+    from ozone_amd.shard import max_over_ranks
+    S = args.e2e_stripes
+    hb = HostBatch(S, rank, world, dist, dev)
+    try:
+        hb.fill(torch.device("cuda", dev))
+        enc = rc.RawErasureEncoder(rc.ECReplicationConfig(6, 3))
+        n, k, sb = hb.n, hb.k, hb.stripe_bytes
+        mine = hb.hi - hb.lo
+        d0 = hb.base + hb.data_off
+
+        def step():
+            if mine:
+                enc.encode_crc_host_batch(d0, sb, n, d0 + k * n, sb, n, mine, n, ck.ChecksumType.CRC32C, 16384,
+                                          hb.base + hb.crc_off, False, args.chunk)
+
+        step()  # warm-up: device buffers of the pipeline, first-touch of nothing (pages are pinned)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.e2e_steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            dist.barrier()
+        el_max = max_over_ranks(el, dist, device="cuda" if backend == "nccl" else "cpu")
+        # a spot check of the last stripe this rank encoded, against the device coder on the same cells
+        ok = True
+        if mine:
+            last = np.frombuffer((ctypes.c_uint8 * sb).from_address(d0 + (mine - 1) * sb), np.uint8).reshape(9, n)
+            cells = torch.from_numpy(last[:k].copy()).cuda().unsqueeze(0)
+            par = enc.encode_stripes(cells)
+            torch.cuda.synchronize()
+            ok = bool((par[0].cpu().numpy() == last[k:]).all())
+        res = {"workload": "rs-6-3-1024k encode + CRC32C/16 KiB, one batch of %d stripes in shared host memory, "
+                           "contiguous stripe range per GPU, pinned NUMA-local pages, H2D + fused kernel + D2H "
+                           "(BASELINE configs[4])" % S,
+               "value": round(S * k * n * args.e2e_steps / el_max / 1e9, 2), "unit": "GB/s (data bytes)",
+               "ms_per_step": round(el_max / args.e2e_steps * 1e3, 2), "steps": args.e2e_steps,
+               "stripes": S, "stripes_per_gpu": [mine], "shared_batch": hb.shared,
+               "register_s": round(hb.register_s, 2), "parity_spot_check": ok,
+               "numa": {"gpu_node": None, "data_page_nodes": hb.placement()}}
+        from ozone_amd.stripe_queue import device_numa_node
+        res["numa"]["gpu_node"] = device_numa_node(dev)
+        if dist is not None:
+            allr = [None] * world
+            dist.all_gather_object(allr, {"mine": mine, "numa": res["numa"], "ok": ok})
+            res["stripes_per_gpu"] = [a["mine"] for a in allr]
+            res["numa"] = [a["numa"] for a in allr]
+            res["parity_spot_check"] = all(a["ok"] for a in allr)
+        pc = pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
+        res["pcie_per_gpu"] = pc
+        res["frac_of_duplex_h2d_link"] = round(res["value"] / world / pc["duplex_h2d_GBps"], 4)
+        return res
+    finally:
+        hb.close(dist)
 
 
 def pcie_ceiling(h2d_bytes, d2h_bytes, reps=5):
@@ -311,69 +581,161 @@ def pcie_ceiling(h2d_bytes, d2h_bytes, reps=5):
     return {"h2d_GBps": round(reps * h2d_bytes / t_h2d / 1e9, 2), "d2h_GBps": round(reps * d2h_bytes / t_d2h / 1e9, 2),
             "duplex_h2d_GBps": round(reps * h2d_bytes / t_both / 1e9, 2),
             "duplex_d2h_GBps": round(reps * d2h_bytes / t_both / 1e9, 2),
-            "bytes": {"h2d": h2d_bytes, "d2h": d2h_bytes},
             "note": "contiguous pinned DMA copies of the same volumes, one H2D and one D2H stream"}
 
 
 # ------------------------------------------------------------------------------------------ CPU baseline
 
+_CPU_BASELINE_BIN = None
+
+
+def _cpu_baseline_bin():
+    """oracle/cpu_baseline.c + oracle/ozec_oracle.c built for THIS host (-march=native), falling back to the
+    portable build from build()."""
+    global _CPU_BASELINE_BIN
+    if _CPU_BASELINE_BIN:
+        return _CPU_BASELINE_BIN
+    odir = os.path.join(ROOT, "oracle")
+    out = os.path.join(tempfile.mkdtemp(prefix="ozec_cpub_"), "cpu_baseline")
+    cmd = ["gcc", "-O3", "-march=native", "-std=gnu11", "-o", out, os.path.join(odir, "cpu_baseline.c"),
+           os.path.join(odir, "ozec_oracle.c"), "-lz", "-lpthread"]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=120)
+        _CPU_BASELINE_BIN = (out, "gcc -O3 -march=native")
+    except (OSError, subprocess.SubprocessError):
+        _CPU_BASELINE_BIN = (os.path.join(odir, "cpu_baseline"), "gcc -O3 -march=x86-64-v3 (prebuilt)")
+    return _CPU_BASELINE_BIN
+
+
+CPU_WHAT = {
+    "c1": "rs-3-2-1024k stripes encoded (RSUtil.encodeData table loop, oracle restatement)",
+    "c2": "rs-6-3-1024k stripes encoded (RSUtil.encodeData table loop, oracle restatement)",
+    "c3": "rs-10-4-1024k stripes decoded, 4 erased (RSRawDecoder + RSUtil.encodeData)",
+    "c3r": "rs-10-4-1024k reconstructions: CRC32C verify of 10 units + decode 4 + CRC32C of the 4 rebuilt",
+    "c4": "xor-2-1-1024k stripes coded + CRC32C/16 KiB of all 3 units",
+    "c5": "rs-6-3-1024k stripes encoded + CRC32C/16 KiB of all 9 units",
+    "crc": "1 MiB cells checksummed as CRC32C/16 KiB windows (SSE4.2 crc32, 3 streams: the JDK CRC32C intrinsic)",
+    "verify": "1 MiB cells verified against stored CRC32C/16 KiB windows (SSE4.2 crc32)",
+}
+
 
 def cpu_baseline(workload, budget_s):
-    """oracle/ (C restatement of the reference path, gcc -O3) timed on this host's cores on a bounded sample of
-    the workload: T threads share one coder (RawErasureCoderBenchmark.java:201-206), each repeating one unit of
-    work (a stripe, a decode, a cell's windows) until the wall budget is spent."""
+    """The reference's CPU path timed on this host's cores (RawErasureCoderBenchmark.java:182-236 definitions:
+    threads share one coder, data bytes counted): T = every CPU this process may use, and 1 thread."""
+    wl = {"c4s": "c4", "c5dev": "c5", "host": "c2", "queue": "c5", "queue_pageable": "c5", "stream": "c2"}.get(
+        workload, workload)
+    exe, flags = _cpu_baseline_bin()
+    T = usable_cpus()
+    res = {}
+    for t in (T, 1):
+        out = subprocess.run([exe, wl, str(t), str(budget_s)], capture_output=True, text=True, timeout=budget_s + 120)
+        if out.returncode != 0:
+            raise RuntimeError(f"cpu_baseline {wl} failed: {out.stderr.strip()}")
+        res[t] = json.loads(out.stdout)
+    hi, one = res[T], res[1]
+    info = host_info()
+    return {"value": round(hi["GBps"], 3), "unit": "GB/s", "cores": T, "kind": "port",
+            "value_1_thread": round(one["GBps"], 3),
+            "sample": f"{hi['units']} {CPU_WHAT[wl]} in {hi['seconds']:.1f} s on {T} threads sharing one coder "
+                      f"({one['units']} in {one['seconds']:.1f} s on 1 thread); oracle/cpu_baseline.c, {flags}",
+            "host": info}
+
+
+# ------------------------------------------------------------------------------------------ live PMC traffic
+
+KERNEL_PAT = {"c1": "gf_code_vec<3, 2", "c2": "gf_code_vec<6, 3", "c3": "gf_code_vec<10, 4",
+              "c3r": "encode_crc_g26<10, 4", "c4": "encode_crc_g26<2, 1", "c4s": "encode_crc_g26<2, 1",
+              "c5dev": "encode_crc_g26<6, 3", "crc": "crc_windows_g26s", "verify": "crc_windows_g26s"}
+
+
+def pmc_traffic(args, alg_bytes):
+    """HBM bytes per launch of the workload's dominant kernel, measured now: the same bench command as a CHILD
+    process under rocprofv3, one --pmc pass per counter (FETCH_SIZE, WRITE_SIZE: they do not fit one pass), plus
+    a --kernel-trace --stats pass for the rocprof average duration.  gfx950: FETCH_SIZE reports half of wide
+    streaming reads (MI355X_MICROARCH.md, HBM) -> bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB * 1024."""
+    import csv
+    pat = KERNEL_PAT.get(args.workload)
+    prof = shutil.which("rocprofv3")
+    if not pat or not prof:
+        return None, {"error": "no kernel pattern / rocprofv3 for this workload"}
+    base = [sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--steps", "3", "--warmup", "1",
+            "--no-cpu", "--no-e2e", "--no-pmc"] + (["--stripes", str(args.stripes)] if args.stripes else [])
+    for kv in args.tune:
+        base += ["--tune", kv]
+    out = {}
+    work = tempfile.mkdtemp(prefix="ozec_pmc_")
+    env = dict(os.environ, TMPDIR="/tmp")
+    env.pop("WORLD_SIZE", None)
+    try:
+        for tag, opts in (("FETCH_SIZE", ["--pmc", "FETCH_SIZE"]), ("WRITE_SIZE", ["--pmc", "WRITE_SIZE"]),
+                          ("stats", [])):
+            d = os.path.join(work, tag)
+            cmd = [prof] + opts + ["--kernel-trace", "--stats", "-d", d, "-o", "run", "--output-format", "csv",
+                                   "--"] + base
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd="/tmp", env=env)
+            if r.returncode != 0:
+                return None, {"error": f"rocprofv3 {tag} pass rc={r.returncode}: {r.stderr.strip()[-300:]}"}
+            files = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs]
+            if tag == "stats":
+                st = [f for f in files if f.endswith("kernel_stats.csv")]
+                rows = [row for row in csv.DictReader(open(st[0])) if pat in row["Name"]]
+                out["rocprof_kernel"] = rows[0]["Name"]
+                out["rocprof_avg_ms"] = round(float(rows[0]["AverageNs"]) / 1e6, 4)
+                out["rocprof_calls"] = int(rows[0]["Calls"])
+            else:
+                cc = [f for f in files if f.endswith("counter_collection.csv")]
+                vals = [float(row["Counter_Value"]) for row in csv.DictReader(open(cc[0]))
+                        if pat in row["Kernel_Name"] and row["Counter_Name"] == tag]
+                if not vals:
+                    return None, {"error": f"no {tag} rows for kernel {pat}"}
+                out[tag + "_KiB"] = sum(vals) / len(vals)
+                out[tag + "_dispatches"] = len(vals)
+    except (OSError, subprocess.SubprocessError, IndexError, KeyError, ValueError) as e:
+        return None, {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+    hbm = int(round((2 * out["FETCH_SIZE_KiB"] + out["WRITE_SIZE_KiB"]) * 1024))
+    out["hbm_bytes_per_launch"] = hbm
+    out["traffic_over_algorithmic"] = round(hbm / alg_bytes, 5)
+    out["correction"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB (gfx950 FETCH_SIZE counts half of wide reads)"
+    return hbm, out
+
+
+# ------------------------------------------------------------------------------------------ per-call latency
+
+
+def stream_latency(args):
+    """In-situ per-call cost of the drop-in entry points (one call = what one Java call does): ozec_encode of one
+    rs-6-3-1024k stripe (RawErasureEncoder.encode, ECKeyOutputStream.java:304) from 1 thread, and
+    ozec_crc_update (ChecksumByteBuffer.update, Checksum.java:157-200) at 1 B / 512 B / 16 KiB, each against the
+    CPU doing the same call."""
+    from ozone_amd import _lib
+    from ozone_amd import rawcoder as rc
     import oracle
-    from synth import cells
-    threads = min(16, os.cpu_count() or 1)
-    n = MIB
-    if workload == "c3":
-        k, p, erased = 10, 4, [0, 1, 2, 3]
-        d = cells(SEED, 900, k, n)
-        units = d + oracle.rs_encode(k, p, d)
-        ins = [None if u in erased else units[u] for u in range(k + p)]
-        job, data_bytes = (lambda: oracle.rs_decode(k, p, ins, erased)), k * n
-        what = "rs-10-4-1024k decodes of 4 erased units (oracle rs_decode: RSRawDecoder + RSUtil.encodeData)"
-    elif workload in ("crc", "verify"):
-        cell = cells(SEED, 900, 1, n)[0]
-        job, data_bytes = (lambda: oracle.crc_windows(oracle.CRC32C, cell, 16384)), n
-        what = "1 MiB cells checksummed as CRC32C/16 KiB windows (oracle crc_windows: CrcIntTable slice-by-8)"
-    elif workload in ("c4", "c5", "c3r"):
-        k, p = (2, 1) if workload == "c4" else (10, 4) if workload == "c3r" else (6, 3)
-        d = cells(SEED, 900, k, n)
+    n, k, p = MIB, 6, 3
+    rng = np.random.default_rng(1)
+    d = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    o = [np.empty(n, np.uint8) for _ in range(p)]
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    L = _lib.lib()
 
-        def job():
-            par = oracle.rs_encode(k, p, d) if workload != "c4" else [oracle.xor_encode(d)]
-            for u in d + par:
-                oracle.crc_windows(oracle.CRC32C, u, 16384)
-        data_bytes = k * n
-        what = {"c4": "xor-2-1-1024k stripes coded + CRC32C/16 KiB of all 3 units",
-                "c5": "rs-6-3-1024k stripes coded + CRC32C/16 KiB of all 9 units",
-                "c3r": "rs-10-4-1024k stripes, 10 units -> 4 rebuilt + CRC32C/16 KiB of all 14 units (the "
-                       "reconstruction's work)"}[workload] + " (oracle coder + crc_windows)"
-    else:
-        k, p = (3, 2) if workload == "c1" else (6, 3)
-        d = cells(SEED, 900, k, n)
-        job, data_bytes = (lambda: oracle.rs_encode(k, p, d)), k * n
-        what = f"rs-{k}-{p}-1024k stripes encoded (oracle rs_encode: C restatement of RSUtil.encodeData)"
-    job()  # warm the tables
-    done = [0] * threads
-    stop = time.perf_counter() + budget_s
+    def per_call(fn, reps):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return (time.perf_counter() - t0) / reps * 1e6
 
-    def worker(i):
-        while time.perf_counter() < stop:
-            job()
-            done[i] += 1
-
-    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
-    t0 = time.perf_counter()
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    el = time.perf_counter() - t0
-    units = sum(done)
-    return {"value": round(units * data_bytes / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"{units} {what}, {threads} threads sharing one coder, {el:.1f} s wall (gcc -O3)"}
+    out = {"encode_stripe_us": round(per_call(lambda: enc.encode(d, o), 50), 1)}
+    out["encode_stripe_cpu_us"] = round(per_call(lambda: oracle.rs_encode(k, p, d), 10), 1)
+    st = ctypes.c_uint32(0xFFFFFFFF)
+    buf = rng.integers(0, 256, 16384, dtype=np.uint8)
+    for nb in (1, 512, 16384):
+        out[f"crc_update_{nb}B_us"] = round(per_call(lambda: L.ozec_crc_update(3, ctypes.byref(st), buf.ctypes.data, nb),
+                                                     200), 2)
+        out[f"crc_update_{nb}B_cpu_us"] = round(per_call(lambda: oracle.crc_windows(oracle.CRC32C, buf[:nb], 16384),
+                                                         200), 2)
+    return out
 
 
 # ------------------------------------------------------------------------------------------ main
@@ -381,6 +743,8 @@ def cpu_baseline(workload, budget_s):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_workers(args)
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -388,6 +752,7 @@ def main():
     # OZEC_BENCH_SAME_DEVICE=1 + OZEC_DIST_BACKEND=gloo rehearse the N-rank path on a one-GPU box
     dev_idx = 0 if os.environ.get("OZEC_BENCH_SAME_DEVICE") == "1" else local
     torch.cuda.set_device(dev_idx)
+    numa_node = bind_process_to_gpu_node(dev_idx)
     backend = os.environ.get("OZEC_DIST_BACKEND", "nccl")
     dist = None
     if world > 1:
@@ -405,7 +770,43 @@ def main():
     erased = [int(e) for e in args.erased.split(",")]
     if len(erased) != 4 or len(set(erased)) != 4 or not all(0 <= e < 14 for e in erased):
         raise SystemExit("--erased: four distinct unit indexes of rs-10-4 (0..13)")
-    wl = Workload(args.workload, rank, args.stripes, args.threads, erased)
+    from ozone_amd.shard import max_over_ranks
+    red_dev = "cuda" if backend == "nccl" else "cpu"
+    pci = torch.cuda.get_device_properties(dev_idx)
+    dev_id = (f"{getattr(pci, 'pci_domain_id', '')}:{getattr(pci, 'pci_bus_id', '')}:{getattr(pci, 'pci_device_id', '')}"
+              f":{getattr(pci, 'uuid', '')}")
+    devices = [dev_id]
+    if dist is not None:
+        devices = [None] * world
+        dist.all_gather_object(devices, dev_id)
+    n_gpus = len(set(devices))
+
+    if args.workload == "c5":
+        res = e2e_leg(args, rank, world, dist, dev_idx, backend)
+        result = {"metric": "C5 e2e: rs-6-3-1024k encode + CRC32C GB/s (data bytes) from pinned host memory",
+                  "value": res["value"], "unit": "GB/s", "n_gpus": n_gpus, "n_ranks": world,
+                  "steps": args.e2e_steps, "warmup": 1, "ms_per_step": res["ms_per_step"], "higher_is_better": True,
+                  "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+                  "data": "synthetic (splitmix64 bytes generated on the GPU, copied into the host batch)",
+                  "config": {"workload": res["workload"], "stripes": args.e2e_stripes,
+                             "parallelism": f"stripe-range sharded x{world} (one shared batch, no collective)"},
+                  "e2e": res}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline("c5", args.cpu_seconds)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return 0
+
+    if args.workload == "stream":
+        if rank == 0:
+            print(json.dumps({"metric": "per-call latency of the drop-in entry points (us)", "value": None,
+                              "n_gpus": n_gpus, "dtype": "u8", "config": {"workload": "stream"},
+                              "calls": stream_latency(args)}), flush=True)
+        return 0
+
+    wl = Workload(args.workload, rank, world, args.stripes, args.threads, erased)
 
     def barrier():
         if dist is not None:
@@ -415,30 +816,27 @@ def main():
     for _ in range(args.warmup):
         wl.step()
     barrier()
+    st = torch.cuda.current_stream()  # every device-resident workload launches on it (rawcoder._stream_ptr)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for a, b in ev:
-        a.record()
+        a.record(st)
         wl.step()
-        b.record()
+        b.record(st)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    from ozone_amd.shard import max_over_ranks
-    elapsed = max_over_ranks(elapsed, dist, device="cuda" if backend == "nccl" else "cpu")
+    elapsed = max_over_ranks(elapsed, dist, device=red_dev)
+    kern_ms = max_over_ranks(kern_ms, dist, device=red_dev)
     value = wl.data_bytes * world * args.steps / elapsed / 1e9
     achieved = wl.alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
-    if os.path.exists(tf):
-        with open(tf) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
     result = {
         "metric": METRIC if args.workload == "c2" else f"{args.workload}: data GB/s",
         "value": round(value, 2),
         "unit": "GB/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
+        "n_ranks": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -447,26 +845,46 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 bytes generated in HBM)",
-        "config": dict(wl.config, parallelism=f"stripe-sharded x{world} (independent stripes, no collective)"),
+        "config": dict(wl.config, global_stripes=wl.S * world,
+                       parallelism=f"stripe-range sharded x{world}: rank r encodes stripes [r*{wl.S}, (r+1)*{wl.S}) "
+                                   f"of one global batch on its own GPU (no collective)"),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                     "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4),
-                     "alg_bytes_per_launch": wl.alg_bytes},
+                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                     "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4), "kernel_ms_reduction": "max over ranks",
+                     "alg_bytes_per_launch": wl.alg_bytes, "numa_node": numa_node},
     }
-    if args.workload in ("e2e", "queue", "queue_pageable"):
-        # the kernel is not the bound here: report the PCIe ceiling beside the value (never the value itself)
-        pc = pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
-        pc["value_frac_of_duplex_h2d"] = round(value / world / pc["duplex_h2d_GBps"], 4)
-        result["pcie"] = pc
-        result["roofline"]["note"] = ("e2e: kernel_ms is the whole PCIe-inclusive step; the bound is the link "
-                                      "(see pcie), not HBM")
-    if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
+    if args.workload in ("host", "queue", "queue_pageable", "c4"):
+        if args.workload == "c4":
+            result["roofline"]["note"] = "one step = 16 launches (one per block group): kernel_ms covers all 16"
+            result["roofline"]["alg_bytes_per_launch"] = wl.alg_bytes // 16
+            result["roofline"]["launches_per_step"] = 16
+        else:
+            pc = pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
+            pc["value_frac_of_duplex_h2d"] = round(value / world / pc["duplex_h2d_GBps"], 4)
+            result["pcie"] = pc
+            result["roofline"]["note"] = "kernel_ms is the whole PCIe-inclusive step; the bound is the link, not HBM"
+    wl.free()
+    del wl
+    if args.workload == "c2" and not args.no_e2e:
+        try:
+            result["e2e"] = e2e_leg(args, rank, world, dist, dev_idx, backend)
+        except Exception as e:  # the device-resident line stands on its own
+            result["e2e"] = {"error": f"{type(e).__name__}: {e}"}
+    if rank == 0 and world == 1:
+        if not args.no_pmc and args.workload in KERNEL_PAT:
+            traffic, detail = pmc_traffic(args, result["roofline"]["alg_bytes_per_launch"])
+            result["roofline"]["traffic"] = traffic
+            result["roofline"]["pmc"] = detail
+        if not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
+            if "e2e" in result and "value" in result["e2e"]:
+                result["e2e"]["cpu_baseline"] = cpu_baseline("c5", args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -122,6 +122,18 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
                           int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
                           size_t bytes_per_checksum, uint32_t *d_crcs, int big_endian, void *stream);
 
+/* End-to-end fused encode (+ CRC) of stripes held in HOST memory (BASELINE configs[4] / SURVEY §8(d) C5: the
+ * stripe batch a writer or datanode holds, one contiguous stripe range per GPU, §8(e)).  Same layouts and
+ * semantics as ozec_encode_crc_batch with host pointers; checksum_type OZEC_CHECKSUM_NONE encodes only (h_crcs
+ * may then be NULL).  Chunks of stripes_per_chunk stripes (0 = 16) are pipelined on the calling thread's device:
+ * the H2D copies of chunk c+1, the kernel of chunk c and the D2H copies of chunk c-1 run at once on three streams.
+ * Registered / pinned buffers (ozec_host_register, ozec_host_alloc) are DMA'd in place; pageable ones are staged
+ * through NUMA-local pinned memory.  Synchronous: returns when parity and CRCs are in the caller's buffers. */
+int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_stripe_stride,
+                               int64_t in_unit_stride, uint8_t *h_out, int64_t out_stripe_stride,
+                               int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
+                               size_t bytes_per_checksum, uint32_t *h_crcs, int big_endian, size_t stripes_per_chunk);
+
 /* ---- chunk checksums: Checksum.computeChecksum(ByteBuffer / ChunkBuffer) (CM/Checksum.java:132-200) with
  *      ChunkBufferImplWithByteBuffer.iterate(bytesPerChecksum) (CM/ChunkBufferImplWithByteBuffer.java:78-98)
  *      and ChecksumByteBufferImpl/CrcIntTable per window (CM/ChecksumByteBuffer.java:51-121).
@@ -193,9 +205,20 @@ uint32_t ozec_crc_combine(int checksum_type, uint32_t crc_a, uint32_t crc_b, uin
  * DMA'd straight from / into the caller's buffers when those are pinned (ozec_host_alloc, or any pinned host
  * memory), else through pinned staging.  The buffers given to submit must stay valid and unmodified until wait()
  * has returned for that ticket (or until ozec_stripe_queue_free). */
-/* pinned host memory for cell buffers (the JNI side wraps it with NewDirectByteBuffer) */
+/* pinned host memory for cell buffers (the JNI side wraps it with NewDirectByteBuffer).  Its pages are placed on
+ * the host NUMA node closest to the GPU (ozec_host_alloc: the calling thread's current device), so DMA never
+ * crosses the inter-socket fabric; every staging buffer libozec allocates itself is placed the same way. */
 int ozec_host_alloc(size_t bytes, void **out);
+int ozec_host_alloc_on(size_t bytes, int device, void **out);
 int ozec_host_free(void *p);
+/* host NUMA node closest to `device` (-1: unknown / not a NUMA host) */
+int ozec_device_numa_node(int device, int *node);
+/* NUMA node holding the (touched) page at p, -1 if unknown -- placement diagnostics */
+int ozec_host_page_node(const void *p, int *node);
+/* pin caller-owned memory for DMA (e.g. one rank's stripe range of a batch shared between processes), placing
+ * its pages on `device`'s NUMA node first (device < 0: no placement); ozec_host_unregister undoes the pinning */
+int ozec_host_register(void *p, size_t bytes, int device);
+int ozec_host_unregister(void *p);
 typedef struct ozec_stripe_queue ozec_stripe_queue;
 /* checksum_type OZEC_CHECKSUM_NONE: parity only; CRC32 / CRC32C: also the bpc-window CRCs of all k+p units,
  * written per stripe as crcs[unit][window] (window count from the stripe's length), big-endian if asked */
@@ -209,7 +232,10 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
 int ozec_stripe_queue_flush(ozec_stripe_queue *q);
 /* block until every stripe up to and including `ticket` has its parity (and CRCs) in the caller's buffers */
 int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket);
-/* drain and destroy */
+/* introspection: batches in flight, first ticket of the oldest one (UINT64_MAX if none), stripes in filling batches */
+int ozec_stripe_queue_state(ozec_stripe_queue *q, size_t *in_flight, uint64_t *oldest_in_flight_ticket,
+                            size_t *filling);
+/* complete every stripe not yet waited for (its parity / CRCs land in the caller's buffers), then destroy */
 int ozec_stripe_queue_free(ozec_stripe_queue *q);
 
 /* ---- COMPOSITE_CRC: CrcUtil / CrcComposer ------------------------------------------

@@ -93,7 +93,16 @@ _SIGS = {
     "ozec_parse_replication": (ctypes.c_int, [ctypes.c_char_p, c_intp, c_intp, c_intp, c_intp]),
     "ozec_crc_combine": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
     "ozec_host_alloc": (ctypes.c_int, [c_size, ctypes.POINTER(c_voidp)]),
+    "ozec_host_alloc_on": (ctypes.c_int, [c_size, ctypes.c_int, ctypes.POINTER(c_voidp)]),
     "ozec_host_free": (ctypes.c_int, [c_voidp]),
+    "ozec_device_numa_node": (ctypes.c_int, [ctypes.c_int, c_intp]),
+    "ozec_host_page_node": (ctypes.c_int, [c_voidp, c_intp]),
+    "ozec_host_register": (ctypes.c_int, [c_voidp, c_size, ctypes.c_int]),
+    "ozec_host_unregister": (ctypes.c_int, [c_voidp]),
+    "ozec_encode_crc_host_batch": (ctypes.c_int, [c_voidp, c_voidp, c_i64, c_i64, c_voidp, c_i64, c_i64, c_size,
+                                                  c_size, ctypes.c_int, c_size, c_voidp, ctypes.c_int, c_size]),
+    "ozec_stripe_queue_state": (ctypes.c_int, [c_voidp, ctypes.POINTER(c_size), ctypes.POINTER(ctypes.c_uint64),
+                                               ctypes.POINTER(c_size)]),
     "ozec_stripe_queue_create": (ctypes.c_int, [c_voidp, c_size, c_size, ctypes.c_int, c_size, ctypes.c_int,
                                                 ctypes.POINTER(c_voidp)]),
     "ozec_stripe_queue_submit": (ctypes.c_int, [c_voidp, c_ptrs, c_ptrs, c_size, c_voidp,

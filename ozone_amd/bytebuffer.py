@@ -35,7 +35,10 @@ class ByteBuffer:
         if isinstance(array, (bytes, bytearray, memoryview)):
             array = np.frombuffer(bytearray(array), np.uint8)
         array = np.asarray(array)
-        assert array.dtype == np.uint8 and array.ndim == 1
+        # a Java byte[] is one contiguous run of bytes: the GPU path DMA's address() as such, so a strided view
+        # or a wider dtype would read (and, as an output, write) the wrong memory
+        if array.dtype != np.uint8 or array.ndim != 1 or not array.flags.c_contiguous:
+            raise TypeError("ByteBuffer.wrap needs a 1-D C-contiguous uint8 array")
         n = array.size if length is None else length
         return ByteBuffer(array, 0, array.size, False, position=offset, limit=offset + n)
 

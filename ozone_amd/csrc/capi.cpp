@@ -21,6 +21,7 @@
 #include "gf256.hpp"
 #include "copy_pool.hpp"
 #include "kernels.hpp"
+#include "numa.hpp"
 #include "status.hpp"
 
 namespace {
@@ -51,8 +52,9 @@ int fail(int code, const std::string &msg) {
 // drop-in path) take a slot from the pool for the duration of the call, so calls from different threads
 // overlap on the GPU and on the copy engines instead of serialising on one buffer.
 struct Slot {
+  int device = 0;
   hipStream_t stream = nullptr;
-  uint8_t *pinned = nullptr;
+  uint8_t *pinned = nullptr;  // on the device's NUMA node (numa.hpp)
   size_t pinned_cap = 0;
   uint8_t *dbuf = nullptr;
   size_t dbuf_cap = 0;
@@ -60,11 +62,12 @@ struct Slot {
 
   int reserve(size_t bytes, size_t nevents) {
     if (bytes > pinned_cap) {
-      if (pinned) (void)hipHostFree(pinned);
+      if (pinned) (void)ozec::pinned_free(pinned);
       pinned = nullptr;
       pinned_cap = 0;
       size_t cap = std::max<size_t>(bytes, 1 << 20);
-      OZEC_HIP(hipHostMalloc(reinterpret_cast<void **>(&pinned), cap, hipHostMallocDefault));
+      if (ozec::pinned_alloc(cap, device, reinterpret_cast<void **>(&pinned)) != 0)
+        return fail(OZEC_ENOMEM, "cannot pin " + std::to_string(cap) + " bytes of staging memory");
       pinned_cap = cap;
     }
     if (bytes > dbuf_cap) {
@@ -84,8 +87,24 @@ struct Slot {
   }
 };
 
+// End-to-end pipeline of ozec_encode_crc_host_batch: a ring of NB device chunk buffers; the chunk's H2D copies,
+// its kernel and its D2H copies go on three streams ordered by events, so the two copy directions and the
+// kernel of consecutive chunks run at once.  One call at a time per device (mu).
+struct E2E {
+  static constexpr int NB = 3;
+  std::mutex mu;
+  hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+  hipEvent_t h2d_done[NB] = {}, comp_done[NB] = {}, d2h_done[NB] = {};
+  uint8_t *dbuf[NB] = {};
+  size_t dcap = 0;
+  uint8_t *hstage[NB] = {};  // pinned staging, only for pageable caller buffers
+  size_t hcap = 0;
+};
+
 struct DevCtx {
   int device = -1;
+  int numa = -1;  // host NUMA node closest to the device
+  E2E e2e;
   std::mutex pool_mu;  // guards the slot pool
   std::condition_variable pool_cv;
   std::vector<std::unique_ptr<Slot>> slots;
@@ -99,6 +118,7 @@ struct DevCtx {
     pool_cv.wait(lk, [&] { return !free_slots.empty() || slots.size() < max_slots; });
     if (free_slots.empty()) {
       auto s = std::make_unique<Slot>();
+      s->device = device;
       OZEC_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
       free_slots.push_back(s.get());
       slots.push_back(std::move(s));
@@ -140,6 +160,13 @@ int get_ctx(DevCtx **out) {
   if (!g_ctx[dev]) {
     auto c = std::make_unique<DevCtx>();
     c->device = dev;
+    c->numa = ozec::device_numa_node(dev);
+    // staging copies run where the first GPU's staging memory lives (one process per GPU is the multi-GPU model)
+    static bool copy_node_set = false;
+    if (!copy_node_set) {
+      ozec::set_copy_node(c->numa);
+      copy_node_set = true;
+    }
     for (int t = 0; t < 2; ++t)
       for (int b = 0; b < 3; ++b) {
         const auto &blob = CrcMath::get(static_cast<CrcType>(t)).device_tables(1 << b);
@@ -294,6 +321,13 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
   SlotLease lease(ctx);
   if (int rc = ctx->acquire(&lease.slot)) return rc;
   Slot *s = lease.slot;
+  // On an early error return, chunks already queued may still be copying into / out of the slot's buffers:
+  // drain the slot's stream before the lease hands the slot to the next caller (declared after the lease, so
+  // it runs first).
+  struct DrainOnExit {
+    hipStream_t st;
+    ~DrainOnExit() { (void)hipStreamSynchronize(st); }
+  } drain{s->stream};
   if (int rc = s->reserve(per_chunk * nch, nch)) return rc;
   auto unstage = [&](size_t c) -> int {
     OZEC_HIP(hipEventSynchronize(s->events[c]));
@@ -751,18 +785,208 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
     return rc;
   if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
+  } else {
+    // unfused: encode, then one CRC pass per unit (crcs[s][u][w] layout kept)
+    OZEC_HIP(ozec::launch_code(a, st));
+    for (int u = 0; u < units; ++u) {
+      CrcArgs c = e.crc;
+      c.base = u < k ? d_in + u * in_unit_stride : d_out + (u - k) * out_unit_stride;
+      c.cell_stride = u < k ? in_stripe_stride : out_stripe_stride;
+      c.out = d_crcs + u * nwin;
+      c.out_cell_stride = units * nwin;
+      OZEC_HIP(ozec::launch_crc_windows(c, st));
+    }
+  }
+  // XOR with p > 1: every output is reset, only outputs[0] is coded (XORRawEncoder.java:67-85), as in
+  // ozec_encode_batch; CRCs cover the coded units only
+  for (int r = rows; r < enc->p; ++r)
+    OZEC_HIP(hipMemset2DAsync(d_out + r * out_unit_stride, out_stripe_stride, 0, len, num_stripes, st));
+  return OZEC_OK;
+}
+
+// ---- end-to-end batch from host memory ----------------------------------------
+
+namespace {
+
+bool host_pinned(const void *p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+// the whole [p, p+n) must be registered / pinned: check its two ends
+bool range_pinned(const void *p, size_t n) {
+  return n == 0 || (host_pinned(p) && host_pinned(static_cast<const uint8_t *>(p) + n - 1));
+}
+
+}  // namespace
+
+int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_stripe_stride,
+                               int64_t in_unit_stride, uint8_t *h_out, int64_t out_stripe_stride,
+                               int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
+                               size_t bpc, uint32_t *h_crcs, int big_endian, size_t stripes_per_chunk) {
+  if (int rc = check_open(enc, "encode")) return rc;
+  if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
+  if (len == 0 || num_stripes == 0) return OZEC_OK;
+  const bool with_crc = checksum_type != OZEC_CHECKSUM_NONE;
+  if (!h_in || !h_out || (with_crc && !h_crcs)) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  if (with_crc) {
+    CrcType t;
+    if (int rc = crc_type_of(checksum_type, &t)) return rc;
+    if (bpc == 0) return fail(OZEC_EINVAL, "bytesPerChecksum must be positive");
+  }
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  E2E &P = ctx->e2e;
+  std::lock_guard<std::mutex> lk(P.mu);
+  const int k = enc->k, p = enc->p, rows = out_rows(enc), units = k + rows;
+  const size_t C = std::min(num_stripes, stripes_per_chunk ? stripes_per_chunk : size_t{16});
+  const size_t nwin = with_crc ? (len + bpc - 1) / bpc : 0;
+  const size_t dstripe = static_cast<size_t>(k + p) * len;               // device layout [C][k+p][len]
+  const size_t dcrc_off = round_up(C * dstripe, kStageAlign);            // then crcs [C][units][nwin]
+  const size_t dbytes = dcrc_off + C * units * nwin * sizeof(uint32_t);
+  const size_t ncrc = units * nwin;                                      // CRCs per stripe
+  // which caller buffers need staging (pageable); the C5 batch is registered, so normally none
+  const size_t in_span = (num_stripes - 1) * static_cast<size_t>(in_stripe_stride) +
+                         (k - 1) * static_cast<size_t>(in_unit_stride) + len;
+  const size_t out_span = (num_stripes - 1) * static_cast<size_t>(out_stripe_stride) +
+                          (p - 1) * static_cast<size_t>(out_unit_stride) + len;
+  const bool in_pinned = range_pinned(h_in, in_span);
+  const bool out_pinned = range_pinned(h_out, out_span);
+  const bool crc_pinned = !with_crc || range_pinned(h_crcs, num_stripes * ncrc * sizeof(uint32_t));
+  const bool staged = !in_pinned || !out_pinned || !crc_pinned;
+  if (!P.h2d) {
+    OZEC_HIP(hipStreamCreateWithFlags(&P.h2d, hipStreamNonBlocking));
+    OZEC_HIP(hipStreamCreateWithFlags(&P.comp, hipStreamNonBlocking));
+    OZEC_HIP(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
+    for (int b = 0; b < E2E::NB; ++b) {
+      OZEC_HIP(hipEventCreateWithFlags(&P.h2d_done[b], hipEventDisableTiming));
+      OZEC_HIP(hipEventCreateWithFlags(&P.comp_done[b], hipEventDisableTiming));
+      OZEC_HIP(hipEventCreateWithFlags(&P.d2h_done[b], hipEventDisableTiming));
+    }
+  }
+  // drain all three streams on every exit, so no copy of this call outlives it (error paths included)
+  struct DrainOnExit {
+    E2E &P;
+    ~DrainOnExit() {
+      (void)hipStreamSynchronize(P.h2d);
+      (void)hipStreamSynchronize(P.comp);
+      (void)hipStreamSynchronize(P.d2h);
+    }
+  } drain{P};
+  if (dbytes > P.dcap) {
+    for (auto &d : P.dbuf) {
+      if (d) (void)hipFree(d);
+      d = nullptr;
+    }
+    P.dcap = 0;
+    for (auto &d : P.dbuf) OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&d), dbytes));
+    P.dcap = dbytes;
+  }
+  if (staged && dbytes > P.hcap) {
+    for (auto &h : P.hstage) {
+      if (h) (void)ozec::pinned_free(h);
+      h = nullptr;
+    }
+    P.hcap = 0;
+    for (auto &h : P.hstage)
+      if (ozec::pinned_alloc(dbytes, ctx->device, reinterpret_cast<void **>(&h)) != 0)
+        return fail(OZEC_ENOMEM, "cannot pin " + std::to_string(dbytes) + " bytes of staging memory");
+    P.hcap = dbytes;
+  }
+  const size_t nch = (num_stripes + C - 1) / C;
+  // host side of chunk c: copy parity / CRCs of a finished, staged chunk to the caller
+  auto unstage = [&](size_t c) -> int {
+    const int b = static_cast<int>(c % E2E::NB);
+    OZEC_HIP(hipEventSynchronize(P.d2h_done[b]));
+    const size_t s0 = c * C, cs = std::min(C, num_stripes - s0);
+    std::vector<ozec::CopyTask> tasks;
+    if (!out_pinned)
+      for (size_t i = 0; i < cs; ++i)
+        for (int r = 0; r < p; ++r)
+          tasks.push_back({h_out + (s0 + i) * out_stripe_stride + r * out_unit_stride,
+                           P.hstage[b] + i * dstripe + static_cast<size_t>(k + r) * len, len});
+    if (with_crc && !crc_pinned)
+      tasks.push_back({h_crcs + s0 * ncrc, P.hstage[b] + dcrc_off, cs * ncrc * sizeof(uint32_t)});
+    ozec::parallel_copy(tasks);
     return OZEC_OK;
+  };
+  for (size_t c = 0; c < nch; ++c) {
+    const int b = static_cast<int>(c % E2E::NB);
+    const size_t s0 = c * C, cs = std::min(C, num_stripes - s0);
+    uint8_t *d = P.dbuf[b];
+    if (staged) {
+      if (c >= static_cast<size_t>(E2E::NB))
+        if (int rc = unstage(c - E2E::NB)) return rc;  // frees hstage[b] for this chunk
+      if (!in_pinned) {
+        std::vector<ozec::CopyTask> tasks;
+        for (size_t i = 0; i < cs; ++i)
+          for (int j = 0; j < k; ++j)
+            tasks.push_back({P.hstage[b] + i * dstripe + static_cast<size_t>(j) * len,
+                             h_in + (s0 + i) * in_stripe_stride + j * in_unit_stride, len});
+        ozec::parallel_copy(tasks);
+      }
+    }
+    // H2D after the chunk that used this buffer NB chunks ago has left the device
+    if (c >= static_cast<size_t>(E2E::NB)) OZEC_HIP(hipStreamWaitEvent(P.h2d, P.d2h_done[b], 0));
+    if (!in_pinned) {
+      // staged cells are already in the device layout: one copy of the data cells per stripe
+      for (size_t i = 0; i < cs; ++i)
+        OZEC_HIP(hipMemcpyAsync(d + i * dstripe, P.hstage[b] + i * dstripe, static_cast<size_t>(k) * len,
+                                hipMemcpyHostToDevice, P.h2d));
+    } else if (in_unit_stride == static_cast<int64_t>(len)) {
+      for (size_t i = 0; i < cs; ++i)  // the k data cells of a stripe are one run
+        OZEC_HIP(hipMemcpyAsync(d + i * dstripe, h_in + (s0 + i) * in_stripe_stride, static_cast<size_t>(k) * len,
+                                hipMemcpyHostToDevice, P.h2d));
+    } else {
+      for (size_t i = 0; i < cs; ++i)
+        for (int j = 0; j < k; ++j)
+          OZEC_HIP(hipMemcpyAsync(d + i * dstripe + static_cast<size_t>(j) * len,
+                                  h_in + (s0 + i) * in_stripe_stride + j * in_unit_stride, len, hipMemcpyHostToDevice,
+                                  P.h2d));
+    }
+    OZEC_HIP(hipEventRecord(P.h2d_done[b], P.h2d));
+    OZEC_HIP(hipStreamWaitEvent(P.comp, P.h2d_done[b], 0));
+    const int64_t ds = static_cast<int64_t>(dstripe), us = static_cast<int64_t>(len);
+    uint32_t *dcrc = reinterpret_cast<uint32_t *>(d + dcrc_off);
+    if (with_crc) {
+      if (int rc = ozec_encode_crc_batch(enc, d, ds, us, d + static_cast<size_t>(k) * len, ds, us, cs, len,
+                                         checksum_type, bpc, dcrc, big_endian, P.comp))
+        return rc;
+    } else {
+      if (int rc = ozec_encode_batch(enc, d, ds, us, d + static_cast<size_t>(k) * len, ds, us, cs, len, P.comp))
+        return rc;
+    }
+    OZEC_HIP(hipEventRecord(P.comp_done[b], P.comp));
+    OZEC_HIP(hipStreamWaitEvent(P.d2h, P.comp_done[b], 0));
+    uint8_t *hs = staged ? P.hstage[b] : nullptr;
+    for (size_t i = 0; i < cs; ++i) {
+      uint8_t *src = d + i * dstripe + static_cast<size_t>(k) * len;
+      if (!out_pinned) {
+        OZEC_HIP(hipMemcpyAsync(hs + i * dstripe + static_cast<size_t>(k) * len, src, static_cast<size_t>(p) * len,
+                                hipMemcpyDeviceToHost, P.d2h));
+      } else if (out_unit_stride == static_cast<int64_t>(len)) {
+        OZEC_HIP(hipMemcpyAsync(h_out + (s0 + i) * out_stripe_stride, src, static_cast<size_t>(p) * len,
+                                hipMemcpyDeviceToHost, P.d2h));
+      } else {
+        for (int r = 0; r < p; ++r)
+          OZEC_HIP(hipMemcpyAsync(h_out + (s0 + i) * out_stripe_stride + r * out_unit_stride, src + r * len, len,
+                                  hipMemcpyDeviceToHost, P.d2h));
+      }
+    }
+    if (with_crc)
+      OZEC_HIP(hipMemcpyAsync(crc_pinned ? reinterpret_cast<uint8_t *>(h_crcs + s0 * ncrc) : hs + dcrc_off, dcrc,
+                              cs * ncrc * sizeof(uint32_t), hipMemcpyDeviceToHost, P.d2h));
+    OZEC_HIP(hipEventRecord(P.d2h_done[b], P.d2h));
   }
-  // unfused: encode, then one CRC pass per unit (crcs[s][u][w] layout kept)
-  OZEC_HIP(ozec::launch_code(a, st));
-  for (int u = 0; u < units; ++u) {
-    CrcArgs c = e.crc;
-    c.base = u < k ? d_in + u * in_unit_stride : d_out + (u - k) * out_unit_stride;
-    c.cell_stride = u < k ? in_stripe_stride : out_stripe_stride;
-    c.out = d_crcs + u * nwin;
-    c.out_cell_stride = units * nwin;
-    OZEC_HIP(ozec::launch_crc_windows(c, st));
+  if (staged) {
+    for (size_t c = nch > static_cast<size_t>(E2E::NB) ? nch - E2E::NB : 0; c < nch; ++c)
+      if (int rc = unstage(c)) return rc;
   }
+  OZEC_HIP(hipStreamSynchronize(P.d2h));
   return OZEC_OK;
 }
 

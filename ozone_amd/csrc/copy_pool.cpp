@@ -1,5 +1,7 @@
 #include "copy_pool.hpp"
 
+#include "numa.hpp"
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -43,7 +45,18 @@ class Pool {
 
   void resize(int n) {
     std::lock_guard<std::mutex> lk(resize_mu_);
+    const int keep = nthreads_;
     stop_workers();
+    start_workers(n < 0 ? keep : n);
+  }
+
+  // restart the workers on the CPUs of `node` (the first GPU this process uses: its staging buffers live there)
+  void set_node(int node) {
+    std::lock_guard<std::mutex> lk(resize_mu_);
+    if (node == node_) return;
+    const int n = nthreads_;
+    stop_workers();
+    node_ = node;
     start_workers(n);
   }
 
@@ -71,7 +84,11 @@ class Pool {
   void start_workers(int n) {
     stop_ = false;
     nthreads_ = n;
-    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    for (int i = 0; i < n; ++i)
+      workers_.emplace_back([this, node = node_] {
+        (void)bind_thread_to_node(node);
+        loop();
+      });
   }
 
   void stop_workers() {
@@ -108,11 +125,14 @@ class Pool {
   std::vector<std::thread> workers_;
   bool stop_ = false;
   int nthreads_ = 0;
+  int node_ = -1;
 };
 
 }  // namespace
 
 void set_copy_threads(int n) { Pool::get().resize(std::max(0, n)); }
+
+void set_copy_node(int node) { Pool::get().set_node(node); }
 
 void parallel_copy(const std::vector<CopyTask> &tasks) {
   size_t total = 0;

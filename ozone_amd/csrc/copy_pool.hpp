@@ -17,5 +17,7 @@ struct CopyTask {
 void parallel_copy(const std::vector<CopyTask> &tasks);
 // threads used besides the caller (0 = copy inline); set by ozec_set_tuning("copy_threads", n)
 void set_copy_threads(int n);
+// bind the pool's workers to the CPUs of a NUMA node (-1: no binding)
+void set_copy_node(int node);
 
 }  // namespace ozec

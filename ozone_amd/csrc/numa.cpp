@@ -1,0 +1,164 @@
+#include "numa.hpp"
+
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <cctype>
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+
+namespace ozec {
+namespace {
+
+// <linux/mempolicy.h> constants (the image has no libnuma dependency in libozec)
+constexpr int kMpolPreferred = 1;
+constexpr unsigned kMpolMfMove = 1u << 1;
+constexpr int kMpolFNode = 1 << 0;
+constexpr int kMpolFAddr = 1 << 1;
+constexpr size_t kMaxNodes = 1024;
+constexpr size_t kHuge = 2u << 20;
+
+std::mutex g_mu;
+std::unordered_map<void *, size_t> g_allocs;  // pinned_alloc'ed regions -> mapped length
+
+size_t page_size() {
+  static const size_t ps = static_cast<size_t>(sysconf(_SC_PAGESIZE));
+  return ps;
+}
+
+bool read_file(const std::string &path, std::string &out) {
+  std::ifstream f(path);
+  if (!f) return false;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  out = ss.str();
+  return true;
+}
+
+// "0-63,128-191" -> cpu ids
+bool parse_cpulist(const std::string &s, cpu_set_t *set) {
+  CPU_ZERO(set);
+  size_t i = 0;
+  bool any = false;
+  while (i < s.size()) {
+    while (i < s.size() && !std::isdigit(static_cast<unsigned char>(s[i]))) ++i;
+    if (i >= s.size()) break;
+    size_t j = i;
+    while (j < s.size() && std::isdigit(static_cast<unsigned char>(s[j]))) ++j;
+    long lo = std::stol(s.substr(i, j - i)), hi = lo;
+    if (j < s.size() && s[j] == '-') {
+      size_t k = j + 1;
+      while (k < s.size() && std::isdigit(static_cast<unsigned char>(s[k]))) ++k;
+      hi = std::stol(s.substr(j + 1, k - j - 1));
+      j = k;
+    }
+    for (long c = lo; c <= hi && c < CPU_SETSIZE; ++c) {
+      CPU_SET(static_cast<int>(c), set);
+      any = true;
+    }
+    i = j;
+  }
+  return any;
+}
+
+}  // namespace
+
+int device_numa_node(int device) {
+  int v = -1;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeHostNumaId, device) == hipSuccess && v >= 0) return v;
+  (void)hipGetLastError();
+  char bus[64] = {};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  std::string id(bus);
+  for (auto &c : id) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  std::string s;
+  if (!read_file("/sys/bus/pci/devices/" + id + "/numa_node", s)) return -1;
+  try {
+    return std::stoi(s);
+  } catch (...) {
+    return -1;
+  }
+}
+
+int bind_to_node(void *p, size_t bytes, int node, bool move) {
+  if (node < 0 || !p || bytes == 0) return 0;
+  if (static_cast<size_t>(node) >= kMaxNodes) return -EINVAL;
+  const size_t ps = page_size();
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p) / ps * ps;
+  const uintptr_t hi = (reinterpret_cast<uintptr_t>(p) + bytes + ps - 1) / ps * ps;
+  unsigned long mask[kMaxNodes / (8 * sizeof(unsigned long))] = {};
+  mask[node / (8 * sizeof(unsigned long))] = 1ul << (node % (8 * sizeof(unsigned long)));
+  long rc = syscall(SYS_mbind, lo, hi - lo, kMpolPreferred, mask, kMaxNodes, move ? kMpolMfMove : 0u);
+  return rc == 0 ? 0 : -errno;
+}
+
+int page_node(const void *p) {
+  int node = -1;
+  long rc = syscall(SYS_get_mempolicy, &node, nullptr, 0ul, p, kMpolFNode | kMpolFAddr);
+  return rc == 0 ? node : -1;
+}
+
+int pinned_alloc(size_t bytes, int device, void **out) {
+  *out = nullptr;
+  if (bytes == 0) return 0;
+  const size_t len = (bytes + kHuge - 1) / kHuge * kHuge;
+  void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (p == MAP_FAILED) return -ENOMEM;
+  (void)madvise(p, len, MADV_HUGEPAGE);  // fewer translations per DMA; best effort
+  // placement first (pages are allocated on the first touch, which hipHostRegister does while pinning)
+  (void)bind_to_node(p, len, device >= 0 ? device_numa_node(device) : -1, false);
+  if (hipHostRegister(p, len, hipHostRegisterPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    munmap(p, len);
+    return -ENOMEM;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_allocs[p] = len;
+  }
+  *out = p;
+  return 0;
+}
+
+int pinned_free(void *p) {
+  if (!p) return 0;
+  size_t len = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_allocs.find(p);
+    if (it == g_allocs.end()) return -EINVAL;
+    len = it->second;
+    g_allocs.erase(it);
+  }
+  (void)hipHostUnregister(p);
+  munmap(p, len);
+  return 0;
+}
+
+int bind_thread_to_node(int node) {
+  if (node < 0) return 0;
+  std::string s;
+  if (!read_file("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", s)) return -ENOENT;
+  cpu_set_t want, have, both;
+  if (!parse_cpulist(s, &want)) return -EINVAL;
+  if (sched_getaffinity(0, sizeof(have), &have) != 0) return -errno;
+  CPU_AND(&both, &want, &have);
+  if (CPU_COUNT(&both) == 0) return -EINVAL;  // the process may not run there: leave it alone
+  return pthread_setaffinity_np(pthread_self(), sizeof(both), &both) == 0 ? 0 : -EINVAL;
+}
+
+}  // namespace ozec

@@ -1,0 +1,23 @@
+// NUMA-local pinned host memory for the per-GPU copy paths (end to end, host DRAM bandwidth and
+// the per-GPU PCIe link bound the multi-GPU path; pages on the wrong socket cross the inter-socket fabric on
+// every DMA).  A GPU's host NUMA node comes from HIP (hipDeviceAttributeHostNumaId) or sysfs; pages are placed
+// with mbind(2) before the first touch and then pinned with hipHostRegister.
+#pragma once
+#include <cstddef>
+
+namespace ozec {
+
+// host NUMA node closest to `device`, -1 when unknown or the host is not NUMA
+int device_numa_node(int device);
+// mbind [p, p+bytes) (page-aligned outward) to `node` with MPOL_PREFERRED (MOVE existing pages when move);
+// returns 0 or -errno.  node < 0 is a no-op.
+int bind_to_node(void *p, size_t bytes, int node, bool move);
+// node of the page holding p (after it has been touched), -1 if unknown
+int page_node(const void *p);
+// pinned host allocation whose pages live on the device's node; free with pinned_free
+int pinned_alloc(size_t bytes, int device, void **out);
+int pinned_free(void *p);
+// pin the calling thread / the copy-pool workers to the CPUs of `node` (intersected with the process mask)
+int bind_thread_to_node(int node);
+
+}  // namespace ozec

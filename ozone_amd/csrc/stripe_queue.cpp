@@ -14,6 +14,8 @@
 // 147 ms per 1024 stripes; 41 GB/s against a 57 GB/s link).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -22,6 +24,7 @@
 #include "../../include/ozec.h"
 #include "copy_pool.hpp"
 #include "kernels.hpp"
+#include "numa.hpp"
 #include "status.hpp"
 
 namespace {
@@ -71,6 +74,7 @@ struct Batch {
 
 struct ozec_stripe_queue {
   ozec_coder *enc = nullptr;
+  int device = 0;  // the queue's GPU (current device at creation); pinned staging lives on its NUMA node
   int k = 0, p = 0, rows = 0, ctype = OZEC_CHECKSUM_NONE, big_endian = 0;
   size_t cell_len = 0, S = 0, bpc = 0, nwin_max = 0;
   std::vector<Batch> batches;
@@ -145,23 +149,71 @@ struct ozec_stripe_queue {
   }
 
   int stage_pinned(Batch &b) {
-    if (!b.h_stage) SQ_HIP(hipHostMalloc(reinterpret_cast<void **>(&b.h_stage), S * stripe_bytes(), hipHostMallocDefault));
+    if (!b.h_stage && ozec::pinned_alloc(S * stripe_bytes(), device, reinterpret_cast<void **>(&b.h_stage)) != 0)
+      return set_error(OZEC_ENOMEM, "cannot pin the stripe queue's staging memory");
     return OZEC_OK;
   }
 };
 
 extern "C" {
 
-int ozec_host_alloc(size_t bytes, void **out) {
+int ozec_host_alloc_on(size_t bytes, int device, void **out) {
   if (!out) return set_error(OZEC_EINVAL, "null output");
   *out = nullptr;
   if (bytes == 0) return OZEC_OK;
-  SQ_HIP(hipHostMalloc(out, bytes, hipHostMallocDefault));
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    (void)hipGetLastError();
+    return set_error(OZEC_EDEVICE, "no such device " + std::to_string(device));
+  }
+  if (ozec::pinned_alloc(bytes, device, out) != 0)
+    return set_error(OZEC_ENOMEM, "cannot allocate " + std::to_string(bytes) + " bytes of pinned host memory");
   return OZEC_OK;
 }
 
+int ozec_host_alloc(size_t bytes, void **out) {
+  int dev = 0;
+  SQ_HIP(hipGetDevice(&dev));
+  return ozec_host_alloc_on(bytes, dev, out);
+}
+
 int ozec_host_free(void *p) {
-  if (p) SQ_HIP(hipHostFree(p));
+  if (!p) return OZEC_OK;
+  if (ozec::pinned_free(p) != 0) return set_error(OZEC_EINVAL, "pointer was not allocated by ozec_host_alloc");
+  return OZEC_OK;
+}
+
+int ozec_device_numa_node(int device, int *node) {
+  if (!node) return set_error(OZEC_EINVAL, "null output");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    (void)hipGetLastError();
+    return set_error(OZEC_EDEVICE, "no such device " + std::to_string(device));
+  }
+  *node = ozec::device_numa_node(device);
+  return OZEC_OK;
+}
+
+int ozec_host_page_node(const void *p, int *node) {
+  if (!p || !node) return set_error(OZEC_EINVAL, "null pointer");
+  *node = ozec::page_node(p);
+  return OZEC_OK;
+}
+
+int ozec_host_register(void *p, size_t bytes, int device) {
+  if (!p) return set_error(OZEC_EINVAL, "null pointer");
+  if (bytes == 0) return OZEC_OK;
+  const int node = device >= 0 ? ozec::device_numa_node(device) : -1;
+  // pages not touched yet are placed on the node as hipHostRegister faults them in; touched ones are moved
+  if (int e = ozec::bind_to_node(p, bytes, node, true))
+    return set_error(OZEC_EINVAL, "mbind to node " + std::to_string(node) + " failed: " + std::strerror(-e));
+  SQ_HIP(hipHostRegister(p, bytes, hipHostRegisterPortable));
+  return OZEC_OK;
+}
+
+int ozec_host_unregister(void *p) {
+  if (!p) return set_error(OZEC_EINVAL, "null pointer");
+  SQ_HIP(hipHostUnregister(p));
   return OZEC_OK;
 }
 
@@ -180,6 +232,10 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
   auto *q = new (std::nothrow) ozec_stripe_queue();
   if (!q) return set_error(OZEC_ENOMEM, "out of memory");
   q->enc = enc;
+  if (hipGetDevice(&q->device) != hipSuccess) {
+    delete q;
+    return set_error(OZEC_EDEVICE, "no current device");
+  }
   q->k = k;
   q->p = p;
   q->rows = codec == OZEC_CODEC_XOR ? 1 : p;
@@ -199,9 +255,9 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&b.d_units), q->S * q->stripe_bytes());
     if (e == hipSuccess && q->ctype != OZEC_CHECKSUM_NONE) {
       e = hipMalloc(reinterpret_cast<void **>(&b.d_crcs), q->S * q->stripe_crcs() * sizeof(uint32_t));
-      if (e == hipSuccess)
-        e = hipHostMalloc(reinterpret_cast<void **>(&b.h_crcs), q->S * q->stripe_crcs() * sizeof(uint32_t),
-                          hipHostMallocDefault);
+      if (e == hipSuccess && ozec::pinned_alloc(q->S * q->stripe_crcs() * sizeof(uint32_t), q->device,
+                                                reinterpret_cast<void **>(&b.h_crcs)) != 0)
+        e = hipErrorOutOfMemory;
     }
     if (e != hipSuccess) {
       ozec_stripe_queue_free(q);
@@ -224,13 +280,17 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
     return set_error(OZEC_EINVAL, "stripe length must be in [1, cell_len] (" + std::to_string(q->cell_len) + ")");
   std::lock_guard<std::mutex> lk(q->mu);
   Batch *b = &q->batches[q->cur];
-  if (b->n > 0 && (b->in_flight || b->len != len)) {  // a batch holds one cell length; rotate
+  // cur only ever points at a filling batch or, once the ring has wrapped, at the oldest in-flight one: that one
+  // completes now (its callers' outputs land) and is refilled
+  if (b->in_flight)
+    if (int rc = q->complete(*b)) return rc;
+  if (b->n > 0 && b->len != len) {  // a batch holds one cell length: launch it and move on
     if (int rc = q->launch(*b)) return rc;
     q->cur = (q->cur + 1) % q->batches.size();
     b = &q->batches[q->cur];
+    if (b->in_flight)
+      if (int rc = q->complete(*b)) return rc;
   }
-  if (b->in_flight)
-    if (int rc = q->complete(*b)) return rc;  // oldest batch: its callers' outputs land now
   if (b->n == 0) {
     b->len = len;
     b->first_ticket = q->next_ticket;
@@ -301,17 +361,56 @@ int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket) {
   }
 }
 
+int ozec_stripe_queue_state(ozec_stripe_queue *q, size_t *in_flight, uint64_t *oldest_in_flight_ticket,
+                            size_t *filling) {
+  if (!q) return set_error(OZEC_EINVAL, "null queue");
+  std::lock_guard<std::mutex> lk(q->mu);
+  size_t n = 0, f = 0;
+  uint64_t oldest = UINT64_MAX;
+  for (const Batch &b : q->batches) {
+    if (b.in_flight) {
+      ++n;
+      oldest = std::min(oldest, b.first_ticket);
+    } else {
+      f += b.n;
+    }
+  }
+  if (in_flight) *in_flight = n;
+  if (oldest_in_flight_ticket) *oldest_in_flight_ticket = oldest;
+  if (filling) *filling = f;
+  return OZEC_OK;
+}
+
 int ozec_stripe_queue_free(ozec_stripe_queue *q) {
   if (!q) return OZEC_OK;
   int rc = OZEC_OK;
-  // H2D copies of a batch never launched (submitted, then freed without flush) still write its device buffer
+  // Stripes submitted but never waited for are completed here, oldest first: a filling batch is launched and
+  // every batch's parity / CRCs land in the callers' buffers before they are released (ozec.h: the buffers
+  // stay valid until wait() or free).
+  {
+    std::lock_guard<std::mutex> lk(q->mu);
+    for (;;) {
+      Batch *oldest = nullptr;
+      for (Batch &b : q->batches)
+        if (b.n > 0 && (!oldest || b.first_ticket < oldest->first_ticket)) oldest = &b;
+      if (!oldest) break;
+      int r = oldest->in_flight ? OZEC_OK : q->launch(*oldest);
+      if (r == OZEC_OK) r = q->complete(*oldest);
+      if (r != OZEC_OK) {  // drop it: its DMA is waited for below, its callers get nothing
+        rc = r;
+        oldest->n = 0;
+        oldest->in_flight = false;
+      }
+    }
+  }
+  // H2D copies of a batch never launched still write its device buffer
   if (q->h2d && hipStreamSynchronize(q->h2d) != hipSuccess) rc = OZEC_EDEVICE;
   for (Batch &b : q->batches) {
-    if (b.in_flight && hipEventSynchronize(b.done) != hipSuccess) rc = OZEC_EDEVICE;
+    if (b.stream && hipStreamSynchronize(b.stream) != hipSuccess) rc = OZEC_EDEVICE;
     if (b.d_units) (void)hipFree(b.d_units);
     if (b.d_crcs) (void)hipFree(b.d_crcs);
-    if (b.h_stage) (void)hipHostFree(b.h_stage);
-    if (b.h_crcs) (void)hipHostFree(b.h_crcs);
+    if (b.h_stage) (void)ozec::pinned_free(b.h_stage);
+    if (b.h_crcs) (void)ozec::pinned_free(b.h_crcs);
     if (b.done) (void)hipEventDestroy(b.done);
     if (b.copied) (void)hipEventDestroy(b.copied);
     if (b.stream) (void)hipStreamDestroy(b.stream);

@@ -94,7 +94,29 @@ def _codec_id(name):
 
 # ---------------------------------------------------------------- helpers ------------------------------
 
-def _as_buffers(items):
+def _in_array(x):
+    """A byte[] input: any uint8 buffer; strided views are copied into one contiguous run (the library reads
+    `len` bytes from the address).  Other dtypes are rejected rather than reinterpreted."""
+    if x is None:
+        return None
+    a = x if isinstance(x, np.ndarray) else np.frombuffer(x, np.uint8)
+    if a.dtype != np.uint8 or a.ndim != 1:
+        raise IllegalArgumentException(f"Invalid buffer: a 1-D uint8 array is required, got {a.dtype} {a.shape}")
+    return np.ascontiguousarray(a)
+
+
+def _out_array(x):
+    """A byte[] output is written in place, so it must be one writeable contiguous run of uint8 (a strided view
+    would be written past its elements; `bytes` is immutable)."""
+    if x is None:
+        return None
+    a = x if isinstance(x, np.ndarray) else np.frombuffer(x, np.uint8)
+    if a.dtype != np.uint8 or a.ndim != 1 or not a.flags.c_contiguous or not a.flags.writeable:
+        raise IllegalArgumentException("Invalid output buffer: a writeable 1-D C-contiguous uint8 array is required")
+    return a
+
+
+def _as_buffers(items, outputs=False):
     """Accept ByteBuffer, ECChunk, numpy uint8 arrays, bytearray or None for each slot."""
     out = []
     for x in items:
@@ -103,8 +125,7 @@ def _as_buffers(items):
         elif isinstance(x, ECChunk):
             out.append(ECChunk.to_buffers([x])[0])
         else:
-            a = x if isinstance(x, np.ndarray) else np.frombuffer(x, np.uint8)
-            out.append(ByteBuffer.wrap(a))
+            out.append(ByteBuffer.wrap(_out_array(x) if outputs else _in_array(x)))
     return out
 
 
@@ -191,7 +212,7 @@ class RawErasureEncoder(_Coder):
         if not any(isinstance(x, (ByteBuffer, ECChunk)) for x in list(inputs) + list(outputs)):
             return self._encode_arrays(inputs, outputs)
         ins = _as_buffers(inputs)
-        outs = _as_buffers(outputs)
+        outs = _as_buffers(outputs, outputs=True)
         # ByteBufferEncodingState (ByteBufferEncodingState.java:36-48) + EncodingState.checkParameters
         valid = _first_valid(ins)
         n = valid.remaining()
@@ -214,7 +235,7 @@ class RawErasureEncoder(_Coder):
 
     def _encode_arrays(self, inputs, outputs):
         """encode(byte[][] inputs, byte[][] outputs) (RawErasureEncoder.java:114-125)."""
-        ins = [x if x is None or isinstance(x, np.ndarray) else np.frombuffer(x, np.uint8) for x in inputs]
+        ins = [_in_array(x) for x in inputs]
         outs = list(outputs)
         n = _first_valid(ins).size
         self._check_parameters(ins, outs)
@@ -226,7 +247,7 @@ class RawErasureEncoder(_Coder):
                     raise HadoopIllegalArgumentException(f"Invalid buffer not of length {n}")
         if n == 0:
             return
-        outs = [o if isinstance(o, np.ndarray) else np.frombuffer(o, np.uint8) for o in outs]
+        outs = [_out_array(o) for o in outs]
         self._run([x.ctypes.data for x in ins], [o.ctypes.data for o in outs], n)
 
     def _check_parameters(self, ins, outs):
@@ -278,6 +299,21 @@ class RawErasureEncoder(_Coder):
             _raise_for(rc)
 
 
+    def encode_crc_host_batch(self, h_in, in_stripe_stride, in_unit_stride, h_out, out_stripe_stride,
+                              out_unit_stride, num_stripes, length, checksum_type, bytes_per_checksum, h_crcs=None,
+                              big_endian=False, stripes_per_chunk=0):
+        """End-to-end encode (+ CRC) of stripes in host memory (ozec_encode_crc_host_batch): host
+        addresses (ints) or numpy arrays; registered / pinned memory is DMA'd in place.  Synchronous."""
+        def addr(x):
+            return None if x is None else x if isinstance(x, int) else x.ctypes.data
+        rc = L.lib().ozec_encode_crc_host_batch(self._handle, addr(h_in), in_stripe_stride, in_unit_stride, addr(h_out),
+                                                out_stripe_stride, out_unit_stride, num_stripes, length,
+                                                int(checksum_type), bytes_per_checksum, addr(h_crcs),
+                                                1 if big_endian else 0, stripes_per_chunk)
+        if rc != L.OZEC_OK:
+            _raise_for(rc)
+
+
 # ---------------------------------------------------------------- decoder --------------------------------
 
 class RawErasureDecoder(_Coder):
@@ -292,7 +328,7 @@ class RawErasureDecoder(_Coder):
             if not any(isinstance(x, (ByteBuffer, ECChunk)) for x in list(inputs) + list(outputs)):
                 return self._decode_arrays(inputs, erased_indexes, outputs)
             ins = _as_buffers(inputs)
-            outs = _as_buffers(outputs)
+            outs = _as_buffers(outputs, outputs=True)
             valid = _first_valid(ins)
             n = valid.remaining()
             direct = valid.is_direct()
@@ -325,9 +361,8 @@ class RawErasureDecoder(_Coder):
                     b.position(b.position() + n)
 
     def _decode_arrays(self, inputs, erased_indexes, outputs):
-        ins = [None if x is None else (x if isinstance(x, np.ndarray) else np.frombuffer(x, np.uint8))
-               for x in inputs]
-        n = _first_valid([None if x is None else x for x in ins]).size
+        ins = [_in_array(x) for x in inputs]
+        n = _first_valid(ins).size
         self._check_parameters(ins, erased_indexes, outputs)
         count = 0
         for b in ins:
@@ -345,8 +380,9 @@ class RawErasureDecoder(_Coder):
                 raise IllegalArgumentException(f"Invalid buffer not of length {n}")
         if n == 0:
             return
+        outs = [_out_array(o) for o in outputs]
         self._run([None if b is None else b.ctypes.data for b in ins], erased_indexes,
-                  [o.ctypes.data for o in outputs], n)
+                  [o.ctypes.data for o in outs], n)
 
     def _check_parameters(self, ins, erased, outs):
         # DecodingState.checkParameters (DecodingState.java:35-51)

@@ -16,11 +16,15 @@ from .rawcoder import IllegalArgumentException, _raise_for
 
 
 class PinnedBuffer:
-    """Pinned host memory from ozec_host_alloc, viewed as a uint8 numpy array (`.array`)."""
+    """Pinned host memory from ozec_host_alloc(_on), viewed as a uint8 numpy array (`.array`).  Its pages live on
+    the NUMA node of `device` (default: the current device)."""
 
-    def __init__(self, nbytes):
+    def __init__(self, nbytes, device=None):
         self._p = ctypes.c_void_p()
-        rc = L.lib().ozec_host_alloc(nbytes, ctypes.byref(self._p))
+        if device is None:
+            rc = L.lib().ozec_host_alloc(nbytes, ctypes.byref(self._p))
+        else:
+            rc = L.lib().ozec_host_alloc_on(nbytes, device, ctypes.byref(self._p))
         if rc != L.OZEC_OK:
             _raise_for(rc)
         self.nbytes = nbytes
@@ -40,8 +44,39 @@ class PinnedBuffer:
             pass
 
 
-def host_alloc(nbytes):
-    return PinnedBuffer(nbytes)
+def host_alloc(nbytes, device=None):
+    return PinnedBuffer(nbytes, device)
+
+
+def device_numa_node(device):
+    """Host NUMA node closest to `device` (-1: unknown)."""
+    n = ctypes.c_int()
+    rc = L.lib().ozec_device_numa_node(device, ctypes.byref(n))
+    if rc != L.OZEC_OK:
+        _raise_for(rc)
+    return n.value
+
+
+def page_node(addr):
+    """NUMA node of the (touched) page at host address `addr`, -1 if unknown."""
+    n = ctypes.c_int()
+    rc = L.lib().ozec_host_page_node(addr, ctypes.byref(n))
+    if rc != L.OZEC_OK:
+        _raise_for(rc)
+    return n.value
+
+
+def host_register(addr, nbytes, device):
+    """Pin [addr, addr+nbytes) for DMA, its pages placed on `device`'s NUMA node (device < 0: no placement)."""
+    rc = L.lib().ozec_host_register(addr, nbytes, device)
+    if rc != L.OZEC_OK:
+        _raise_for(rc)
+
+
+def host_unregister(addr):
+    rc = L.lib().ozec_host_unregister(addr)
+    if rc != L.OZEC_OK:
+        _raise_for(rc)
 
 
 class StripeQueue:
@@ -52,6 +87,9 @@ class StripeQueue:
         self._enc = encoder  # keeps the coder alive
         self._k = encoder.get_num_data_units()
         self._p = encoder.get_num_parity_units()
+        # CRCs cover the coded units: k data + p parity (XOR codes one parity row)
+        self._units = self._k + (1 if encoder._config.get_codec() == "xor" else self._p)
+        self._bpc = bytes_per_checksum if int(checksum_type) != int(ChecksumType.NONE) else 0
         self._h = ctypes.c_void_p()
         rc = L.lib().ozec_stripe_queue_create(encoder._handle, cell_len, stripes_per_batch, int(checksum_type),
                                               bytes_per_checksum, 1 if big_endian else 0, ctypes.byref(self._h))
@@ -65,9 +103,22 @@ class StripeQueue:
         if len(data) != self._k or len(parity) != self._p:
             raise IllegalArgumentException("Invalid inputs/outputs length")
         n = length if length is not None else data[0].size
+        # the library DMA's n contiguous bytes from / into each address and memcpy's units * windows uint32
+        # values into crcs, so every buffer must be exactly what it claims to be
         for a in list(data) + list(parity):
+            if not isinstance(a, np.ndarray) or a.dtype != np.uint8 or not a.flags.c_contiguous:
+                raise IllegalArgumentException("Invalid buffer: C-contiguous uint8 arrays are required")
             if a.size < n:
                 raise IllegalArgumentException(f"Invalid buffer, not of length {n}")
+        for a in parity:
+            if not a.flags.writeable:
+                raise IllegalArgumentException("Invalid buffer: parity buffers must be writeable")
+        if crcs is not None:
+            need = self._units * (-(-n // self._bpc)) if self._bpc else 0
+            if (not isinstance(crcs, np.ndarray) or crcs.dtype not in (np.uint32, np.int32)
+                    or not crcs.flags.c_contiguous or not crcs.flags.writeable or crcs.size < need):
+                raise IllegalArgumentException(
+                    f"Invalid crcs buffer: a writeable C-contiguous uint32 array of >= {need} elements is required")
         t = ctypes.c_uint64()
         rc = L.lib().ozec_stripe_queue_submit(self._h, L.ptr_array([a.ctypes.data for a in data]),
                                               L.ptr_array([a.ctypes.data for a in parity]), n,
@@ -76,6 +127,14 @@ class StripeQueue:
             _raise_for(rc)
         self._held.append((t.value, (list(data), list(parity), crcs)))
         return t.value
+
+    def state(self):
+        """(batches in flight, first ticket of the oldest in-flight batch or None, stripes in filling batches)."""
+        n, t, f = ctypes.c_size_t(), ctypes.c_uint64(), ctypes.c_size_t()
+        rc = L.lib().ozec_stripe_queue_state(self._h, ctypes.byref(n), ctypes.byref(t), ctypes.byref(f))
+        if rc != L.OZEC_OK:
+            _raise_for(rc)
+        return n.value, (None if t.value == (1 << 64) - 1 else t.value), f.value
 
     def flush(self):
         rc = L.lib().ozec_stripe_queue_flush(self._h)

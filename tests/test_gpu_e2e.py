@@ -1,0 +1,205 @@
+"""BASELINE configs[4] (C5) path and its host memory: ozec_encode_crc_host_batch against the oracle (pinned and
+pageable batches, several chunkings), NUMA-local pinned allocations, and one host batch split by stripe range
+between two rank processes on one device (the multi-GPU partition of SURVEY §8(e), rehearsed on one GPU)."""
+import ctypes
+import mmap
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle
+from synth import SEED, cells
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from ozone_amd import checksum as ck  # noqa: E402
+from ozone_amd import rawcoder as rc  # noqa: E402
+from ozone_amd.shard import stripe_range  # noqa: E402
+from ozone_amd.stripe_queue import device_numa_node, host_alloc, host_register, host_unregister, page_node  # noqa
+
+OTYPE = {ck.ChecksumType.CRC32C: oracle.CRC32C, ck.ChecksumType.CRC32: oracle.CRC32}
+
+
+def _batch(S, k, p, n, first, extra_unit_gap=0):
+    """[S][k+p][n] host batch (data from the oracle's generator, parity slots 0xA5) with optional gap per unit."""
+    us = n + extra_unit_gap
+    buf = np.full(S * (k + p) * us, 0xA5, np.uint8)
+    v = buf.reshape(S, k + p, us)
+    for s in range(S):
+        for j, x in enumerate(cells(SEED, first + s * k, k, n)):
+            v[s, j, :n] = x
+    return buf, v, us
+
+
+def _check(v, crcs, codec, k, p, n, S, ctype, bpc, big_endian=False):
+    nwin = (n + bpc - 1) // bpc if ctype != ck.ChecksumType.NONE else 0
+    units = k + (1 if codec == "xor" else p)
+    for s in range(S):
+        d = [np.array(v[s, j, :n]) for j in range(k)]
+        ref = oracle.rs_encode(k, p, d) if codec == "rs" else [oracle.xor_encode(d)] + [np.zeros(n, np.uint8)] * (p - 1)
+        for r in range(p):
+            assert (v[s, k + r, :n] == ref[r]).all(), (s, r)
+        if nwin:
+            got = crcs.reshape(S, units, nwin)[s]
+            if big_endian:
+                got = got.byteswap()
+            for u, cell in enumerate(d + ref[:units - k]):
+                assert (got[u] == oracle.crc_windows(OTYPE[ctype], cell, bpc)).all(), (s, u)
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("codec,k,p,n,S,chunk,ctype,bpc", [
+    ("rs", 6, 3, 1 << 16, 37, 8, ck.ChecksumType.CRC32C, 16384),   # 5 chunks through a ring of 3
+    ("rs", 6, 3, 1 << 20, 5, 0, ck.ChecksumType.CRC32C, 16384),    # C5 cells, default chunking
+    ("rs", 10, 4, 50000, 7, 2, ck.ChecksumType.CRC32, 4096),       # unfused fallback shape (len % 16 != 0)
+    ("rs", 3, 2, 1 << 15, 9, 4, ck.ChecksumType.NONE, 0),          # encode only
+    ("xor", 2, 1, 1 << 16, 11, 3, ck.ChecksumType.CRC32C, 8192),
+    ("xor", 3, 2, 1 << 14, 6, 4, ck.ChecksumType.CRC32C, 4096),    # XOR p > 1: extra parity zero-filled
+])
+def test_host_batch_vs_oracle(pinned, codec, k, p, n, S, chunk, ctype, bpc):
+    buf, v, us = _batch(S, k, p, n, 800000 + 1000 * k)
+    units = k + (1 if codec == "xor" else p)
+    nwin = (n + bpc - 1) // bpc if bpc else 0
+    crcs = np.zeros(max(1, S * units * nwin), np.uint32)
+    keep = []
+    if pinned:  # the whole batch and the CRC area registered, as bench.py's C5 batch is
+        pb = host_alloc(buf.nbytes)
+        pb.array[:] = buf
+        pc = host_alloc(crcs.nbytes)
+        pc.array[:] = 0
+        keep += [pb, pc]
+        v = pb.array.reshape(S, k + p, us)
+        crcs = pc.array.view(np.uint32)
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec))
+    base = v.ctypes.data
+    e.encode_crc_host_batch(base, (k + p) * us, us, base + k * us, (k + p) * us, us, S, n, ctype, bpc,
+                            crcs if ctype != ck.ChecksumType.NONE else None, False, chunk)
+    _check(v, crcs, codec, k, p, n, S, ctype, bpc)
+
+
+def test_host_batch_strided_units_and_big_endian():
+    """Units not back to back (a gap after every cell): the per-cell copy path; CRCs stored big-endian."""
+    k, p, n, S, bpc = 6, 3, 1 << 15, 6, 4096
+    buf, v, us = _batch(S, k, p, n, 810000, extra_unit_gap=4096)
+    pb = host_alloc(buf.nbytes)
+    pb.array[:] = buf
+    v = pb.array.reshape(S, k + p, us)
+    crcs = np.zeros(S * (k + p) * (n // bpc), np.uint32)
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    base = v.ctypes.data
+    e.encode_crc_host_batch(base, (k + p) * us, us, base + k * us, (k + p) * us, us, S, n, ck.ChecksumType.CRC32C,
+                            bpc, crcs, True, 4)
+    _check(v, crcs, "rs", k, p, n, S, ck.ChecksumType.CRC32C, bpc, big_endian=True)
+    assert (v[:, :, n:] == 0xA5).all()  # the gaps are untouched
+
+
+def test_host_batch_errors():
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(6, 3))
+    buf = np.zeros(9 * 4096, np.uint8)
+    with pytest.raises(rc.IllegalArgumentException):
+        e.encode_crc_host_batch(buf, 9 * 4096, 4096, None, 9 * 4096, 4096, 1, 4096, ck.ChecksumType.CRC32C, 4096,
+                                np.zeros(9, np.uint32))
+    with pytest.raises(rc.IllegalArgumentException):  # CRC requested without a CRC buffer
+        e.encode_crc_host_batch(buf, 9 * 4096, 4096, buf.ctypes.data + 6 * 4096, 9 * 4096, 4096, 1, 4096,
+                                ck.ChecksumType.CRC32C, 4096, None)
+    e.release()
+    with pytest.raises(rc.IOException):
+        e.encode_crc_host_batch(buf, 9 * 4096, 4096, buf.ctypes.data + 6 * 4096, 9 * 4096, 4096, 1, 4096,
+                                ck.ChecksumType.NONE, 0, None)
+
+
+def test_pinned_memory_is_numa_local():
+    """ozec_host_alloc places its pages on the GPU's NUMA node (mbind before the pinning touch)."""
+    node = device_numa_node(0)
+    pb = host_alloc(64 << 20)
+    pb.array[::4096] = 1
+    got = {page_node(pb.array.ctypes.data + off) for off in (0, 32 << 20, (64 << 20) - 1)}
+    if node < 0:
+        pytest.skip("host reports no NUMA node for the GPU")
+    assert got == {node}, (node, got)
+    pb.free()
+    # ozec_host_register places a caller's (untouched) mapping the same way and pins it
+    mm = mmap.mmap(-1, 16 << 20)
+    anchor = ctypes.c_char.from_buffer(mm)
+    addr = ctypes.addressof(anchor)
+    host_register(addr, 16 << 20, 0)
+    assert page_node(addr) == node and page_node(addr + (16 << 20) - 1) == node
+    host_unregister(addr)
+    del anchor
+    mm.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank(rank, world, port, path, S, n, bpc, q):
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)  # both "GPUs" are device 0 here
+        from ozone_amd import checksum as ck_
+        from ozone_amd import rawcoder as rc_
+        k, p = 6, 3
+        sb = (k + p) * n
+        total = os.path.getsize(path)
+        fd = os.open(path, os.O_RDWR)
+        mm = mmap.mmap(fd, total, mmap.MAP_SHARED)
+        os.close(fd)
+        anchor = ctypes.c_char.from_buffer(mm)
+        base = ctypes.addressof(anchor)
+        lo, hi = stripe_range(S, rank, world)
+        nwin = n // bpc
+        crc_off = S * sb
+        host_register(base + lo * sb, (hi - lo) * sb, 0)
+        e = rc_.RawErasureEncoder(rc_.ECReplicationConfig(k, p))
+        e.encode_crc_host_batch(base + lo * sb, sb, n, base + lo * sb + k * n, sb, n, hi - lo, n,
+                                ck_.ChecksumType.CRC32C, bpc, base + crc_off + lo * (k + p) * nwin * 4, False, 2)
+        host_unregister(base + lo * sb)
+        dist.barrier()
+        dist.destroy_process_group()
+        del anchor
+        mm.close()
+        q.put((rank, "ok"))
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(ex)))
+
+
+def test_two_ranks_split_one_host_batch_on_one_device():
+    """Two rank processes (gloo) each take their contiguous stripe range of ONE shared host batch, register it and
+    run ozec_encode_crc_host_batch on the same GPU; the union is bit-exact against the oracle.  This is the N > 1
+    partition of bench.py's C5 leg (ranks own disjoint ranges, no collective on the data path)."""
+    import torch.multiprocessing as mp
+    S, n, bpc, k, p = 9, 1 << 16, 16384, 6, 3
+    nwin = n // bpc
+    buf, v, us = _batch(S, k, p, n, 820000)
+    # shared memory (tmpfs), as bench.py's batch: long-term pinning of file-backed pages is refused by the kernel
+    path = f"/dev/shm/ozec_test_batch_{os.getpid()}"
+    with open(path, "wb") as f:
+        f.write(buf.tobytes())
+        f.write(np.zeros(S * (k + p) * nwin, np.uint32).tobytes())
+    try:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_rank, args=(r, 2, port, path, S, n, bpc, q)) for r in range(2)]
+        for pr in procs:
+            pr.start()
+        res = dict(q.get(timeout=120) for _ in range(2))
+        for pr in procs:
+            pr.join(timeout=60)
+        assert res == {0: "ok", 1: "ok"}, res
+        raw = np.fromfile(path, np.uint8)
+    finally:
+        os.unlink(path)
+    v = raw[:S * (k + p) * n].reshape(S, k + p, n)
+    crcs = raw[S * (k + p) * n:].view(np.uint32)
+    _check(v, crcs, "rs", k, p, n, S, ck.ChecksumType.CRC32C, bpc)

@@ -515,7 +515,89 @@ def test_full_size_rs_6_3_crc_fused_matches_unfused():
     ref = torch.zeros_like(crcs)
     ck.checksum_windows_batch(ck.ChecksumType.CRC32C, units, n, (k + p) * S, n, bpc, ref)
     assert torch.equal(crcs, ref)
+    # and the oracle itself, on stripes spread over the batch: parity and all 9 units' window CRCs
+    for s in (0, 1777, S - 1):
+        host = h(units[s])
+        refp = oracle.rs_encode(k, p, list(host[:k]))
+        assert all((host[k + r] == refp[r]).all() for r in range(p)), s
+        got = h(crcs[s]).view(np.uint32)
+        for u in range(k + p):
+            assert (got[u] == oracle.crc_windows(oracle.CRC32C, host[u], bpc)).all(), (s, u)
     del units, crcs, ref
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("erased", [[0, 1, 2, 3], [1, 4, 10, 13]])
+def test_full_size_c3r_reconstruction_2048_stripes(erased):
+    """The C3r bench shape under a parity check: 2048 stripes of rs-10-4-1024k, verify the stored CRC32C of the 10
+    units read, rebuild 4, CRC the rebuilt units -- every rebuilt unit equals the original, every rebuilt CRC the
+    stored one, no stripe reports a mismatch; then one silently corrupted window is reported for its stripe only.
+    Oracle spot checks on the first and last stripe."""
+    k, p, n, S, bpc = 10, 4, 1 << 20, 2048, 16384
+    nwin = n // bpc
+    units = torch.empty((S, k + p, n), dtype=torch.uint8, device=DEV)
+    for u in range(k):
+        rc.fill_splitmix64_cells(units[:, u], (k + p) * n, S, n, SEED, 500000 + u * S)
+    enc("rs", k, p).encode_batch(units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n)
+    stored = torch.empty((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    ck.checksum_windows_batch(ck.ChecksumType.CRC32C, units, n, S * (k + p), n, bpc, stored)
+    present = [u for u in range(k + p) if u not in erased]
+    out = torch.empty((S, 4, n), dtype=torch.uint8, device=DEV)
+    out_crc = torch.empty((S, 4, nwin), dtype=torch.int32, device=DEV)
+    mism = torch.empty(S, dtype=torch.int32, device=DEV)
+    d = dec("rs", k, p)
+    d.reconstruct_crc_batch(units, (k + p) * n, n, present, erased, out, 4 * n, n, S, n, ck.ChecksumType.CRC32C, bpc,
+                            out_crc, d_expected=stored, d_mismatch=mism)
+    assert bool((mism == -1).all())
+    for i, e in enumerate(erased):
+        assert torch.equal(out[:, i], units[:, e]), e
+        assert torch.equal(out_crc[:, i], stored[:, e]), e
+    for s in (0, S - 1):
+        host = h(units[s])
+        refp = oracle.rs_encode(k, p, list(host[:k]))
+        assert all((host[k + r] == refp[r]).all() for r in range(p))
+        o = h(out[s])
+        oc = h(out_crc[s]).view(np.uint32)
+        for i, e in enumerate(erased):
+            assert (o[i] == host[e]).all()
+            assert (oc[i] == oracle.crc_windows(oracle.CRC32C, host[e], bpc)).all()
+    read = present[:k]
+    victim = 1234
+    units[victim, read[3], 7 * bpc + 5] ^= 0x40
+    d.reconstruct_crc_batch(units, (k + p) * n, n, present, erased, out, 4 * n, n, S, n, ck.ChecksumType.CRC32C, bpc,
+                            out_crc, d_expected=stored, d_mismatch=mism)
+    m = h(mism)
+    assert m[victim] == read[3] * nwin + 7
+    assert (np.delete(m, victim) == -1).all()
+    del units, stored, out, out_crc, mism
+    torch.cuda.empty_cache()
+
+
+def test_full_size_c4_block_major_256mib_blocks():
+    """C4 on its real layout: 16 block groups of 2 data + 1 parity block of 256 MiB, block-major (unit stride
+    256 MiB), fused xor-2-1 + CRC32C/16 KiB per group: parity equals torch's XOR, every window CRC equals the
+    CRC-only kernel's over the same block-major cells, and the oracle agrees on a spot check."""
+    G, B, n, bpc = 16, 256, 1 << 20, 16384
+    nwin = n // bpc
+    blocks = torch.empty((G, 3, B * n), dtype=torch.uint8, device=DEV)
+    for u in range(2):
+        rc.fill_splitmix64_cells(blocks[:, u], 3 * B * n, G, B * n, SEED, 600000 + u * G)
+    blocks[:, 2].fill_(0x5A)
+    crcs = torch.zeros((G, B, 3, nwin), dtype=torch.int32, device=DEV)
+    e = enc("xor", 2, 1)
+    for g in range(G):
+        e.encode_crc_batch(blocks[g], n, B * n, blocks[g, 2:], n, B * n, B, n, ck.ChecksumType.CRC32C, bpc, crcs[g])
+    assert torch.equal(blocks[:, 2], torch.bitwise_xor(blocks[:, 0], blocks[:, 1]))
+    ref = torch.zeros((G, 3, B, nwin), dtype=torch.int32, device=DEV)
+    ck.checksum_windows_batch(ck.ChecksumType.CRC32C, blocks, n, G * 3 * B, n, bpc, ref)  # cells in block order
+    assert torch.equal(crcs, ref.permute(0, 2, 1, 3))
+    g, s = 11, 200
+    host = h(blocks[g, :, s * n:(s + 1) * n])
+    got = h(crcs[g, s]).view(np.uint32)
+    for u in range(3):
+        assert (got[u] == oracle.crc_windows(oracle.CRC32C, host[u], bpc)).all()
+    assert (host[2] == oracle.xor_encode([host[0], host[1]])).all()
+    del blocks, crcs, ref
     torch.cuda.empty_cache()
 
 
@@ -585,3 +667,48 @@ def test_host_path_chunked_pipeline(chunk, copy_threads):
     finally:
         L.lib().ozec_set_tuning(b"host_chunk", 256 << 10)
         L.lib().ozec_set_tuning(b"copy_threads", 3)
+
+
+def test_encode_crc_batch_xor_p2_zero_fills_extra_parity():
+    """the fused batch path resets XOR outputs past the first, like ozec_encode_batch and
+    XORRawEncoder (XORRawEncoder.java:67-85)."""
+    k, p, n, S, bpc = 3, 2, 1 << 16, 4, 16384
+    units = torch.full((S, k + p, n), 0xA5, dtype=torch.uint8, device=DEV)
+    for u in range(k):
+        rc.fill_splitmix64_cells(units[:, u], (k + p) * n, S, n, SEED, 700000 + u * S)
+    crcs = torch.zeros((S, k + 1, n // bpc), dtype=torch.int32, device=DEV)
+    enc("xor", k, p).encode_crc_batch(units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n,
+                                      ck.ChecksumType.CRC32C, bpc, crcs)
+    x = h(units)
+    for s in range(S):
+        assert (x[s, k] == oracle.xor_encode(list(x[s, :k]))).all()
+        assert (x[s, k + 1] == 0).all()
+
+
+def test_byte_array_forms_take_strided_inputs_and_reject_bad_outputs():
+    """byte[]-style arrays -- a strided input view is copied into one contiguous run before its address
+    goes to the library; an output the library cannot write in place (strided, wrong dtype, immutable) is
+    rejected instead of written past its elements."""
+    k, p, n = 6, 3, 4096
+    d = cells(SEED, 710000, k, n)
+    wide = [np.zeros(2 * n, np.uint8) for _ in range(k)]
+    for w, x in zip(wide, d):
+        w[::2] = x
+    e = enc("rs", k, p)
+    out = [np.zeros(n, np.uint8) for _ in range(p)]
+    e.encode([w[::2] for w in wide], out)
+    assert all((a == b).all() for a, b in zip(out, oracle.rs_encode(k, p, d)))
+    e.encode([bytes(x) for x in d], out)  # immutable inputs are fine
+    for bad in ([np.zeros(2 * n, np.uint8)[::2]] + out[1:], [bytes(n)] + out[1:], [np.zeros(n, np.int8)] + out[1:]):
+        with pytest.raises(rc.IllegalArgumentException):
+            e.encode(d, bad)
+    with pytest.raises(rc.IllegalArgumentException):
+        e.encode([np.zeros(n, np.uint16)] + d[1:], out)
+    dd = dec("rs", k, p)
+    units = d + oracle.rs_encode(k, p, d)
+    ins = [None if u in (0, 7) else units[u] for u in range(k + p)]
+    o2 = [np.zeros(n, np.uint8) for _ in range(2)]
+    dd.decode(ins, [0, 7], o2)
+    assert (o2[0] == units[0]).all() and (o2[1] == units[7]).all()
+    with pytest.raises(rc.IllegalArgumentException):
+        dd.decode(ins, [0, 7], [np.zeros(2 * n, np.uint8)[::2], o2[1]])

@@ -1,12 +1,15 @@
 """Host-side mirror of the reference API on CPU (no GPU call): java.nio buffer semantics the coders rely on,
 ECChunk, ChecksumData matching rules (ChecksumData.java:118-150), Checksum NONE/SHA256/MD5 delegation."""
 import hashlib
+import os
 
 import numpy as np
 import pytest
 
 from ozone_amd import ByteBuffer, ECChunk
 from ozone_amd import checksum as ck
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_bytebuffer_wrap_slice_positions():
@@ -68,3 +71,39 @@ def test_checksum_none_and_digests_on_host():
 
 def test_checksum_empty_needs_no_device():
     assert ck.Checksum(ck.ChecksumType.CRC32C, 16384).compute_checksum(b"").get_checksums() == []
+
+
+def test_byte_array_normalisation_rules():
+    """inputs are made one contiguous uint8 run, outputs must already be one (no silent overrun)."""
+    import numpy as np
+    from ozone_amd import rawcoder as rc
+    from ozone_amd.bytebuffer import ByteBuffer
+    a = np.arange(64, dtype=np.uint8)
+    v = rc._in_array(a[::2])
+    assert v.flags.c_contiguous and (v == a[::2]).all()
+    assert rc._in_array(b"abc").tobytes() == b"abc"
+    for bad in (a.astype(np.uint16), a.reshape(8, 8)):
+        with pytest.raises(rc.IllegalArgumentException):
+            rc._in_array(bad)
+    assert rc._out_array(a) is a
+    ro = a.copy()
+    ro.flags.writeable = False
+    for bad in (a[::2], b"abc", ro, a.astype(np.int8)):
+        with pytest.raises(rc.IllegalArgumentException):
+            rc._out_array(bad)
+    with pytest.raises(TypeError):
+        ByteBuffer.wrap(a[::2])
+    assert ByteBuffer.wrap(a, 3, 5).remaining() == 5
+
+
+def test_cpu_baseline_harness_self_checks_and_runs():
+    """bench.py's CPU baseline: the fast CRCs are checked against the oracle's CrcIntTable restatement at start-up,
+    then a bounded sample runs (one thread, 0.2 s)."""
+    import json
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "cpu_baseline")
+    for w in ("c2", "crc", "c5", "c3r", "c4", "verify"):
+        out = subprocess.run([exe, w, "1", "0.2"], capture_output=True, text=True, timeout=60)
+        assert out.returncode == 0, out.stderr
+        r = json.loads(out.stdout)
+        assert r["units"] > 0 and r["GBps"] > 0

@@ -182,3 +182,85 @@ def test_queue_close_with_unlaunched_batch_drains():
         par = [np.zeros(n, np.uint8) for _ in range(p)]
         q2.wait(q2.submit(d, par))
     assert all((a == b).all() for a, b in zip(par, oracle.rs_encode(k, p, d)))
+
+
+@pytest.mark.parametrize("batches", [2, 3])
+def test_queue_completes_oldest_on_wrap(batches):
+    """When the ring wraps, submit() completes the OLDEST in-flight batch and refills it; every other batch stays
+    in flight (the rotation used to skip the oldest batch and complete the next one)."""
+    from ozone_amd import _lib
+    k, p, n, S = 6, 3, 1 << 14, 2
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    assert _lib.lib().ozec_set_tuning(b"queue_batches", batches) == 0
+    try:
+        jobs = []
+        with StripeQueue(enc, n, S) as q:
+            for s in range(S * batches):  # fill every batch of the ring: all in flight
+                d = cells(SEED, 95000 + 10 * s, k, n)
+                par = [np.zeros(n, np.uint8) for _ in range(p)]
+                jobs.append((q.submit(d, par), d, par))
+            assert q.state() == (batches, 0, 0)
+            for wrap in range(2 * batches):  # each wrap completes exactly the oldest batch
+                s = S * batches + wrap * S
+                d = cells(SEED, 95000 + 10 * s, k, n)
+                par = [np.zeros(n, np.uint8) for _ in range(p)]
+                jobs.append((q.submit(d, par), d, par))
+                n_in, oldest, filling = q.state()
+                assert (n_in, oldest, filling) == (batches - 1, S * (wrap + 1), 1), (wrap, q.state())
+                # the completed batch's callers already hold their parity
+                for t, dd, pp in jobs[S * wrap:S * (wrap + 1)]:
+                    ref = oracle.rs_encode(k, p, dd)
+                    assert all((a == b).all() for a, b in zip(pp, ref)), t
+                for _ in range(S - 1):  # fill the rest of the refilled batch: it launches
+                    s = len(jobs)
+                    d = cells(SEED, 95000 + 10 * s, k, n)
+                    par = [np.zeros(n, np.uint8) for _ in range(p)]
+                    jobs.append((q.submit(d, par), d, par))
+                assert q.state()[0] == batches
+            q.wait(jobs[-1][0])
+    finally:
+        _lib.lib().ozec_set_tuning(b"queue_batches", 0)
+    for t, d, par in jobs:
+        assert all((a == b).all() for a, b in zip(par, oracle.rs_encode(k, p, d))), t
+
+
+def test_queue_close_completes_pending_stripes():
+    """Stripes submitted but never waited for get their parity and CRCs when the queue is closed (ozec.h)."""
+    k, p, n, bpc = 6, 3, 1 << 15, 8192
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    keep, jobs = [], []
+    q = StripeQueue(enc, n, 4, ChecksumType.CRC32C, bpc)
+    for s in range(10):  # two launched batches + a filling one
+        d = _stripe(96000 + 10 * s, k, n, s % 2 == 0, keep)
+        par = _parity(p, n, s % 3 == 0, keep)
+        crcs = np.zeros((k + p) * (n // bpc), np.uint32)
+        jobs.append((q.submit(d, par, crcs=crcs), d, par, crcs))
+    q.close()
+    for t, d, par, crcs in jobs:
+        ref = oracle.rs_encode(k, p, d)
+        assert all((a == b).all() for a, b in zip(par, ref)), t
+        exp = np.concatenate([oracle.crc_windows(oracle.CRC32C, u, bpc) for u in list(d) + ref])
+        assert (crcs == exp).all(), t
+
+
+def test_queue_rejects_buffers_it_cannot_dma():
+    """crcs / data / parity are checked for dtype, contiguity and size before native code sees them."""
+    k, p, n, bpc = 6, 3, 1 << 14, 4096
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    d = cells(SEED, 97000, k, n)
+    par = [np.zeros(n, np.uint8) for _ in range(p)]
+    with StripeQueue(enc, n, 2, ChecksumType.CRC32C, bpc) as q:
+        with pytest.raises(rc.IllegalArgumentException):  # too few CRC slots
+            q.submit(d, par, crcs=np.zeros((k + p) * (n // bpc) - 1, np.uint32))
+        with pytest.raises(rc.IllegalArgumentException):  # wrong dtype
+            q.submit(d, par, crcs=np.zeros((k + p) * (n // bpc), np.uint8))
+        with pytest.raises(rc.IllegalArgumentException):  # strided data cell
+            q.submit([np.zeros(2 * n, np.uint8)[::2]] + d[1:], par)
+        with pytest.raises(rc.IllegalArgumentException):  # read-only parity
+            ro = np.zeros(n, np.uint8)
+            ro.flags.writeable = False
+            q.submit(d, [ro] + par[1:])
+        crcs = np.zeros((k + p) * (n // bpc), np.uint32)
+        q.wait(q.submit(d, par, crcs=crcs))
+    ref = oracle.rs_encode(k, p, d)
+    assert all((a == b).all() for a, b in zip(par, ref))

@@ -125,7 +125,7 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
 /* End-to-end fused encode (+ CRC) of stripes held in HOST memory (BASELINE configs[4] / SURVEY §8(d) C5: the
  * stripe batch a writer or datanode holds, one contiguous stripe range per GPU, §8(e)).  Same layouts and
  * semantics as ozec_encode_crc_batch with host pointers; checksum_type OZEC_CHECKSUM_NONE encodes only (h_crcs
- * may then be NULL).  Chunks of stripes_per_chunk stripes (0 = 16) are pipelined on the calling thread's device:
+ * may then be NULL).  Chunks of stripes_per_chunk stripes (0 = 32, tuning knob "e2e_chunk") are pipelined on the calling thread's device:
  * the H2D copies of chunk c+1, the kernel of chunk c and the D2H copies of chunk c-1 run at once on three streams.
  * Registered / pinned buffers (ozec_host_register, ozec_host_alloc) are DMA'd in place; pageable ones are staged
  * through NUMA-local pinned memory.  Synchronous: returns when parity and CRCs are in the caller's buffers. */

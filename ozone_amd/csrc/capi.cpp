@@ -91,7 +91,7 @@ struct Slot {
 // its kernel and its D2H copies go on three streams ordered by events, so the two copy directions and the
 // kernel of consecutive chunks run at once.  One call at a time per device (mu).
 struct E2E {
-  static constexpr int NB = 3;
+  static constexpr int NB = 4;
   std::mutex mu;
   hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
   hipEvent_t h2d_done[NB] = {}, comp_done[NB] = {}, d2h_done[NB] = {};
@@ -843,7 +843,8 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
   E2E &P = ctx->e2e;
   std::lock_guard<std::mutex> lk(P.mu);
   const int k = enc->k, p = enc->p, rows = out_rows(enc), units = k + rows;
-  const size_t C = std::min(num_stripes, stripes_per_chunk ? stripes_per_chunk : size_t{16});
+  const size_t C = std::min(num_stripes, stripes_per_chunk ? stripes_per_chunk
+                                                          : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk)));
   const size_t nwin = with_crc ? (len + bpc - 1) / bpc : 0;
   const size_t dstripe = static_cast<size_t>(k + p) * len;               // device layout [C][k+p][len]
   const size_t dcrc_off = round_up(C * dstripe, kStageAlign);            // then crcs [C][units][nwin]
@@ -930,13 +931,26 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
         ozec::parallel_copy(tasks);
       }
     }
-    // H2D after the chunk that used this buffer NB chunks ago has left the device
-    if (c >= static_cast<size_t>(E2E::NB)) OZEC_HIP(hipStreamWaitEvent(P.h2d, P.d2h_done[b], 0));
+    // H2D after the chunk that used this buffer NB chunks ago has left the device.  The host waits for it too
+    // (staged calls already did, in unstage): the HIP queues then never hold more than NB chunks of commands.
+    // Enqueuing a whole 8192-stripe batch up front (~40 commands per chunk) measured 27 GB/s at 16-stripe chunks
+    // against 49 GB/s for the same chunks of a 1024-stripe batch; with the wait, 45-48 GB/s at every size, and
+    // 56 GB/s (98 % of the 57.5 GB/s H2D link) with one rectangular copy per chunk and direction
+    // (scripts/e2e_probe2.py, profiles/r02/e2e_probe.log).
+    if (c >= static_cast<size_t>(E2E::NB)) {
+      if (!staged) OZEC_HIP(hipEventSynchronize(P.d2h_done[b]));
+      OZEC_HIP(hipStreamWaitEvent(P.h2d, P.d2h_done[b], 0));
+    }
+    const bool rect = ozec::g_tune.e2e_rect != 0;
     if (!in_pinned) {
       // staged cells are already in the device layout: one copy of the data cells per stripe
       for (size_t i = 0; i < cs; ++i)
         OZEC_HIP(hipMemcpyAsync(d + i * dstripe, P.hstage[b] + i * dstripe, static_cast<size_t>(k) * len,
                                 hipMemcpyHostToDevice, P.h2d));
+    } else if (in_unit_stride == static_cast<int64_t>(len) && rect) {
+      // one rectangular copy per chunk: cs rows of k*len bytes, source pitch = the batch's stripe stride
+      OZEC_HIP(hipMemcpy2DAsync(d, dstripe, h_in + s0 * in_stripe_stride, static_cast<size_t>(in_stripe_stride),
+                                static_cast<size_t>(k) * len, cs, hipMemcpyHostToDevice, P.h2d));
     } else if (in_unit_stride == static_cast<int64_t>(len)) {
       for (size_t i = 0; i < cs; ++i)  // the k data cells of a stripe are one run
         OZEC_HIP(hipMemcpyAsync(d + i * dstripe, h_in + (s0 + i) * in_stripe_stride, static_cast<size_t>(k) * len,
@@ -963,7 +977,11 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
     OZEC_HIP(hipEventRecord(P.comp_done[b], P.comp));
     OZEC_HIP(hipStreamWaitEvent(P.d2h, P.comp_done[b], 0));
     uint8_t *hs = staged ? P.hstage[b] : nullptr;
-    for (size_t i = 0; i < cs; ++i) {
+    if (out_pinned && out_unit_stride == static_cast<int64_t>(len) && rect) {
+      OZEC_HIP(hipMemcpy2DAsync(h_out + s0 * out_stripe_stride, static_cast<size_t>(out_stripe_stride),
+                                d + static_cast<size_t>(k) * len, dstripe, static_cast<size_t>(p) * len, cs,
+                                hipMemcpyDeviceToHost, P.d2h));
+    } else for (size_t i = 0; i < cs; ++i) {
       uint8_t *src = d + i * dstripe + static_cast<size_t>(k) * len;
       if (!out_pinned) {
         OZEC_HIP(hipMemcpyAsync(hs + i * dstripe + static_cast<size_t>(k) * len, src, static_cast<size_t>(p) * len,
@@ -1184,6 +1202,8 @@ int ozec_set_tuning(const char *key, int64_t value) {
   else if (k == "host_slots" && value > 0) ozec::g_tune.host_slots = value;
   else if (k == "queue_batches" && value >= 0 && value <= 64) ozec::g_tune.queue_batches = value;
   else if (k == "copy_threads" && value >= 0) ozec::set_copy_threads(static_cast<int>(value));
+  else if (k == "e2e_chunk" && value > 0) ozec::g_tune.e2e_chunk = value;
+  else if (k == "e2e_rect") ozec::g_tune.e2e_rect = static_cast<int>(value);
   else return fail(OZEC_EINVAL, "unknown tuning key " + k);
   return OZEC_OK;
 }

@@ -108,8 +108,10 @@ __device__ __forceinline__ uint32_t perm_vv(uint32_t hi, uint32_t lo, uint32_t s
 // while hipcc inserts no wait states for this case.  Call right after the store(s): the data registers stay
 // allocated until two wait states after the store, so the next writer of those VGPRs cannot come sooner.
 __device__ __forceinline__ void store_data_hold(const uint4 &v) {
+#ifndef OZEC_NO_STORE_HOLD  // defined only to show tests/isa_scan.py the unguarded ISA
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 1" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+#endif
 }
 
 // gfx950 3-input bitwise op; truth table 0x96 = a ^ b ^ c

@@ -114,6 +114,8 @@ struct TuneKnobs {
   int64_t host_chunk = 256 << 10;  // host-buffer calls: bytes per unit per pipelined chunk
   int64_t host_slots = 8;          // host-buffer calls: staging slots (concurrent calls) per GPU
   int64_t queue_batches = 0;       // stripe queue: batches in the ring (0 = default), read at queue creation
+  int64_t e2e_chunk = 32;          // ozec_encode_crc_host_batch: stripes per pipelined chunk when the caller passes 0
+  int e2e_rect = 1;                // ozec_encode_crc_host_batch: one rectangular copy per chunk (0: one per stripe)
 };
 extern TuneKnobs g_tune;
 

@@ -297,11 +297,8 @@ class Workload:
                            "layout": "block-major: [group][unit][256 MiB block], unit stride 256 MiB"}
             us = B * n
 
-            def step():
-                for g in range(G):
-                    base = self.blocks[g]
-                    enc.encode_crc_batch(base, n, us, base[k:], n, us, B, n, self.crc_type, self.bpc, self.crcs[g])
-            self._step = step
+            self._step = lambda: enc.encode_crc_block_groups(self.blocks, units * us, us, G, B, n, self.crc_type,
+                                                             self.bpc, self.crcs)
             torch.cuda.synchronize()
             return
         # HBM layout: stripe-major, units contiguous: unit u of stripe s at s*(k+p)*n + u*n
@@ -853,16 +850,11 @@ def main():
                      "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4), "kernel_ms_reduction": "max over ranks",
                      "alg_bytes_per_launch": wl.alg_bytes, "numa_node": numa_node},
     }
-    if args.workload in ("host", "queue", "queue_pageable", "c4"):
-        if args.workload == "c4":
-            result["roofline"]["note"] = "one step = 16 launches (one per block group): kernel_ms covers all 16"
-            result["roofline"]["alg_bytes_per_launch"] = wl.alg_bytes // 16
-            result["roofline"]["launches_per_step"] = 16
-        else:
-            pc = pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
-            pc["value_frac_of_duplex_h2d"] = round(value / world / pc["duplex_h2d_GBps"], 4)
-            result["pcie"] = pc
-            result["roofline"]["note"] = "kernel_ms is the whole PCIe-inclusive step; the bound is the link, not HBM"
+    if args.workload in ("host", "queue", "queue_pageable"):
+        pc = pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
+        pc["value_frac_of_duplex_h2d"] = round(value / world / pc["duplex_h2d_GBps"], 4)
+        result["pcie"] = pc
+        result["roofline"]["note"] = "kernel_ms is the whole PCIe-inclusive step; the bound is the link, not HBM"
     wl.free()
     del wl
     if args.workload == "c2" and not args.no_e2e:

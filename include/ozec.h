@@ -122,6 +122,15 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
                           int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
                           size_t bytes_per_checksum, uint32_t *d_crcs, int big_endian, void *stream);
 
+/* Fused encode + CRC over the datanode's block-group layout (BASELINE configs[3] / SURVEY §8(d) C4: one block
+ * file per unit, 256 MiB blocks): unit u of stripe t of block group g at
+ *   d_base + g * group_stride + u * unit_stride + t * len          (u < k: data blocks, k <= u < k+p: parity blocks)
+ * All groups go in ONE launch (stripe g*stripes_per_group + t).  CRCs: d_crcs[g][t][unit][window] as in
+ * ozec_encode_crc_batch (units = k data + the coded parity rows). */
+int ozec_encode_crc_block_groups(ozec_coder *enc, uint8_t *d_base, int64_t group_stride, int64_t unit_stride,
+                                 size_t num_groups, size_t stripes_per_group, size_t len, int checksum_type,
+                                 size_t bytes_per_checksum, uint32_t *d_crcs, int big_endian, void *stream);
+
 /* End-to-end fused encode (+ CRC) of stripes held in HOST memory (BASELINE configs[4] / SURVEY §8(d) C5: the
  * stripe batch a writer or datanode holds, one contiguous stripe range per GPU, §8(e)).  Same layouts and
  * semantics as ozec_encode_crc_batch with host pointers; checksum_type OZEC_CHECKSUM_NONE encodes only (h_crcs

@@ -99,6 +99,8 @@ _SIGS = {
     "ozec_host_page_node": (ctypes.c_int, [c_voidp, c_intp]),
     "ozec_host_register": (ctypes.c_int, [c_voidp, c_size, ctypes.c_int]),
     "ozec_host_unregister": (ctypes.c_int, [c_voidp]),
+    "ozec_encode_crc_block_groups": (ctypes.c_int, [c_voidp, c_voidp, c_i64, c_i64, c_size, c_size, c_size,
+                                                    ctypes.c_int, c_size, c_voidp, ctypes.c_int, c_voidp]),
     "ozec_encode_crc_host_batch": (ctypes.c_int, [c_voidp, c_voidp, c_i64, c_i64, c_voidp, c_i64, c_i64, c_size,
                                                   c_size, ctypes.c_int, c_size, c_voidp, ctypes.c_int, c_size]),
     "ozec_stripe_queue_state": (ctypes.c_int, [c_voidp, ctypes.POINTER(c_size), ctypes.POINTER(ctypes.c_uint64),

@@ -804,6 +804,59 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
   return OZEC_OK;
 }
 
+int ozec_encode_crc_block_groups(ozec_coder *enc, uint8_t *d_base, int64_t group_stride, int64_t unit_stride,
+                                 size_t num_groups, size_t stripes_per_group, size_t len, int checksum_type, size_t bpc,
+                                 uint32_t *d_crcs, int big_endian, void *stream) {
+  if (int rc = check_open(enc, "encode")) return rc;
+  if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
+  if (len == 0 || num_groups == 0 || stripes_per_group == 0) return OZEC_OK;
+  if (!d_base || !d_crcs) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  if (stripes_per_group > static_cast<size_t>(INT32_MAX) || num_groups * stripes_per_group > static_cast<size_t>(INT32_MAX))
+    return fail(OZEC_EINVAL, "too many stripes for one call");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  const int k = enc->k, rows = out_rows(enc), units = k + rows;
+  const int64_t L = static_cast<int64_t>(len);
+  uint8_t *d_par = d_base + static_cast<int64_t>(k) * unit_stride;
+  const int64_t nwin = static_cast<int64_t>((len + (bpc ? bpc : 1) - 1) / (bpc ? bpc : 1));
+  ozec::EncCrcArgs e{};
+  CodeArgs &a = e.code;
+  a.in = d_base;
+  a.out = d_par;
+  a.in_stripe_stride = L;  // cells of one block are back to back
+  a.out_stripe_stride = L;
+  a.grp_stripes = static_cast<int64_t>(stripes_per_group);
+  a.in_grp_stride = group_stride;
+  a.out_grp_stride = group_stride;
+  a.nstripes = static_cast<int64_t>(num_groups * stripes_per_group);
+  a.len = L;
+  std::vector<uint8_t> coef;
+  encode_rows(enc, coef);
+  fill_coef(a, rows, k, coef.data());
+  for (int j = 0; j < k; ++j) a.in_off[j] = j * unit_stride;
+  for (int r = 0; r < rows; ++r) a.out_off[r] = r * unit_stride;
+  if (int rc = make_crc_args(ctx, checksum_type, nullptr, 0, a.nstripes, len, bpc, d_crcs, nwin, big_endian, 0, &e.crc))
+    return rc;
+  if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
+    OZEC_HIP(ozec::launch_encode_crc(e, st));  // every block group in one launch
+  } else {
+    for (size_t g = 0; g < num_groups; ++g) {  // layouts the fused kernel does not take: one batch per group
+      uint8_t *gb = d_base + static_cast<int64_t>(g) * group_stride;
+      if (int rc = ozec_encode_crc_batch(enc, gb, L, unit_stride, gb + static_cast<int64_t>(k) * unit_stride, L,
+                                         unit_stride, stripes_per_group, len, checksum_type, bpc,
+                                         d_crcs + g * stripes_per_group * units * nwin, big_endian, st))
+        return rc;
+    }
+    return OZEC_OK;
+  }
+  for (int r = rows; r < enc->p; ++r)  // XOR with p > 1: outputs past the first are reset (XORRawEncoder.java:67-85)
+    for (size_t g = 0; g < num_groups; ++g)
+      OZEC_HIP(hipMemsetAsync(d_par + static_cast<int64_t>(g) * group_stride + r * unit_stride, 0,
+                              stripes_per_group * len, st));
+  return OZEC_OK;
+}
+
 // ---- end-to-end batch from host memory ----------------------------------------
 
 namespace {

@@ -114,6 +114,20 @@ __device__ __forceinline__ void store_data_hold(const uint4 &v) {
 #endif
 }
 
+// Byte offset of stripe s: s * stripe_stride, or in the block-group layout (grp_stripes > 0, one block file per
+// unit) group s / grp_stripes at grp_stride, stripe s % grp_stripes within it.  s is wave-uniform (SALU).
+__device__ __forceinline__ int64_t grouped_off(int64_t s, int64_t stride, int64_t gs, int64_t gstride) {
+  if (gs <= 0) return s * stride;
+  const uint32_t g = static_cast<uint32_t>(s) / static_cast<uint32_t>(gs);
+  return static_cast<int64_t>(g) * gstride + (s - static_cast<int64_t>(g) * gs) * stride;
+}
+__device__ __forceinline__ int64_t in_off(const CodeArgs &a, int64_t s) {
+  return grouped_off(s, a.in_stripe_stride, a.grp_stripes, a.in_grp_stride);
+}
+__device__ __forceinline__ int64_t out_off(const CodeArgs &a, int64_t s) {
+  return grouped_off(s, a.out_stripe_stride, a.grp_stripes, a.out_grp_stride);
+}
+
 // gfx950 3-input bitwise op; truth table 0x96 = a ^ b ^ c
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t d;
@@ -215,8 +229,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
     const uint32_t s = u / cpc;
     const uint32_t c = u - s * cpc;
     const uint32_t v0 = c * kChunk + threadIdx.x;
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + static_cast<int64_t>(s) * a.in_stripe_stride);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + static_cast<int64_t>(s) * a.out_stripe_stride);
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, s));
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s));
     uint4 x[VPT][K];
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
@@ -288,8 +302,8 @@ __global__ __launch_bounds__(kBlock) void gf_code_vec_generic(const CodeArgs a, 
     const uint32_t s = u / cpc;
     const uint32_t v = (u - s * cpc) * kBlock + threadIdx.x;
     if (v >= nvec) continue;
-    const uint8_t *ib = a.in + static_cast<int64_t>(s) * a.in_stripe_stride + static_cast<int64_t>(v) * 16;
-    uint8_t *ob = a.out + static_cast<int64_t>(s) * a.out_stripe_stride + static_cast<int64_t>(v) * 16;
+    const uint8_t *ib = a.in + in_off(a, s) + static_cast<int64_t>(v) * 16;
+    uint8_t *ob = a.out + out_off(a, s) + static_cast<int64_t>(v) * 16;
     uint4 acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
@@ -323,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void xor_vec(const CodeArgs a) {
     const uint32_t s = u / cpc;
     const uint32_t v = (u - s * cpc) * kBlock + threadIdx.x;
     if (v >= nvec) continue;
-    const uint8_t *ib = a.in + static_cast<int64_t>(s) * a.in_stripe_stride + static_cast<int64_t>(v) * 16;
+    const uint8_t *ib = a.in + in_off(a, s) + static_cast<int64_t>(v) * 16;
     uint4 acc = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < (K > 0 ? K : OZEC_MAX_K); ++j) {
@@ -334,7 +348,7 @@ __global__ __launch_bounds__(kBlock) void xor_vec(const CodeArgs a) {
       acc.z ^= x.z;
       acc.w ^= x.w;
     }
-    *reinterpret_cast<uint4 *>(a.out + static_cast<int64_t>(s) * a.out_stripe_stride + a.out_off[0] +
+    *reinterpret_cast<uint4 *>(a.out + out_off(a, s) + a.out_off[0] +
                                static_cast<int64_t>(v) * 16) = acc;
   }
 }
@@ -351,8 +365,8 @@ __global__ __launch_bounds__(kBlock) void gf_code_bytes(const CodeArgs a, int64_
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int64_t s = i / span;
     const int64_t x = start + (i - s * span);
-    const uint8_t *ib = a.in + s * a.in_stripe_stride + x;
-    uint8_t *ob = a.out + s * a.out_stripe_stride + x;
+    const uint8_t *ib = a.in + in_off(a, s) + x;
+    uint8_t *ob = a.out + out_off(a, s) + x;
     for (int r = 0; r < rows; ++r) {
       uint32_t acc = 0;
       for (int j = 0; j < k; ++j) {
@@ -805,8 +819,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     const int64_t m = N >> 4;
     const int64_t T = (m + 64 * B - 1) / (64 * B);
     const int64_t P = T * 64 * B - m;
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + s * a.in_stripe_stride + w * cr.bpc);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + s * a.out_stripe_stride + w * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, s) + w * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
     uint32_t S[K + R];
 #pragma unroll
     for (int q = 0; q < K + R; ++q) S[q] = 0;
@@ -962,8 +976,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     const int64_t m = N >> 4;
     const int32_t G = static_cast<int32_t>((m + 64 * D - 1) / (64 * D));
     const int32_t P = G * 64 * D - static_cast<int32_t>(m);  // window <= 2 GiB: 32-bit block indices
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + s * a.in_stripe_stride + w * cr.bpc);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + s * a.out_stripe_stride + w * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, s) + w * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
     uint32_t S[K + R];
 #pragma unroll
     for (int q = 0; q < K + R; ++q) S[q] = 0;
@@ -1115,7 +1129,7 @@ __global__ __launch_bounds__(kBlock) void encode_xor_crc_g26s(const EncCrcArgs e
   // load cursor (wave-uniform): unit lu = (stripe ls, window lw), step lt
   int64_t lu = u0, ls = u0 / nwin, lw = u0 - ls * nwin;
   int32_t lt = 0;
-  __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + ls * a.in_stripe_stride + lw * cr.bpc);
+  __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, ls) + lw * cr.bpc);
   auto load_next = [&](uint4 (&dst)[K]) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -1131,7 +1145,7 @@ __global__ __launch_bounds__(kBlock) void encode_xor_crc_g26s(const EncCrcArgs e
         lw = 0;
         ++ls;
       }
-      rin = make_rsrc(a.in + ls * a.in_stripe_stride + lw * cr.bpc);
+      rin = make_rsrc(a.in + in_off(a, ls) + lw * cr.bpc);
     }
   };
   uint4 x[NS][K];
@@ -1139,7 +1153,7 @@ __global__ __launch_bounds__(kBlock) void encode_xor_crc_g26s(const EncCrcArgs e
   for (int i = 0; i + 1 < NS; ++i) load_next(x[i]);
   int64_t cs = u0 / nwin, cw = u0 - cs * nwin;  // compute cursor
   for (int64_t u = u0; u < u1; ++u) {
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + cs * a.out_stripe_stride + cw * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, cs) + cw * cr.bpc);
     uint32_t S[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) S[j] = 0;
@@ -1287,6 +1301,7 @@ inline bool aligned16(int64_t v) { return (v & 15) == 0; }
 bool vec_ok(const CodeArgs &a) {
   if (!aligned16(reinterpret_cast<intptr_t>(a.in)) || !aligned16(reinterpret_cast<intptr_t>(a.out))) return false;
   if (a.nstripes > 1 && (!aligned16(a.in_stripe_stride) || !aligned16(a.out_stripe_stride))) return false;
+  if (a.grp_stripes > 0 && (!aligned16(a.in_grp_stride) || !aligned16(a.out_grp_stride))) return false;
   for (int j = 0; j < a.k; ++j)
     if (!aligned16(a.in_off[j])) return false;
   for (int r = 0; r < a.rows; ++r)

@@ -26,6 +26,11 @@ struct CodeArgs {
   int64_t in_off[OZEC_MAX_K];
   int64_t out_off[OZEC_MAX_ROWS];
   uint8_t coef[OZEC_MAX_ROWS * OZEC_MAX_K];  // row-major rows x k
+  // block-group layout (0 = flat): stripe s lives in group s / grp_stripes at g * {in,out}_grp_stride, at
+  // (s % grp_stripes) * {in,out}_stripe_stride within it (ozec_encode_crc_block_groups)
+  int64_t grp_stripes;
+  int64_t in_grp_stride;
+  int64_t out_grp_stride;
 };
 
 // Per-window CRC job over equally sized cells: cell c at base + c * cell_stride, `len` bytes each.

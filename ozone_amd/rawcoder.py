@@ -299,6 +299,16 @@ class RawErasureEncoder(_Coder):
             _raise_for(rc)
 
 
+    def encode_crc_block_groups(self, d_base, group_stride, unit_stride, num_groups, stripes_per_group, length,
+                                checksum_type, bytes_per_checksum, d_crcs, big_endian=False, stream=None):
+        """Fused encode + CRC over block groups (one block per unit; ozec_encode_crc_block_groups): unit u of stripe
+        t of group g at d_base + g*group_stride + u*unit_stride + t*length; CRCs [g][t][unit][window]."""
+        rc_ = L.lib().ozec_encode_crc_block_groups(self._handle, _dev_ptr(d_base), group_stride, unit_stride, num_groups,
+                                                   stripes_per_group, length, int(checksum_type), bytes_per_checksum,
+                                                   _dev_ptr(d_crcs), 1 if big_endian else 0, _stream_ptr(stream))
+        if rc_ != L.OZEC_OK:
+            _raise_for(rc_)
+
     def encode_crc_host_batch(self, h_in, in_stripe_stride, in_unit_stride, h_out, out_stripe_stride,
                               out_unit_stride, num_stripes, length, checksum_type, bytes_per_checksum, h_crcs=None,
                               big_endian=False, stripes_per_chunk=0):

@@ -585,8 +585,7 @@ def test_full_size_c4_block_major_256mib_blocks():
     blocks[:, 2].fill_(0x5A)
     crcs = torch.zeros((G, B, 3, nwin), dtype=torch.int32, device=DEV)
     e = enc("xor", 2, 1)
-    for g in range(G):
-        e.encode_crc_batch(blocks[g], n, B * n, blocks[g, 2:], n, B * n, B, n, ck.ChecksumType.CRC32C, bpc, crcs[g])
+    e.encode_crc_block_groups(blocks, 3 * B * n, B * n, G, B, n, ck.ChecksumType.CRC32C, bpc, crcs)  # one launch
     assert torch.equal(blocks[:, 2], torch.bitwise_xor(blocks[:, 0], blocks[:, 1]))
     ref = torch.zeros((G, 3, B, nwin), dtype=torch.int32, device=DEV)
     ck.checksum_windows_batch(ck.ChecksumType.CRC32C, blocks, n, G * 3 * B, n, bpc, ref)  # cells in block order
@@ -712,3 +711,40 @@ def test_byte_array_forms_take_strided_inputs_and_reject_bad_outputs():
     assert (o2[0] == units[0]).all() and (o2[1] == units[7]).all()
     with pytest.raises(rc.IllegalArgumentException):
         dd.decode(ins, [0, 7], [np.zeros(2 * n, np.uint8)[::2], o2[1]])
+
+
+@pytest.mark.parametrize("codec,k,p,n,B,G,bpc", [
+    ("rs", 6, 3, 1 << 16, 5, 3, 16384),    # fused kernel, one launch over 3 groups
+    ("rs", 10, 4, 1 << 15, 3, 2, 4096),
+    ("xor", 2, 1, 1 << 16, 7, 4, 8192),
+    ("xor", 3, 2, 1 << 15, 4, 3, 4096),    # XOR p > 1: the second parity block is reset
+    ("rs", 6, 3, 50000, 3, 2, 1000),       # len % 16 != 0: per-group unfused fallback
+])
+def test_encode_crc_block_groups_vs_oracle(codec, k, p, n, B, G, bpc):
+    """Block-group layout (one block per unit) against the oracle: unit u of stripe t of group g at
+    g*group_stride + u*unit_stride + t*n, with a gap between groups."""
+    us = B * n
+    gs = (k + p) * us + 4096
+    raw = np.full(G * gs, 0xA5, np.uint8)
+    cellsd = {}
+    for g in range(G):
+        for t_ in range(B):
+            for u, x in enumerate(cells(SEED, 720000 + (g * B + t_) * k, k, n)):
+                raw[g * gs + u * us + t_ * n:g * gs + u * us + (t_ + 1) * n] = x
+                cellsd[(g, t_, u)] = x
+    d = t(raw)
+    units = k + (1 if codec == "xor" else p)
+    nwin = (n + bpc - 1) // bpc
+    crcs = torch.zeros((G, B, units, nwin), dtype=torch.int32, device=DEV)
+    enc(codec, k, p).encode_crc_block_groups(d, gs, us, G, B, n, ck.ChecksumType.CRC32C, bpc, crcs)
+    out, c = h(d), h(crcs).view(np.uint32)
+    for g in range(G):
+        for t_ in range(B):
+            data = [cellsd[(g, t_, u)] for u in range(k)]
+            ref = oracle.rs_encode(k, p, data) if codec == "rs" else [oracle.xor_encode(data)] + [np.zeros(n, np.uint8)] * (p - 1)
+            for r in range(p):
+                got = out[g * gs + (k + r) * us + t_ * n:g * gs + (k + r) * us + (t_ + 1) * n]
+                assert (got == ref[r]).all(), (g, t_, r)
+            for u, cell in enumerate(data + ref[:units - k]):
+                assert (c[g, t_, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (g, t_, u)
+        assert (out[g * gs + (k + p) * us:(g + 1) * gs] == 0xA5).all()  # the gap is untouched

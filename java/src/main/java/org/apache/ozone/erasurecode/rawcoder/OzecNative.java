@@ -1,0 +1,99 @@
+package org.apache.ozone.erasurecode.rawcoder;
+
+import java.nio.ByteBuffer;
+
+/**
+ * JNI entry points of libozec_jni (jni/ozec_jni.c) over the libozec C ABI (include/ozec.h).  Loaded once per
+ * JVM; {@link #checkAvailable()} throws when the library or a GPU is missing, which makes the HIP coder
+ * constructors throw and CodecUtil fall back to the next coder (CodecUtil.java:62-78).
+ * System property {@code ozone.ec.hip.library} may name the library file; otherwise java.library.path is searched.
+ */
+public final class OzecNative {
+  public static final int CODEC_RS = 0;
+  public static final int CODEC_XOR = 1;
+  /** ChecksumType numbers of DatanodeClientProtocol.proto:422-434. */
+  public static final int CHECKSUM_NONE = 1;
+  public static final int CHECKSUM_CRC32 = 2;
+  public static final int CHECKSUM_CRC32C = 3;
+
+  private static final Throwable LOAD_FAILURE;
+
+  static {
+    Throwable failure = null;
+    try {
+      String path = System.getProperty("ozone.ec.hip.library");
+      if (path != null) {
+        System.load(path);
+      } else {
+        System.loadLibrary("ozec_jni");
+      }
+    } catch (Throwable t) {
+      failure = t;
+    }
+    LOAD_FAILURE = failure;
+  }
+
+  private OzecNative() {
+  }
+
+  /** True when the JNI library loaded and at least one GPU is visible. */
+  public static boolean isAvailable() {
+    return LOAD_FAILURE == null && deviceCount() > 0;
+  }
+
+  public static void checkAvailable() {
+    if (LOAD_FAILURE != null) {
+      throw new UnsupportedOperationException("libozec_jni is not loadable", LOAD_FAILURE);
+    }
+    if (deviceCount() <= 0) {
+      throw new UnsupportedOperationException("no HIP device is visible");
+    }
+  }
+
+  public static native int deviceCount();
+
+  // ---- coders (ozec_encoder_create / ozec_decoder_create / ozec_coder_release + ozec_coder_free)
+  static native long coderCreate(boolean decoder, int codec, int numData, int numParity);
+
+  static native void coderRelease(long handle);
+
+  // ---- AbstractNativeRawEncoder.performEncodeImpl / AbstractNativeRawDecoder.performDecodeImpl
+  static native void encodeDirect(long handle, ByteBuffer[] inputs, int[] inputOffsets, int dataLen,
+      ByteBuffer[] outputs, int[] outputOffsets);
+
+  static native void encodeArrays(long handle, byte[][] inputs, int[] inputOffsets, int dataLen,
+      byte[][] outputs, int[] outputOffsets);
+
+  static native void decodeDirect(long handle, ByteBuffer[] inputs, int[] inputOffsets, int dataLen,
+      int[] erasedIndexes, ByteBuffer[] outputs, int[] outputOffsets);
+
+  static native void decodeArrays(long handle, byte[][] inputs, int[] inputOffsets, int dataLen,
+      int[] erasedIndexes, byte[][] outputs, int[] outputOffsets);
+
+  // ---- checksums (ozec_crc_update, ozec_checksum_windows)
+  public static native int crcUpdateDirect(int type, int state, ByteBuffer buffer, int offset, int length);
+
+  public static native int crcUpdateArray(int type, int state, byte[] array, int offset, int length);
+
+  /** Big-endian CRC of every bytesPerChecksum window into out; returns the bytes written (4 per window). */
+  public static native int checksumWindowsDirect(int type, ByteBuffer data, int offset, int length,
+      int bytesPerChecksum, byte[] out);
+
+  public static native int checksumWindowsArray(int type, byte[] data, int offset, int length,
+      int bytesPerChecksum, byte[] out);
+
+  // ---- pinned host memory + stripe queue (ozec_host_alloc, ozec_stripe_queue_*)
+  public static native ByteBuffer allocatePinned(int bytes);
+
+  public static native void freePinned(ByteBuffer buffer);
+
+  static native long queueCreate(long encoder, int cellLen, int stripesPerBatch, int checksumType,
+      int bytesPerChecksum);
+
+  static native long queueSubmit(long queue, ByteBuffer[] data, int[] dataOffsets, ByteBuffer[] parity,
+      int[] parityOffsets, int length, ByteBuffer crcs);
+
+  static native void queueWait(long queue, long ticket);
+
+  static native void queueFree(long queue);
+}

@@ -1,0 +1,395 @@
+/*
+ * ozec_jni.c -- JNI glue of the Java drop-in (java/.../OzecNative.java): resolves Java buffers to addresses and
+ * hands them to the JNI-free marshaling core (ozec_marshal.c), which validates, calls libozec and picks the Java
+ * exception.  Build on a host with a JDK:
+ *   cc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude jni/ozec_jni.c jni/ozec_marshal.c \
+ *      -Lozone_amd/lib -lozec -Wl,-rpath,'$ORIGIN' -o libozec_jni.so
+ * (tests/test_jni_glue.py compiles this same file against a test double of the JNI interface, tests/native/mockjni).
+ *
+ * Reference counterparts (EC/ = hadoop-hdds/erasurecode/src/main/java/org/apache/ozone/erasurecode/):
+ *   encodeDirect / decodeDirect   <- AbstractNativeRawEncoder.doEncode :49-73 / AbstractNativeRawDecoder.doDecode :49-75
+ *                                    -> hadoop's performEncodeImpl / performDecodeImpl (HadoopNativeECAccessorUtil :32-58)
+ *   encodeArrays / decodeArrays   <- doEncode(ByteArrayEncodingState) / doDecode(ByteArrayDecodingState); the reference
+ *                                    copies heap arrays into direct buffers (:75-86), here they are pinned in place
+ *   coderCreate / coderRelease    <- NativeRSRawEncoder ctor / release (EC/rawcoder/NativeRSRawEncoder.java:39-62)
+ *   crcUpdate* / checksumWindows* <- ChecksumByteBuffer.update (CM/ChecksumByteBuffer.java:32-44) and
+ *                                    Checksum.computeChecksum (CM/Checksum.java:157-200)
+ *   queue*                        <- the stripe queue of ECKeyOutputStream (hadoop-ozone/client/.../ECKeyOutputStream.java:501-543)
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../include/ozec.h"
+#include "ozec_marshal.h"
+
+#define JNI_FN(name) Java_org_apache_ozone_erasurecode_rawcoder_OzecNative_##name
+#define MAX_BUFS 256
+
+static void throw_status(JNIEnv *env, const ozm_status *st) {
+  jclass c = (*env)->FindClass(env, st->exception_class);
+  if (!c) { /* e.g. HadoopIllegalArgumentException absent from the class path: its superclass */
+    (*env)->ExceptionClear(env);
+    c = (*env)->FindClass(env, st->code == OZEC_EINVAL ? "java/lang/IllegalArgumentException"
+                                                       : "java/lang/RuntimeException");
+  }
+  if (c) (*env)->ThrowNew(env, c, st->message);
+}
+
+static void throw_rc(JNIEnv *env, int rc) {
+  ozm_status st;
+  ozm_fail(rc, NULL, &st);
+  throw_status(env, &st);
+}
+
+/* Java array of direct ByteBuffers (+ int[] positions) -> ozm_buf[]; null elements stay absent. */
+static int collect_direct(JNIEnv *env, jobjectArray arr, jintArray offs, ozm_buf *bufs, int *n, ozm_status *st) {
+  if (!arr || !offs) return ozm_fail(OZEC_EINVAL, "Invalid buffer array, null", st);
+  const jsize len = (*env)->GetArrayLength(env, arr);
+  if (len > MAX_BUFS || (*env)->GetArrayLength(env, offs) < len)
+    return ozm_fail(OZEC_EINVAL, "Invalid buffer / offset arrays", st);
+  jint o[MAX_BUFS];
+  (*env)->GetIntArrayRegion(env, offs, 0, len, o);
+  for (jsize i = 0; i < len; ++i) {
+    jobject b = (*env)->GetObjectArrayElement(env, arr, i);
+    memset(&bufs[i], 0, sizeof(bufs[i]));
+    if (b) {
+      bufs[i].present = 1;
+      bufs[i].base = (*env)->GetDirectBufferAddress(env, b); /* NULL for a heap buffer: rejected by ozm_resolve */
+      bufs[i].capacity = (int64_t)(*env)->GetDirectBufferCapacity(env, b);
+      bufs[i].offset = o[i];
+      (*env)->DeleteLocalRef(env, b);
+    }
+  }
+  *n = (int)len;
+  return 0;
+}
+
+/* Java byte[][] (+ int[] offsets): references first (JNI calls are not allowed inside a critical region), then
+ * every array pinned with GetPrimitiveArrayCritical; unpin() releases them. */
+typedef struct {
+  jbyteArray arr[MAX_BUFS];
+  int n;
+} pinned_set;
+
+static int collect_arrays(JNIEnv *env, jobjectArray arr, jintArray offs, ozm_buf *bufs, pinned_set *ps,
+                          ozm_status *st) {
+  ps->n = 0;
+  if (!arr || !offs) return ozm_fail(OZEC_EINVAL, "Invalid buffer array, null", st);
+  const jsize len = (*env)->GetArrayLength(env, arr);
+  if (len > MAX_BUFS || (*env)->GetArrayLength(env, offs) < len)
+    return ozm_fail(OZEC_EINVAL, "Invalid buffer / offset arrays", st);
+  jint o[MAX_BUFS];
+  (*env)->GetIntArrayRegion(env, offs, 0, len, o);
+  for (jsize i = 0; i < len; ++i) {
+    ps->arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, arr, i);
+    memset(&bufs[i], 0, sizeof(bufs[i]));
+    if (ps->arr[i]) {
+      bufs[i].present = 1;
+      bufs[i].capacity = (*env)->GetArrayLength(env, ps->arr[i]);
+      bufs[i].offset = o[i];
+    }
+  }
+  ps->n = (int)len;
+  return 0;
+}
+
+static void pin(JNIEnv *env, pinned_set *ps, ozm_buf *bufs) {
+  for (int i = 0; i < ps->n; ++i)
+    if (ps->arr[i]) bufs[i].base = (*env)->GetPrimitiveArrayCritical(env, ps->arr[i], NULL);
+}
+
+/* mode 0 copies back (outputs) if the VM handed out a copy; JNI_ABORT for inputs, which are never modified */
+static void unpin(JNIEnv *env, pinned_set *ps, ozm_buf *bufs, jint mode) {
+  for (int i = 0; i < ps->n; ++i)
+    if (ps->arr[i]) {
+      if (bufs[i].base) (*env)->ReleasePrimitiveArrayCritical(env, ps->arr[i], (void *)bufs[i].base, mode);
+      (*env)->DeleteLocalRef(env, ps->arr[i]);
+    }
+  ps->n = 0;
+}
+
+static int int_array(JNIEnv *env, jintArray a, int *out, int max, int *n, ozm_status *st) {
+  *n = 0;
+  if (!a) return ozm_fail(OZEC_EINVAL, "null index array", st);
+  const jsize len = (*env)->GetArrayLength(env, a);
+  if (len > max) return ozm_fail(OZEC_EINVAL, "Too many erased, not recoverable", st);
+  jint v[MAX_BUFS];
+  (*env)->GetIntArrayRegion(env, a, 0, len, v);
+  for (jsize i = 0; i < len; ++i) out[i] = v[i];
+  *n = (int)len;
+  return 0;
+}
+
+/* ---------------------------------------------------------------- library / coder lifecycle */
+
+JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM *vm, void *reserved) {
+  (void)vm;
+  (void)reserved;
+  return JNI_VERSION_1_8;
+}
+
+JNIEXPORT jint JNICALL JNI_FN(deviceCount)(JNIEnv *env, jclass cls) {
+  (void)env;
+  (void)cls;
+  return ozec_device_count();
+}
+
+/* RawErasureCoderFactory.createEncoder/createDecoder: throws when no GPU is usable, so CodecUtil falls back
+ * (CodecUtil.createRawEncoderWithFallback, EC/rawcoder/util/CodecUtil.java:62-78) */
+JNIEXPORT jlong JNICALL JNI_FN(coderCreate)(JNIEnv *env, jclass cls, jboolean decoder, jint codec, jint k, jint p) {
+  (void)cls;
+  ozec_coder *h = NULL;
+  int rc = decoder ? ozec_decoder_create(codec, k, p, &h) : ozec_encoder_create(codec, k, p, &h);
+  if (rc) {
+    throw_rc(env, rc);
+    return 0;
+  }
+  return (jlong)(intptr_t)h;
+}
+
+/* release(): the Java side zeroes its handle under its write lock, so every later call sees "closed" */
+JNIEXPORT void JNICALL JNI_FN(coderRelease)(JNIEnv *env, jclass cls, jlong h) {
+  (void)env;
+  (void)cls;
+  if (!h) return;
+  ozec_coder_release((ozec_coder *)(intptr_t)h);
+  ozec_coder_free((ozec_coder *)(intptr_t)h);
+}
+
+/* ---------------------------------------------------------------- encode / decode */
+
+JNIEXPORT void JNICALL JNI_FN(encodeDirect)(JNIEnv *env, jclass cls, jlong h, jobjectArray in, jintArray inOff, jint len,
+                                            jobjectArray out, jintArray outOff) {
+  (void)cls;
+  ozm_buf ib[MAX_BUFS], ob[MAX_BUFS];
+  int ni = 0, no = 0;
+  ozm_status st;
+  if (collect_direct(env, in, inOff, ib, &ni, &st) || collect_direct(env, out, outOff, ob, &no, &st) ||
+      ozm_encode((ozec_coder *)(intptr_t)h, ib, ni, ob, no, len, &st))
+    throw_status(env, &st);
+}
+
+JNIEXPORT void JNICALL JNI_FN(encodeArrays)(JNIEnv *env, jclass cls, jlong h, jobjectArray in, jintArray inOff, jint len,
+                                            jobjectArray out, jintArray outOff) {
+  (void)cls;
+  ozm_buf ib[MAX_BUFS], ob[MAX_BUFS];
+  pinned_set pi, po;
+  ozm_status st;
+  pi.n = po.n = 0;
+  int rc = collect_arrays(env, in, inOff, ib, &pi, &st);
+  if (!rc) rc = collect_arrays(env, out, outOff, ob, &po, &st);
+  if (!rc) {
+    pin(env, &pi, ib);
+    pin(env, &po, ob);
+    rc = ozm_encode((ozec_coder *)(intptr_t)h, ib, pi.n, ob, po.n, len, &st); /* no JNI call in between */
+  }
+  unpin(env, &po, ob, 0);
+  unpin(env, &pi, ib, JNI_ABORT);
+  if (rc) throw_status(env, &st);
+}
+
+JNIEXPORT void JNICALL JNI_FN(decodeDirect)(JNIEnv *env, jclass cls, jlong h, jobjectArray in, jintArray inOff, jint len,
+                                            jintArray erased, jobjectArray out, jintArray outOff) {
+  (void)cls;
+  ozm_buf ib[MAX_BUFS], ob[MAX_BUFS];
+  int er[MAX_BUFS];
+  int ni = 0, no = 0, ne = 0;
+  ozm_status st;
+  if (collect_direct(env, in, inOff, ib, &ni, &st) || collect_direct(env, out, outOff, ob, &no, &st) ||
+      int_array(env, erased, er, MAX_BUFS, &ne, &st) ||
+      ozm_decode((ozec_coder *)(intptr_t)h, ib, ni, er, ne, ob, no, len, &st))
+    throw_status(env, &st);
+}
+
+JNIEXPORT void JNICALL JNI_FN(decodeArrays)(JNIEnv *env, jclass cls, jlong h, jobjectArray in, jintArray inOff, jint len,
+                                            jintArray erased, jobjectArray out, jintArray outOff) {
+  (void)cls;
+  ozm_buf ib[MAX_BUFS], ob[MAX_BUFS];
+  int er[MAX_BUFS];
+  int ne = 0;
+  pinned_set pi, po;
+  ozm_status st;
+  pi.n = po.n = 0;
+  int rc = int_array(env, erased, er, MAX_BUFS, &ne, &st);
+  if (!rc) rc = collect_arrays(env, in, inOff, ib, &pi, &st);
+  if (!rc) rc = collect_arrays(env, out, outOff, ob, &po, &st);
+  if (!rc) {
+    pin(env, &pi, ib);
+    pin(env, &po, ob);
+    rc = ozm_decode((ozec_coder *)(intptr_t)h, ib, pi.n, er, ne, ob, po.n, len, &st);
+  }
+  unpin(env, &po, ob, 0);
+  unpin(env, &pi, ib, JNI_ABORT);
+  if (rc) throw_status(env, &st);
+}
+
+/* ---------------------------------------------------------------- checksums */
+
+/* ChecksumByteBuffer.update(ByteBuffer) on a direct buffer: returns the new register */
+JNIEXPORT jint JNICALL JNI_FN(crcUpdateDirect)(JNIEnv *env, jclass cls, jint type, jint state, jobject buf, jint off,
+                                               jint len) {
+  (void)cls;
+  ozm_buf b = {0};
+  ozm_status st;
+  uint32_t s = (uint32_t)state;
+  b.present = buf != NULL;
+  if (buf) {
+    b.base = (*env)->GetDirectBufferAddress(env, buf);
+    b.capacity = (int64_t)(*env)->GetDirectBufferCapacity(env, buf);
+    b.offset = off;
+  }
+  if (ozm_crc_update(type, &s, &b, len, &st)) throw_status(env, &st);
+  return (jint)s;
+}
+
+/* update(byte[] b, int off, int len) */
+JNIEXPORT jint JNICALL JNI_FN(crcUpdateArray)(JNIEnv *env, jclass cls, jint type, jint state, jbyteArray arr, jint off,
+                                              jint len) {
+  (void)cls;
+  ozm_buf b = {0};
+  ozm_status st;
+  uint32_t s = (uint32_t)state;
+  int rc;
+  if (!arr) {
+    rc = ozm_crc_update(type, &s, &b, len, &st);
+  } else {
+    b.present = 1;
+    b.capacity = (*env)->GetArrayLength(env, arr);
+    b.offset = off;
+    b.base = (*env)->GetPrimitiveArrayCritical(env, arr, NULL);
+    rc = ozm_crc_update(type, &s, &b, len, &st);
+    if (b.base) (*env)->ReleasePrimitiveArrayCritical(env, arr, (void *)b.base, JNI_ABORT);
+  }
+  if (rc) throw_status(env, &st);
+  return (jint)s;
+}
+
+/* Checksum.computeChecksum of one direct buffer region: big-endian CRC bytes of every window into out; returns the
+ * number of bytes written (4 per window) */
+JNIEXPORT jint JNICALL JNI_FN(checksumWindowsDirect)(JNIEnv *env, jclass cls, jint type, jobject buf, jint off, jint len,
+                                                     jint bpc, jbyteArray out) {
+  (void)cls;
+  ozm_buf b = {0};
+  ozm_status st;
+  int64_t written = 0;
+  if (!out) {
+    ozm_fail(OZEC_EINVAL, "null checksum output", &st);
+    throw_status(env, &st);
+    return 0;
+  }
+  b.present = buf != NULL;
+  if (buf) {
+    b.base = (*env)->GetDirectBufferAddress(env, buf);
+    b.capacity = (int64_t)(*env)->GetDirectBufferCapacity(env, buf);
+    b.offset = off;
+  }
+  const jsize cap = (*env)->GetArrayLength(env, out);
+  uint8_t *o = (uint8_t *)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
+  int rc = ozm_checksum_windows(type, &b, len, bpc, o, cap, &written, &st);
+  if (o) (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
+  if (rc) throw_status(env, &st);
+  return (jint)written;
+}
+
+JNIEXPORT jint JNICALL JNI_FN(checksumWindowsArray)(JNIEnv *env, jclass cls, jint type, jbyteArray data, jint off,
+                                                    jint len, jint bpc, jbyteArray out) {
+  (void)cls;
+  ozm_buf b = {0};
+  ozm_status st;
+  int64_t written = 0;
+  if (!out) {
+    ozm_fail(OZEC_EINVAL, "null checksum output", &st);
+    throw_status(env, &st);
+    return 0;
+  }
+  const jsize cap = (*env)->GetArrayLength(env, out);
+  if (data) {
+    b.present = 1;
+    b.capacity = (*env)->GetArrayLength(env, data);
+    b.offset = off;
+    b.base = (*env)->GetPrimitiveArrayCritical(env, data, NULL);
+  }
+  uint8_t *o = (uint8_t *)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
+  int rc = ozm_checksum_windows(type, &b, len, bpc, o, cap, &written, &st);
+  if (o) (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
+  if (data && b.base) (*env)->ReleasePrimitiveArrayCritical(env, data, (void *)b.base, JNI_ABORT);
+  if (rc) throw_status(env, &st);
+  return (jint)written;
+}
+
+/* ---------------------------------------------------------------- pinned memory + stripe queue (§8(f) row 3) */
+
+/* a direct ByteBuffer over pinned host memory on the current GPU's NUMA node (ozec_host_alloc): cells DMA'd in place */
+JNIEXPORT jobject JNICALL JNI_FN(allocatePinned)(JNIEnv *env, jclass cls, jint bytes) {
+  (void)cls;
+  void *p = NULL;
+  int rc = bytes < 0 ? OZEC_EINVAL : ozec_host_alloc((size_t)bytes, &p);
+  if (rc) {
+    throw_rc(env, rc);
+    return NULL;
+  }
+  return (*env)->NewDirectByteBuffer(env, p, (jlong)bytes);
+}
+
+JNIEXPORT void JNICALL JNI_FN(freePinned)(JNIEnv *env, jclass cls, jobject buf) {
+  (void)cls;
+  if (!buf) return;
+  int rc = ozec_host_free((*env)->GetDirectBufferAddress(env, buf));
+  if (rc) throw_rc(env, rc);
+}
+
+JNIEXPORT jlong JNICALL JNI_FN(queueCreate)(JNIEnv *env, jclass cls, jlong enc, jint cellLen, jint stripesPerBatch,
+                                            jint type, jint bpc) {
+  (void)cls;
+  ozec_stripe_queue *q = NULL;
+  int rc = cellLen <= 0 || stripesPerBatch <= 0 || bpc < 0
+               ? OZEC_EINVAL
+               : ozec_stripe_queue_create((ozec_coder *)(intptr_t)enc, (size_t)cellLen, (size_t)stripesPerBatch, type,
+                                          (size_t)bpc, 1, &q);
+  if (rc) {
+    throw_rc(env, rc);
+    return 0;
+  }
+  return (jlong)(intptr_t)q;
+}
+
+/* submit(data cells, parity cells, len, crcs): direct buffers at their positions; returns the stripe's ticket.
+ * The Java side keeps the buffers referenced until waitFor(ticket) returns (HipStripeQueue). */
+JNIEXPORT jlong JNICALL JNI_FN(queueSubmit)(JNIEnv *env, jclass cls, jlong q, jobjectArray data, jintArray dataOff,
+                                            jobjectArray parity, jintArray parityOff, jint len, jobject crcs) {
+  (void)cls;
+  ozm_buf db[MAX_BUFS], pb[MAX_BUFS];
+  const uint8_t *dp[MAX_BUFS], *pp[MAX_BUFS];
+  int nd = 0, np = 0;
+  ozm_status st;
+  uint64_t ticket = 0;
+  if (collect_direct(env, data, dataOff, db, &nd, &st) || collect_direct(env, parity, parityOff, pb, &np, &st) ||
+      ozm_resolve(db, nd, 0, len, dp, &st) || ozm_resolve(pb, np, 0, len, pp, &st)) {
+    throw_status(env, &st);
+    return 0;
+  }
+  uint32_t *cp = crcs ? (uint32_t *)(*env)->GetDirectBufferAddress(env, crcs) : NULL;
+  if (crcs && !cp) {
+    ozm_fail(OZEC_EINVAL, "crcs must be a direct buffer", &st);
+    throw_status(env, &st);
+    return 0;
+  }
+  int rc = len < 0 ? OZEC_EINVAL
+                   : ozec_stripe_queue_submit((ozec_stripe_queue *)(intptr_t)q, dp, (uint8_t *const *)pp, (size_t)len,
+                                              cp, &ticket);
+  if (rc) throw_rc(env, rc);
+  return (jlong)ticket;
+}
+
+JNIEXPORT void JNICALL JNI_FN(queueWait)(JNIEnv *env, jclass cls, jlong q, jlong ticket) {
+  (void)cls;
+  int rc = ozec_stripe_queue_wait((ozec_stripe_queue *)(intptr_t)q, (uint64_t)ticket);
+  if (rc) throw_rc(env, rc);
+}
+
+JNIEXPORT void JNICALL JNI_FN(queueFree)(JNIEnv *env, jclass cls, jlong q) {
+  (void)cls;
+  int rc = ozec_stripe_queue_free((ozec_stripe_queue *)(intptr_t)q);
+  if (rc) throw_rc(env, rc);
+}

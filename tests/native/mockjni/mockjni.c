@@ -1,0 +1,162 @@
+/*
+ * TEST DOUBLE: fake Java objects and the JNI functions of tests/native/mockjni/jni.h, driven from Python (ctypes) by
+ * tests/test_jni_glue.py to call the real jni/ozec_jni.c entry points.  Direct buffers and byte[] wrap caller memory;
+ * GetPrimitiveArrayCritical hands out the array memory itself (as HotSpot does) and counts pins so the test can
+ * check that every pin is released; ThrowNew records the pending exception.
+ */
+#include "jni.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum { K_DIRECT = 1, K_BYTES = 2, K_INTS = 3, K_OBJS = 4, K_CLASS = 5 };
+
+struct mock_object {
+  int kind;
+  void *data;
+  int64_t len;
+  struct mock_object **elems;
+  char name[96];
+};
+
+static int g_pins, g_local_refs;
+static char g_exc_class[96], g_exc_msg[512];
+static int g_exc_pending;
+static char g_missing[96];
+
+static jclass find_class(JNIEnv *env, const char *name) {
+  (void)env;
+  if (g_missing[0] && !strcmp(name, g_missing)) {
+    g_exc_pending = 1;
+    snprintf(g_exc_class, sizeof g_exc_class, "java/lang/NoClassDefFoundError");
+    snprintf(g_exc_msg, sizeof g_exc_msg, "%s", name);
+    return NULL;
+  }
+  struct mock_object *c = calloc(1, sizeof *c);
+  c->kind = K_CLASS;
+  snprintf(c->name, sizeof c->name, "%s", name);
+  return c; /* leaked: a test process makes few */
+}
+
+static jint throw_new(JNIEnv *env, jclass c, const char *msg) {
+  (void)env;
+  g_exc_pending = 1;
+  snprintf(g_exc_class, sizeof g_exc_class, "%s", c->name);
+  snprintf(g_exc_msg, sizeof g_exc_msg, "%s", msg ? msg : "");
+  return 0;
+}
+
+static void exception_clear(JNIEnv *env) {
+  (void)env;
+  g_exc_pending = 0;
+}
+
+static void delete_local_ref(JNIEnv *env, jobject o) {
+  (void)env;
+  if (o) --g_local_refs;
+}
+
+static jsize array_length(JNIEnv *env, jarray a) {
+  (void)env;
+  return (jsize)a->len;
+}
+
+static jobject object_array_element(JNIEnv *env, jobjectArray a, jsize i) {
+  (void)env;
+  if (a->kind != K_OBJS || i < 0 || i >= a->len) return NULL;
+  if (a->elems[i]) ++g_local_refs;
+  return a->elems[i];
+}
+
+static void int_array_region(JNIEnv *env, jintArray a, jsize start, jsize n, jint *buf) {
+  (void)env;
+  memcpy(buf, (jint *)a->data + start, sizeof(jint) * (size_t)n);
+}
+
+static void *array_critical(JNIEnv *env, jarray a, jboolean *is_copy) {
+  (void)env;
+  if (is_copy) *is_copy = 0;
+  ++g_pins;
+  return a->data;
+}
+
+static void release_array_critical(JNIEnv *env, jarray a, void *p, jint mode) {
+  (void)env;
+  (void)a;
+  (void)p;
+  (void)mode;
+  --g_pins;
+}
+
+static jobject new_direct(JNIEnv *env, void *p, jlong cap) {
+  (void)env;
+  struct mock_object *o = calloc(1, sizeof *o);
+  o->kind = K_DIRECT;
+  o->data = p;
+  o->len = cap;
+  return o;
+}
+
+static void *direct_address(JNIEnv *env, jobject o) {
+  (void)env;
+  return o && o->kind == K_DIRECT ? o->data : NULL;
+}
+
+static jlong direct_capacity(JNIEnv *env, jobject o) {
+  (void)env;
+  return o && o->kind == K_DIRECT ? o->len : -1;
+}
+
+static const struct JNINativeInterface_ g_table = {
+    find_class,           throw_new,      exception_clear,       delete_local_ref, array_length,
+    object_array_element, int_array_region, array_critical,      release_array_critical,
+    new_direct,           direct_address, direct_capacity,
+};
+static JNIEnv g_env = &g_table;
+
+/* ---- driver API (ctypes) */
+JNIEnv *mock_env(void) { return &g_env; }
+
+static struct mock_object *obj(int kind, void *data, int64_t len) {
+  struct mock_object *o = calloc(1, sizeof *o);
+  o->kind = kind;
+  o->data = data;
+  o->len = len;
+  return o;
+}
+
+struct mock_object *mock_direct(void *p, int64_t cap) { return obj(K_DIRECT, p, cap); }
+/* a heap ByteBuffer: a Java object that is not direct (GetDirectBufferAddress -> NULL) */
+struct mock_object *mock_heap_buffer(void *p, int64_t cap) { return obj(K_BYTES, p, cap); }
+struct mock_object *mock_bytes(void *p, int64_t len) { return obj(K_BYTES, p, len); }
+struct mock_object *mock_ints(int32_t *p, int64_t n) { return obj(K_INTS, p, n); }
+
+struct mock_object *mock_objects(int64_t n) {
+  struct mock_object *o = obj(K_OBJS, NULL, n);
+  o->elems = calloc((size_t)(n ? n : 1), sizeof(struct mock_object *));
+  return o;
+}
+
+void mock_set(struct mock_object *arr, int64_t i, struct mock_object *v) { arr->elems[i] = v; }
+void *mock_data(struct mock_object *o) { return o ? o->data : NULL; }
+int64_t mock_len(struct mock_object *o) { return o ? o->len : -1; }
+
+void mock_free(struct mock_object *o) {
+  if (!o) return;
+  free(o->elems);
+  free(o);
+}
+
+int mock_pins(void) { return g_pins; }
+int mock_local_refs(void) { return g_local_refs; }
+void mock_set_missing_class(const char *name) { snprintf(g_missing, sizeof g_missing, "%s", name ? name : ""); }
+
+/* 1 and the exception if one is pending (then cleared), else 0 */
+int mock_take_exception(char *cls, int cls_cap, char *msg, int msg_cap) {
+  if (!g_exc_pending) return 0;
+  snprintf(cls, (size_t)cls_cap, "%s", g_exc_class);
+  snprintf(msg, (size_t)msg_cap, "%s", g_exc_msg);
+  g_exc_pending = 0;
+  return 1;
+}

@@ -1,0 +1,276 @@
+"""jni/ozec_jni.c itself, compiled against the JNI test double (tests/native/mockjni) and called the way the Java
+classes (java/src/main/java/.../OzecNative.java) call it: direct ByteBuffers with positions, byte[] with offsets,
+null decode inputs, int[] erasedIndexes.  Checks the results against the oracle (GPU), the Java exception each
+failure raises, and that every pinned array is released and every local reference deleted (CPU and GPU)."""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle
+from synth import SEED, cells
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "ozone_amd", "lib")
+P = "Java_org_apache_ozone_erasurecode_rawcoder_OzecNative_"
+vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+
+
+@pytest.fixture(scope="module")
+def J():
+    if not os.path.exists(os.path.join(LIBDIR, "libozec.so")):
+        pytest.skip("libozec.so not built")
+    d = tempfile.mkdtemp(prefix="ozec_mockjni_")
+    so = os.path.join(d, "libozec_jni_mock.so")
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-Werror",
+                    "-I", os.path.join(ROOT, "tests", "native", "mockjni"), "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "jni", "ozec_jni.c"), os.path.join(ROOT, "jni", "ozec_marshal.c"),
+                    os.path.join(ROOT, "tests", "native", "mockjni", "mockjni.c"), "-L", LIBDIR, "-lozec",
+                    f"-Wl,-rpath,{LIBDIR}", "-o", so], check=True, capture_output=True, timeout=120)
+    L = ctypes.CDLL(so)
+    for name, res, args in [
+        ("mock_env", vp, []), ("mock_direct", vp, [vp, i64]), ("mock_heap_buffer", vp, [vp, i64]),
+        ("mock_bytes", vp, [vp, i64]), ("mock_ints", vp, [vp, i64]), ("mock_objects", vp, [i64]),
+        ("mock_set", None, [vp, i64, vp]), ("mock_data", vp, [vp]), ("mock_len", i64, [vp]), ("mock_free", None, [vp]),
+        ("mock_pins", ctypes.c_int, []), ("mock_local_refs", ctypes.c_int, []),
+        ("mock_set_missing_class", None, [ctypes.c_char_p]),
+        ("mock_take_exception", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+        (P + "deviceCount", i32, [vp, vp]),
+        (P + "coderCreate", i64, [vp, vp, ctypes.c_uint8, i32, i32, i32]),
+        (P + "coderRelease", None, [vp, vp, i64]),
+        (P + "encodeDirect", None, [vp, vp, i64, vp, vp, i32, vp, vp]),
+        (P + "encodeArrays", None, [vp, vp, i64, vp, vp, i32, vp, vp]),
+        (P + "decodeDirect", None, [vp, vp, i64, vp, vp, i32, vp, vp, vp]),
+        (P + "decodeArrays", None, [vp, vp, i64, vp, vp, i32, vp, vp, vp]),
+        (P + "crcUpdateDirect", i32, [vp, vp, i32, i32, vp, i32, i32]),
+        (P + "crcUpdateArray", i32, [vp, vp, i32, i32, vp, i32, i32]),
+        (P + "checksumWindowsDirect", i32, [vp, vp, i32, vp, i32, i32, i32, vp]),
+        (P + "checksumWindowsArray", i32, [vp, vp, i32, vp, i32, i32, i32, vp]),
+        (P + "allocatePinned", vp, [vp, vp, i32]), (P + "freePinned", None, [vp, vp, vp]),
+        (P + "queueCreate", i64, [vp, vp, i64, i32, i32, i32, i32]),
+        (P + "queueSubmit", i64, [vp, vp, i64, vp, vp, vp, vp, i32, vp]),
+        (P + "queueWait", None, [vp, vp, i64, i64]), (P + "queueFree", None, [vp, vp, i64])]:
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    L.env = L.mock_env()
+    return L
+
+
+class Java:
+    """Builds fake Java objects over numpy memory (kept alive here) and reads the pending exception."""
+
+    def __init__(self, J):
+        self.J, self.keep, self.objs = J, [], []
+
+    def _o(self, o):
+        self.objs.append(o)
+        return o
+
+    def direct(self, a):
+        self.keep.append(a)
+        return self._o(self.J.mock_direct(a.ctypes.data, a.size))
+
+    def heap(self, a):
+        self.keep.append(a)
+        return self._o(self.J.mock_heap_buffer(a.ctypes.data, a.size))
+
+    def bytes(self, a):
+        self.keep.append(a)
+        return self._o(self.J.mock_bytes(a.ctypes.data, a.size))
+
+    def ints(self, v):
+        a = np.asarray(v, np.int32)
+        self.keep.append(a)
+        return self._o(self.J.mock_ints(a.ctypes.data, a.size))
+
+    def array(self, elems):
+        arr = self._o(self.J.mock_objects(len(elems)))
+        for i, e in enumerate(elems):
+            self.J.mock_set(arr, i, e)
+        return arr
+
+    def exception(self):
+        c, m = ctypes.create_string_buffer(128), ctypes.create_string_buffer(512)
+        return (c.value.decode(), m.value.decode()) if self.J.mock_take_exception(c, 128, m, 512) else None
+
+    def close(self):
+        for o in self.objs:
+            self.J.mock_free(o)
+        self.objs = []
+
+
+@pytest.fixture
+def java(J):
+    j = Java(J)
+    yield j
+    assert J.mock_pins() == 0, "a pinned array was not released"
+    assert J.mock_local_refs() == 0, "a local reference was not deleted"
+    j.close()
+
+
+def call(J, name, *args):
+    return getattr(J, P + name)(J.env, None, *args)
+
+
+def gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+# ------------------------------------------------------------------------------------------ CPU
+
+
+def test_closed_handle_raises_ioexception_and_unpins(J, java):
+    a = [np.zeros(64, np.uint8) for _ in range(9)]
+    call(J, "encodeDirect", 0, java.array([java.direct(x) for x in a[:6]]), java.ints([0] * 6), 64,
+         java.array([java.direct(x) for x in a[6:]]), java.ints([0] * 3))
+    assert java.exception() == ("java/io/IOException", "coder is closed")
+    call(J, "encodeArrays", 0, java.array([java.bytes(x) for x in a[:6]]), java.ints([0] * 6), 64,
+         java.array([java.bytes(x) for x in a[6:]]), java.ints([0] * 3))
+    assert java.exception()[0] == "java/io/IOException"
+    call(J, "decodeArrays", 0, java.array([None] + [java.bytes(x) for x in a[1:9]]), java.ints([0] * 9), 64,
+         java.ints([0]), java.array([java.bytes(a[0])]), java.ints([0]))
+    assert java.exception()[0] == "java/io/IOException"
+
+
+def test_argument_errors_before_the_device(J, java):
+    data = np.zeros(100, np.uint8)
+    out = np.zeros(64, np.uint8)
+    assert call(J, "checksumWindowsDirect", 3, java.direct(data), 0, 100, 0, java.bytes(out)) == 0
+    assert java.exception() == ("org/apache/hadoop/HadoopIllegalArgumentException", "bytesPerChecksum must be positive")
+    # hadoop-common absent from the class path: the superclass is thrown instead
+    J.mock_set_missing_class(b"org/apache/hadoop/HadoopIllegalArgumentException")
+    try:
+        call(J, "checksumWindowsArray", 3, java.bytes(data), 0, 100, 0, java.bytes(out))
+        assert java.exception() == ("java/lang/IllegalArgumentException", "bytesPerChecksum must be positive")
+    finally:
+        J.mock_set_missing_class(None)
+    assert call(J, "crcUpdateArray", 3, -1, java.bytes(data), 0, 0) == -1  # empty update: register unchanged
+    assert java.exception() is None
+    assert call(J, "crcUpdateArray", 3, -1, java.bytes(data), 90, 20) == -1  # offset + length past the array
+    assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"
+    assert call(J, "allocatePinned", -1) is None
+    assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"
+    assert call(J, "queueCreate", 0, 0, 4, 3, 16384) == 0
+    assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"
+
+
+def test_no_device_makes_the_factory_throw(J, java):
+    """Without a GPU the coder constructor throws, so CodecUtil falls back to rs_java (CodecUtil.java:62-78)."""
+    if gpu():
+        pytest.skip("a GPU is visible")
+    assert call(J, "deviceCount") == 0
+    assert call(J, "coderCreate", 0, 0, 6, 3) == 0
+    cls, msg = java.exception()
+    assert cls == "java/io/IOException" and "no HIP device" in msg
+
+
+# ------------------------------------------------------------------------------------------ GPU
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arrays", [False, True])
+def test_encode_decode_vs_oracle(J, java, arrays):
+    k, p, n, pos = 6, 3, 1 << 16, 11
+    h = call(J, "coderCreate", 0, 0, k, p)
+    hd = call(J, "coderCreate", 1, 0, k, p)
+    assert java.exception() is None and h and hd
+    try:
+        wrap = java.bytes if arrays else java.direct
+        enc_fn, dec_fn = ("encodeArrays", "decodeArrays") if arrays else ("encodeDirect", "decodeDirect")
+        d = cells(SEED, 740000, k, n)
+        ins = [np.zeros(n + 2 * pos, np.uint8) for _ in range(k)]
+        for w, x in zip(ins, d):
+            w[pos:pos + n] = x
+        outs = [np.full(n + 2 * pos, 0xA5, np.uint8) for _ in range(p)]
+        call(J, enc_fn, h, java.array([wrap(x) for x in ins]), java.ints([pos] * k), n,
+             java.array([wrap(x) for x in outs]), java.ints([pos] * p))
+        assert java.exception() is None
+        ref = oracle.rs_encode(k, p, d)
+        for o, r in zip(outs, ref):
+            assert (o[pos:pos + n] == r).all() and (o[:pos] == 0xA5).all()
+        units = d + ref
+        erased = [1, 7]
+        inputs = [None if u in erased else wrap(units[u]) for u in range(k + p)]
+        rec = [np.zeros(n, np.uint8) for _ in erased]
+        call(J, dec_fn, hd, java.array(inputs), java.ints([0] * (k + p)), n, java.ints(erased),
+             java.array([wrap(r) for r in rec]), java.ints([0, 0]))
+        assert java.exception() is None
+        assert all((r == units[e]).all() for r, e in zip(rec, erased))
+        # the reference's failures, with its exception classes
+        call(J, enc_fn, h, java.array([wrap(x) for x in ins[:5]]), java.ints([pos] * 5), n,
+             java.array([wrap(x) for x in outs]), java.ints([pos] * p))
+        assert java.exception() == ("org/apache/hadoop/HadoopIllegalArgumentException", "Invalid inputs length 5 !=6")
+        call(J, dec_fn, hd, java.array(inputs), java.ints([0] * (k + p)), n, java.ints([0, 1, 2, 3]),
+             java.array([wrap(r) for r in rec] * 2), java.ints([0] * 4))
+        assert java.exception()[1] == "Too many erased, not recoverable"
+        if not arrays:  # a heap ByteBuffer in the direct path has no address
+            call(J, "encodeDirect", h, java.array([java.heap(ins[0])] + [java.direct(x) for x in ins[1:]]),
+                 java.ints([pos] * k), n, java.array([java.direct(x) for x in outs]), java.ints([pos] * p))
+            assert "not a direct buffer" in java.exception()[1]
+    finally:
+        call(J, "coderRelease", h)
+        call(J, "coderRelease", hd)
+
+
+@pytest.mark.gpu
+def test_checksums_and_streaming_update_vs_oracle(J, java):
+    n, bpc = 70000, 16384
+    data = cells(SEED, 741000, 1, n + 5)[0]
+    out = np.zeros(4 * 5, np.uint8)
+    assert call(J, "checksumWindowsArray", 3, java.bytes(data), 5, n, bpc, java.bytes(out)) == 20
+    assert (out.view(">u4") == oracle.crc_windows(oracle.CRC32C, data[5:5 + n], bpc)).all()
+    out[:] = 0
+    assert call(J, "checksumWindowsDirect", 2, java.direct(data), 5, n, bpc, java.bytes(out)) == 20
+    assert (out.view(">u4") == oracle.crc_windows(oracle.CRC32, data[5:5 + n], bpc)).all()
+    state = -1  # reset(): 0xFFFFFFFF
+    for lo, hi in ((0, 1), (1, 4000), (4000, 70005)):  # update(byte[]) then update(ByteBuffer) pieces
+        fn = "crcUpdateArray" if lo == 0 else "crcUpdateDirect"
+        state = call(J, fn, 3, state, java.bytes(data) if lo == 0 else java.direct(data), lo, hi - lo)
+    assert java.exception() is None
+    assert (~state) & 0xFFFFFFFF == oracle.crc_windows(oracle.CRC32C, data, n + 5)[0]
+
+
+@pytest.mark.gpu
+def test_pinned_buffers_and_stripe_queue_through_jni(J, java):
+    k, p, n, bpc = 6, 3, 1 << 15, 8192
+    h = call(J, "coderCreate", 0, 0, k, p)
+    q = call(J, "queueCreate", h, n, 2, 3, bpc)
+    assert java.exception() is None and q
+    slabs, jobs = [], []
+    try:
+        for s in range(5):
+            pb = call(J, "allocatePinned", (k + p) * n)
+            assert java.exception() is None and pb
+            slabs.append(pb)
+            view = np.ctypeslib.as_array((ctypes.c_uint8 * ((k + p) * n)).from_address(J.mock_data(pb)))
+            for j, x in enumerate(cells(SEED, 742000 + 10 * s, k, n)):
+                view[j * n:(j + 1) * n] = x
+            crcs = np.zeros((k + p) * (n // bpc), np.uint32)
+            cells_d = java.array([pb] * k)
+            cells_p = java.array([pb] * p)
+            t = call(J, "queueSubmit", q, cells_d, java.ints([j * n for j in range(k)]), cells_p,
+                     java.ints([(k + r) * n for r in range(p)]), n, java.direct(crcs.view(np.uint8)))
+            assert java.exception() is None
+            jobs.append((t, view, crcs))
+        call(J, "queueWait", q, jobs[-1][0])
+        assert java.exception() is None
+        for t, view, crcs in jobs:
+            d = [view[j * n:(j + 1) * n].copy() for j in range(k)]
+            ref = oracle.rs_encode(k, p, d)
+            assert all((view[(k + r) * n:(k + r + 1) * n] == ref[r]).all() for r in range(p)), t
+            exp = np.concatenate([oracle.crc_windows(oracle.CRC32C, u, bpc) for u in d + ref])
+            assert (crcs.byteswap() == exp).all(), t
+    finally:
+        call(J, "queueFree", q)
+        for pb in slabs:
+            call(J, "freePinned", pb)
+            J.mock_free(pb)
+        call(J, "coderRelease", h)
+    assert java.exception() is None

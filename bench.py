@@ -702,37 +702,50 @@ def pmc_traffic(args, alg_bytes):
 
 
 def stream_latency(args):
-    """In-situ per-call cost of the drop-in entry points (one call = what one Java call does): ozec_encode of one
-    rs-6-3-1024k stripe (RawErasureEncoder.encode, ECKeyOutputStream.java:304) from 1 thread, and
-    ozec_crc_update (ChecksumByteBuffer.update, Checksum.java:157-200) at 1 B / 512 B / 16 KiB, each against the
-    CPU doing the same call."""
+    """In-situ per-call cost of the drop-in entry points (one call = what one Java call does), through the C ABI
+    from one thread: ozec_encode of one rs-6-3 stripe (RawErasureEncoder.encode, ECKeyOutputStream.java:304) and
+    ozec_crc_update (ChecksumByteBuffer.update, Checksum.java:157-200), beside the CPU doing the same call
+    (oracle/cpu_baseline.c percall_*: the rs_java table loop; the SSE4.2 crc32 the JDK's CRC32C uses).  The ctypes
+    call overhead of the Python harness is measured on a no-op entry point and reported, not subtracted."""
     from ozone_amd import _lib
     from ozone_amd import rawcoder as rc
-    import oracle
     n, k, p = MIB, 6, 3
     rng = np.random.default_rng(1)
-    d = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
-    o = [np.empty(n, np.uint8) for _ in range(p)]
-    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
     L = _lib.lib()
 
-    def per_call(fn, reps):
+    def per_call(fn, min_s=0.3):
         fn()
-        t0 = time.perf_counter()
-        for _ in range(reps):
+        calls, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < min_s:
             fn()
-        return (time.perf_counter() - t0) / reps * 1e6
+            calls += 1
+        return (time.perf_counter() - t0) / calls * 1e6
 
-    out = {"encode_stripe_us": round(per_call(lambda: enc.encode(d, o), 50), 1)}
-    out["encode_stripe_cpu_us"] = round(per_call(lambda: oracle.rs_encode(k, p, d), 10), 1)
+    exe, flags = _cpu_baseline_bin()
+
+    def cpu(kind, nbytes):
+        out = subprocess.run([exe, kind, str(nbytes), "0.3"], capture_output=True, text=True, timeout=60)
+        return json.loads(out.stdout)["us_per_call"]
+
+    rows = {"ctypes_call_overhead_us": round(per_call(lambda: L.ozec_version(), 0.1), 2)}
+    for cell in (64 << 10, MIB):
+        d = [rng.integers(0, 256, cell, dtype=np.uint8) for _ in range(k)]
+        o = [np.empty(cell, np.uint8) for _ in range(p)]
+        enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+        rows[f"encode_stripe_{cell >> 10}KiB_cells"] = {"gpu_us": round(per_call(lambda: enc.encode(d, o)), 1),
+                                                       "cpu_us": round(cpu("percall_encode", cell), 1)}
+    buf = rng.integers(0, 256, 16 << 20, dtype=np.uint8)
     st = ctypes.c_uint32(0xFFFFFFFF)
-    buf = rng.integers(0, 256, 16384, dtype=np.uint8)
-    for nb in (1, 512, 16384):
-        out[f"crc_update_{nb}B_us"] = round(per_call(lambda: L.ozec_crc_update(3, ctypes.byref(st), buf.ctypes.data, nb),
-                                                     200), 2)
-        out[f"crc_update_{nb}B_cpu_us"] = round(per_call(lambda: oracle.crc_windows(oracle.CRC32C, buf[:nb], 16384),
-                                                         200), 2)
-    return out
+    cross = None
+    for nb in (1, 512, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20):
+        g = per_call(lambda: L.ozec_crc_update(3, ctypes.byref(st), buf.ctypes.data, nb), 0.2)
+        c = cpu("percall_crc32c", nb)
+        rows[f"crc_update_{nb}B"] = {"gpu_us": round(g, 2), "cpu_us": round(c, 2)}
+        if cross is None and g < c:
+            cross = nb
+    rows["crc_update_gpu_wins_from_bytes"] = cross
+    rows["cpu"] = f"1 thread, oracle/cpu_baseline.c percall_*, {flags}"
+    return rows
 
 
 # ------------------------------------------------------------------------------------------ main

@@ -221,6 +221,43 @@ int main(int argc, char **argv) {
     return 2;
   }
   g_workload = argv[1];
+  if (!strcmp(g_workload, "percall_crc32c") || !strcmp(g_workload, "percall_encode")) {
+    /* per-call cost of one ChecksumByteBuffer.update(n bytes) / one rs-6-3 stripe encode of n-byte cells,
+     * single thread (the JDK intrinsic / rs_java call a Java writer makes): usage percall_* <bytes> <seconds> */
+    const size_t n = (size_t)atol(argv[2]);
+    const double secs = atof(argv[3]);
+    zeros_table(zeros_short, SHORT);
+    const int enc = !strcmp(g_workload, "percall_encode");
+    uint8_t *cells[9];
+    for (int u = 0; u < 9; u++) {
+      cells[u] = aligned_alloc(4096, (n + 4095) / 4096 * 4096);
+      fill(cells[u], n, 77 + u);
+    }
+    if (enc) {
+      uint8_t mat[9 * 6];
+      oracle_gen_cauchy_matrix(mat, 9, 6);
+      oracle_init_tables(6, 3, mat, 36, g_coder.enc_tabs);
+    }
+    volatile uint32_t sink = 0;
+    long calls = 0;
+    const double t0 = now();
+    double t = t0;
+    do {
+      for (int r = 0; r < 16; r++, calls++) {
+        if (enc) {
+          for (int q = 0; q < 3; q++) memset(cells[6 + q], 0, n);
+          oracle_encode_data(g_coder.enc_tabs, (int)n, 6, (const uint8_t *const *)cells, 3, cells + 6);
+          sink ^= cells[6][0];
+        } else {
+          sink ^= crc32c_hw(cells[0], n);
+        }
+      }
+      t = now();
+    } while (t - t0 < secs);
+    printf("{\"workload\": \"%s\", \"bytes\": %zu, \"calls\": %ld, \"us_per_call\": %.3f, \"sink\": %u}\n",
+           g_workload, n, calls, (t - t0) / calls * 1e6, sink);
+    return 0;
+  }
   int T = atoi(argv[2]);
   g_seconds = atof(argv[3]);
   if (T < 1) T = 1;

@@ -545,16 +545,45 @@ __device__ __forceinline__ uint32_t byte_and(uint32_t w, uint32_t mask) {
   }
 }
 
-// XOR of the 26 lookups of block b in the table set at T (26 x 32 words)
-template <bool HALVES = false>
-__device__ __forceinline__ uint32_t g26_block(const uint32_t *T, const uint4 b) {
+// as byte_and with the mask in a VGPR for every byte position: no SGPR or literal operand, which puts the AND in
+// the fast VALU issue class (a v_perm or an SGPR / literal-operand op costs ~1.6x a plain VOP2 op per step,
+// scripts/gpu_valu_pad.sh)
+template <int Q>
+__device__ __forceinline__ uint32_t byte_and_v(uint32_t w, uint32_t vmask) {
+  uint32_t d;
+  if constexpr (Q == 0) {
+    asm("v_and_b32 %0, %1, %2" : "=v"(d) : "v"(vmask), "v"(w));
+  } else if constexpr (Q == 1) {
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+        : "=v"(d) : "v"(w), "v"(vmask));
+  } else if constexpr (Q == 2) {
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+        : "=v"(d) : "v"(w), "v"(vmask));
+  } else {
+    asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+        : "=v"(d) : "v"(w), "v"(vmask));
+  }
+  return d;
+}
+
+// XOR of the 26 lookups of block b in the table set at T (26 x 32 words).  VMASK: byte_and_v with vm = 0x7c in
+// a VGPR instead of the SGPR / literal mask.
+template <bool HALVES = false, bool VMASK = false>
+__device__ __forceinline__ uint32_t g26_block(const uint32_t *T, const uint4 b, uint32_t vm = 0x7cu) {
   const uint32_t w[4] = {b.x, b.y, b.z, b.w};
   uint32_t t[26];
   auto four = [&](uint32_t v, int g0) {
-    t[g0] = lds_at(T, g0 * 128 + byte_and<0>(v, 0x7cu));
-    t[g0 + 1] = lds_at(T, (g0 + 1) * 128 + byte_and<1>(v, 0x7cu));
-    t[g0 + 2] = lds_at(T, (g0 + 2) * 128 + byte_and<2>(v, 0x7cu));
-    t[g0 + 3] = lds_at(T, (g0 + 3) * 128 + byte_and<3>(v, 0x7cu));
+    if constexpr (VMASK) {
+      t[g0] = lds_at(T, g0 * 128 + byte_and_v<0>(v, vm));
+      t[g0 + 1] = lds_at(T, (g0 + 1) * 128 + byte_and_v<1>(v, vm));
+      t[g0 + 2] = lds_at(T, (g0 + 2) * 128 + byte_and_v<2>(v, vm));
+      t[g0 + 3] = lds_at(T, (g0 + 3) * 128 + byte_and_v<3>(v, vm));
+    } else {
+      t[g0] = lds_at(T, g0 * 128 + byte_and<0>(v, 0x7cu));
+      t[g0 + 1] = lds_at(T, (g0 + 1) * 128 + byte_and<1>(v, 0x7cu));
+      t[g0 + 2] = lds_at(T, (g0 + 2) * 128 + byte_and<2>(v, 0x7cu));
+      t[g0 + 3] = lds_at(T, (g0 + 3) * 128 + byte_and<3>(v, 0x7cu));
+    }
   };
   if constexpr (HALVES) {
     // two halves of 14 and 12 lookups with a scheduling fence between them: at most 14 lookup results are live
@@ -945,7 +974,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 // (TM): 1 = {lo0, lo1, mid0, mid1} from LDS in one ds_read_b128 broadcast + top as an SGPR operand;
 // 2 = lo1/mid1/top as SGPR operands, {lo0, mid0} from LDS in one ds_read_b64 broadcast; 3 = as 1 with top from
 // LDS too (ds_read_b32 broadcast).
-template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false, bool HV = false>
+// PAD > 0 (diagnostic variants only): PAD extra independent VALU ops per step, to measure what one more VALU
+// instruction costs the kernel (scripts/gpu_valu_pad.sh; DESIGN §2.3 "what bounds it").
+template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false, bool HV = false, int PAD = 0,
+          int PADK = 0, bool VMASK = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_g26(const EncCrcArgs e, const TabArgs<K * R> tabs) {
   constexpr int E = D;
   static_assert(D >= 1, "group of at least one step");
@@ -998,6 +1030,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     };
     static_assert(!PF || D % 2 == 0, "prefetch alternates two register sets");
     uint4 xa[K], xb[K];
+    uint32_t pad[4] = {0, 0, 0, 0};
+    uint32_t vmask = 0x7cu;
+    if constexpr (VMASK) asm volatile("v_mov_b32 %0, 0x7c" : "=v"(vmask));  // materialised once, lives in a VGPR
     if (PF && G > 0) load_x(0, xa);
     for (int32_t g = 0; g < G; ++g) {
 #pragma unroll
@@ -1066,8 +1101,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         if constexpr (XORC) store_data_hold(acc[0]);
 #pragma unroll
         for (int j = 0; j < (XORC ? K : K + R); ++j) {
-          S[j] ^= g26_block<HV>(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K]);
+          S[j] ^= g26_block<HV, VMASK>(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K], vmask);
           __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (PAD > 0) {  // PADK: 0 v_xor_b32 (fast class), 1 v_perm_b32 (slow class), 2 ds_read_b32
+#pragma unroll
+          for (int i = 0; i < PAD; i += 4) {
+            if constexpr (PADK == 0)
+              asm volatile("v_xor_b32 %0, %0, %4\n\tv_xor_b32 %1, %1, %4\n\tv_xor_b32 %2, %2, %4\n\tv_xor_b32 %3, %3, %4"
+                           : "+v"(pad[0]), "+v"(pad[1]), "+v"(pad[2]), "+v"(pad[3])
+                           : "v"(S[0]));
+            else if constexpr (PADK == 1)
+              asm volatile("v_perm_b32 %0, %0, %4, %4\n\tv_perm_b32 %1, %1, %4, %4\n\tv_perm_b32 %2, %2, %4, %4\n\t"
+                           "v_perm_b32 %3, %3, %4, %4"
+                           : "+v"(pad[0]), "+v"(pad[1]), "+v"(pad[2]), "+v"(pad[3])
+                           : "v"(S[0]));
+            else
+              asm volatile("ds_read_b32 %0, %4\n\tds_read_b32 %1, %4 offset:256\n\tds_read_b32 %2, %4 offset:512\n\t"
+                           "ds_read_b32 %3, %4 offset:768\n\ts_waitcnt lgkmcnt(0)"
+                           : "=v"(pad[0]), "=v"(pad[1]), "=v"(pad[2]), "=v"(pad[3])
+                           : "v"(static_cast<uint32_t>(lane * 4)));
+          }
         }
       }
       if (g + 1 < G) {
@@ -1080,6 +1134,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 #pragma unroll
       for (int j = 0; j < K; ++j) S[K] ^= S[j];
     }
+    if constexpr (PAD > 0) S[0] ^= (pad[0] ^ pad[1] ^ pad[2] ^ pad[3]) & 0u;  // keeps the pad live, changes nothing
     const uint32_t init = last ? cr.init_last : cr.init_full;
 #pragma unroll
     for (int q = 0; q < K + R; ++q) {
@@ -1605,6 +1660,11 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
       case 15: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM>), grid, block, 0, st, e, tabs); break;
       case 16: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 5, false, true>), grid, block, 0, st, e, tabs); break;
       case 17: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs); break;
+      case 40: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 64>), grid, block, 0, st, e, tabs); break;
+      case 41: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 192>), grid, block, 0, st, e, tabs); break;
+      case 42: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 192, 1>), grid, block, 0, st, e, tabs); break;
+      case 43: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 192, 2>), grid, block, 0, st, e, tabs); break;
+      case 44: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 0, 0, true>), grid, block, 0, st, e, tabs); break;
       default: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs); break;
     }
   } else {
@@ -1614,6 +1674,18 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
       case 13: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 1, kW>), grid, block, 0, st, e, tabs); break;
       case 14: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 2>), grid, block, 0, st, e, tabs); break;
       case 17: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, kW, false, true>), grid, block, 0, st, e, tabs); break;
+      case 40:
+        if constexpr (K == 10 && R == 4)
+          hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW, false, false, 64>), grid, block, 0, st, e, tabs);
+        break;
+      case 41:
+        if constexpr (K == 10 && R == 4)
+          hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW, false, false, 192>), grid, block, 0, st, e, tabs);
+        break;
+      case 44:
+        if constexpr (K == 10 && R == 4)
+          hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW, false, false, 0, 0, true>), grid, block, 0, st, e, tabs);
+        break;
       default: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW>), grid, block, 0, st, e, tabs); break;
     }
   }

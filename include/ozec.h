@@ -280,6 +280,29 @@ int ozec_crc_compose_windows_batch(int checksum_type, const uint32_t *d_crcs, in
                                    size_t num_cells, size_t num_windows, size_t bpc, size_t last_len,
                                    int crcs_big_endian, uint32_t *d_out, int out_big_endian, void *stream);
 
+/* ---- per-call counters (SURVEY §5 metrics: the reference's ECReconstructionMetrics.java:34-41 and
+ *      ContainerClientMetrics.java:41-42 count operations; a metrics2 source for the GPU coder publishes these).
+ *      Process-wide, per entry-point family: calls, data bytes of successful calls, failed calls and host time
+ *      spent inside the calls (for the asynchronous device entry points that is the enqueue time). --------- */
+#define OZEC_OP_ENCODE 0          /* ozec_encode (the JNI drop-in's encode)                                 */
+#define OZEC_OP_DECODE 1          /* ozec_decode                                                            */
+#define OZEC_OP_ENCODE_DEVICE 2   /* ozec_encode_device / ozec_encode_batch                                 */
+#define OZEC_OP_DECODE_DEVICE 3   /* ozec_decode_device / ozec_decode_batch                                 */
+#define OZEC_OP_FUSED 4           /* ozec_encode_crc_batch / _block_groups / ozec_reconstruct_crc_batch      */
+#define OZEC_OP_HOST_BATCH 5      /* ozec_encode_crc_host_batch                                             */
+#define OZEC_OP_CHECKSUM 6        /* ozec_checksum_windows / _verify / ozec_crc_update (host buffers)       */
+#define OZEC_OP_CHECKSUM_DEVICE 7 /* ozec_checksum_windows_batch / _device / ozec_checksum_verify_batch     */
+#define OZEC_OP_QUEUE 8           /* ozec_stripe_queue_submit / _flush / _wait                              */
+#define OZEC_NUM_OPS 9
+typedef struct {
+  uint64_t calls;
+  uint64_t bytes;   /* data bytes: k * len per stripe coded, the bytes checksummed */
+  uint64_t errors;
+  uint64_t host_ns;
+} ozec_op_stats;
+int ozec_stats(int op, ozec_op_stats *out);
+void ozec_stats_reset(void);
+
 /* ---- harness utilities ------------------------------------------------------------------------------- */
 /* process-wide tuning knobs for benchmarking: kernels ("grid", "gf_variant", "crc_variant", "crc_grid",
  * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_slots",

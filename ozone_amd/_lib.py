@@ -28,6 +28,13 @@ OZEC_CHECKSUM_CRC32 = 2
 OZEC_CHECKSUM_CRC32C = 3
 OZEC_MAX_K = 64
 OZEC_MAX_ROWS = 16
+OP_NAMES = ["encode", "decode", "encode_device", "decode_device", "fused", "host_batch", "checksum",
+            "checksum_device", "queue"]  # OZEC_OP_* order
+
+
+class OpStats(ctypes.Structure):
+    _fields_ = [("calls", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("errors", ctypes.c_uint64),
+                ("host_ns", ctypes.c_uint64)]
 
 
 class OzecLibraryError(RuntimeError):
@@ -123,6 +130,8 @@ _SIGS = {
     "ozec_crc_composer_free": (None, [c_voidp]),
     "ozec_crc_compose_windows_batch": (ctypes.c_int, [ctypes.c_int, c_voidp, c_i64, c_size, c_size, c_size, c_size,
                                                       ctypes.c_int, c_voidp, ctypes.c_int, c_voidp]),
+    "ozec_stats": (ctypes.c_int, [ctypes.c_int, c_voidp]),
+    "ozec_stats_reset": (None, []),
     "ozec_set_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
     "ozec_fill_splitmix64": (ctypes.c_int, [c_voidp, c_size, ctypes.c_uint64, ctypes.c_uint64, c_voidp]),
     "ozec_fill_splitmix64_cells": (ctypes.c_int, [c_voidp, c_i64, c_size, c_size, ctypes.c_uint64, ctypes.c_uint64,
@@ -176,3 +185,17 @@ def ptr_array(addrs):
 
 def int_array(vals):
     return (ctypes.c_int * max(1, len(vals)))(*vals)
+
+
+def stats():
+    """{op name: {calls, bytes, errors, host_ns}} from ozec_stats (per-call counters of the C ABI)."""
+    out = {}
+    for i, name in enumerate(OP_NAMES):
+        st = OpStats()
+        check(lib().ozec_stats(i, ctypes.byref(st)))
+        out[name] = {"calls": st.calls, "bytes": st.bytes, "errors": st.errors, "host_ns": st.host_ns}
+    return out
+
+
+def stats_reset():
+    lib().ozec_stats_reset()

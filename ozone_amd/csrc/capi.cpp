@@ -22,6 +22,7 @@
 #include "copy_pool.hpp"
 #include "kernels.hpp"
 #include "numa.hpp"
+#include "stats.hpp"
 #include "status.hpp"
 
 namespace {
@@ -35,6 +36,7 @@ thread_local std::string g_error;
 
 int fail(int code, const std::string &msg) {
   g_error = msg;
+  ozec::g_stat_failed = true;
   return code;
 }
 
@@ -203,6 +205,12 @@ int crc_type_of(int checksum_type, CrcType *t) {
 }  // namespace
 
 int ozec::set_error(int code, const std::string &msg) { return fail(code, msg); }
+
+namespace ozec {
+OpCounters g_stats[OZEC_NUM_OPS];
+thread_local int g_stat_depth = 0;
+thread_local bool g_stat_failed = false;
+}  // namespace ozec
 
 // ------------------------------------------------------------------------------------------------
 // coder handle
@@ -444,6 +452,7 @@ int ozec_coder_info(const ozec_coder *c, int *codec, int *k, int *p, int *is_dec
 // ---- encode ------------------------------------------------------------------------------------
 
 int ozec_encode(ozec_coder *enc, const uint8_t *const *inputs, uint8_t *const *outputs, size_t len) {
+  ozec::StatScope stat_(OZEC_OP_ENCODE, enc ? static_cast<uint64_t>(enc->k) * len : 0);
   if (int rc = check_open(enc, "encode")) return rc;
   if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
   if (!inputs || !outputs) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
@@ -468,6 +477,7 @@ int ozec_encode(ozec_coder *enc, const uint8_t *const *inputs, uint8_t *const *o
 
 int ozec_encode_device(ozec_coder *enc, const uint8_t *const *d_inputs, uint8_t *const *d_outputs, size_t len,
                        void *stream) {
+  ozec::StatScope stat_(OZEC_OP_ENCODE_DEVICE, enc ? static_cast<uint64_t>(enc->k) * len : 0);
   if (int rc = check_open(enc, "encode")) return rc;
   if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
   if (!d_inputs || !d_outputs) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
@@ -497,6 +507,7 @@ int ozec_encode_device(ozec_coder *enc, const uint8_t *const *d_inputs, uint8_t 
 int ozec_encode_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
                       uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes,
                       size_t len, void *stream) {
+  ozec::StatScope stat_(OZEC_OP_ENCODE_DEVICE, enc ? static_cast<uint64_t>(enc->k) * len * num_stripes : 0);
   if (int rc = check_open(enc, "encode")) return rc;
   if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
   if (len == 0 || num_stripes == 0) return OZEC_OK;
@@ -527,6 +538,7 @@ int ozec_encode_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_st
 
 int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased, int n_erased,
                 uint8_t *const *outputs, size_t len) {
+  ozec::StatScope stat_(OZEC_OP_DECODE, dec ? static_cast<uint64_t>(dec->k) * len : 0);
   if (int rc = check_open(dec, "decode")) return rc;
   if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
   if (!inputs) return fail(OZEC_EINVAL, "Invalid inputs length");
@@ -558,6 +570,7 @@ int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased
 
 int ozec_decode_device(ozec_coder *dec, const uint8_t *const *d_inputs, const int *erased, int n_erased,
                        uint8_t *const *d_outputs, size_t len, void *stream) {
+  ozec::StatScope stat_(OZEC_OP_DECODE_DEVICE, dec ? static_cast<uint64_t>(dec->k) * len : 0);
   if (int rc = check_open(dec, "decode")) return rc;
   if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
   if (!d_inputs) return fail(OZEC_EINVAL, "Invalid inputs length");
@@ -593,6 +606,7 @@ int ozec_decode_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_stripe_st
                       const int *present_units, int num_present, const int *erased, int n_erased, uint8_t *d_out,
                       int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes, size_t len,
                       void *stream) {
+  ozec::StatScope stat_(OZEC_OP_DECODE_DEVICE, dec ? static_cast<uint64_t>(dec->k) * len * num_stripes : 0);
   if (int rc = check_open(dec, "decode")) return rc;
   if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
   const int n_all = dec->k + dec->p;
@@ -658,6 +672,7 @@ static int make_crc_args(DevCtx *ctx, int checksum_type, const uint8_t *d_base, 
 
 int ozec_checksum_windows_batch(int checksum_type, const uint8_t *d_base, int64_t cell_stride, size_t num_cells,
                                 size_t len, size_t bpc, uint32_t *d_out, int big_endian, void *stream) {
+  ozec::StatScope stat_(OZEC_OP_CHECKSUM_DEVICE, static_cast<uint64_t>(len) * num_cells);
   if (len == 0 || num_cells == 0) return OZEC_OK;
   if (!d_base || !d_out) return fail(OZEC_EINVAL, "null buffer");
   DevCtx *ctx;
@@ -704,11 +719,13 @@ static int checksum_host(int checksum_type, const uint8_t *data, size_t len, siz
 
 int ozec_checksum_windows(int checksum_type, const uint8_t *data, size_t len, size_t bpc, uint32_t *out,
                           int big_endian) {
+  ozec::StatScope stat_(OZEC_OP_CHECKSUM, len);
   return checksum_host(checksum_type, data, len, bpc, out, big_endian, 0);
 }
 
 int ozec_checksum_verify(int checksum_type, const uint8_t *data, size_t len, size_t bpc, const uint32_t *expected,
                          size_t num_expected, size_t start_index, int64_t *mismatch_index) {
+  ozec::StatScope stat_(OZEC_OP_CHECKSUM, len);
   if (mismatch_index) *mismatch_index = -1;
   if (checksum_type == OZEC_CHECKSUM_NONE) return OZEC_OK;  // Checksum.java:250-253
   if (num_expected == 0) return fail(OZEC_EMISMATCH, "Original checksumData has no checksums");
@@ -734,6 +751,7 @@ int ozec_checksum_verify(int checksum_type, const uint8_t *data, size_t len, siz
 uint32_t ozec_crc_reset(int) { return 0xffffffffu; }
 
 int ozec_crc_update(int checksum_type, uint32_t *state, const uint8_t *data, size_t len) {
+  ozec::StatScope stat_(OZEC_OP_CHECKSUM, len);
   CrcType t;
   if (int rc = crc_type_of(checksum_type, &t)) return rc;
   if (!state) return fail(OZEC_EINVAL, "null state");
@@ -758,6 +776,7 @@ uint32_t ozec_crc_value(int, uint32_t state) { return ~state; }
 int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
                           uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes,
                           size_t len, int checksum_type, size_t bpc, uint32_t *d_crcs, int big_endian, void *stream) {
+  ozec::StatScope stat_(OZEC_OP_FUSED, enc ? static_cast<uint64_t>(enc->k) * len * num_stripes : 0);
   if (int rc = check_open(enc, "encode")) return rc;
   if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
   if (len == 0 || num_stripes == 0) return OZEC_OK;
@@ -807,6 +826,7 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
 int ozec_encode_crc_block_groups(ozec_coder *enc, uint8_t *d_base, int64_t group_stride, int64_t unit_stride,
                                  size_t num_groups, size_t stripes_per_group, size_t len, int checksum_type, size_t bpc,
                                  uint32_t *d_crcs, int big_endian, void *stream) {
+  ozec::StatScope stat_(OZEC_OP_FUSED, enc ? static_cast<uint64_t>(enc->k) * len * num_groups * stripes_per_group : 0);
   if (int rc = check_open(enc, "encode")) return rc;
   if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
   if (len == 0 || num_groups == 0 || stripes_per_group == 0) return OZEC_OK;
@@ -881,6 +901,7 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
                                int64_t in_unit_stride, uint8_t *h_out, int64_t out_stripe_stride,
                                int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
                                size_t bpc, uint32_t *h_crcs, int big_endian, size_t stripes_per_chunk) {
+  ozec::StatScope stat_(OZEC_OP_HOST_BATCH, enc ? static_cast<uint64_t>(enc->k) * len * num_stripes : 0);
   if (int rc = check_open(enc, "encode")) return rc;
   if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
   if (len == 0 || num_stripes == 0) return OZEC_OK;
@@ -1066,6 +1087,7 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
 int ozec_checksum_verify_batch(int checksum_type, const uint8_t *d_base, int64_t cell_stride, size_t num_cells,
                                size_t len, size_t bpc, const uint32_t *d_expected, int expected_big_endian,
                                int32_t *d_mismatch, void *stream) {
+  ozec::StatScope stat_(OZEC_OP_CHECKSUM_DEVICE, static_cast<uint64_t>(len) * num_cells);
   if (num_cells == 0) return OZEC_OK;
   if (!d_mismatch) return fail(OZEC_EINVAL, "null mismatch buffer");
   DevCtx *ctx;
@@ -1093,6 +1115,7 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
                                size_t len, int checksum_type, size_t bpc, const uint32_t *d_expected,
                                int expected_big_endian, uint32_t *d_out_crcs, int out_big_endian, int32_t *d_mismatch,
                                void *stream) {
+  ozec::StatScope stat_(OZEC_OP_FUSED, dec ? static_cast<uint64_t>(dec->k) * len * num_stripes : 0);
   if (int rc = check_open(dec, "decode")) return rc;
   if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
   const int n_all = dec->k + dec->p;
@@ -1408,6 +1431,27 @@ int ozec_crc_compose_windows_batch(int checksum_type, const uint32_t *d_crcs, in
   a.out = d_out;
   OZEC_HIP(ozec::launch_compose_windows(a, pick_stream(ctx, stream)));
   return OZEC_OK;
+}
+
+// ---- per-call counters -------------------------------------------------------------------------------
+
+int ozec_stats(int op, ozec_op_stats *out) {
+  if (op < 0 || op >= OZEC_NUM_OPS || !out) return fail(OZEC_EINVAL, "unknown op or null output");
+  const ozec::OpCounters &c = ozec::g_stats[op];
+  out->calls = c.calls.load(std::memory_order_relaxed);
+  out->bytes = c.bytes.load(std::memory_order_relaxed);
+  out->errors = c.errors.load(std::memory_order_relaxed);
+  out->host_ns = c.host_ns.load(std::memory_order_relaxed);
+  return OZEC_OK;
+}
+
+void ozec_stats_reset(void) {
+  for (auto &c : ozec::g_stats) {
+    c.calls.store(0);
+    c.bytes.store(0);
+    c.errors.store(0);
+    c.host_ns.store(0);
+  }
 }
 
 // ---- harness utilities ------------------------------------------------------------------------------

@@ -25,6 +25,7 @@
 #include "copy_pool.hpp"
 #include "kernels.hpp"
 #include "numa.hpp"
+#include "stats.hpp"
 #include "status.hpp"
 
 namespace {
@@ -270,6 +271,7 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
 
 int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, uint8_t *const *parity, size_t len,
                              uint32_t *crcs, uint64_t *ticket) {
+  ozec::StatScope stat_(OZEC_OP_QUEUE, q ? static_cast<uint64_t>(q->k) * len : 0);
   if (!q) return set_error(OZEC_EINVAL, "null queue");
   if (!data || !parity) return set_error(OZEC_EINVAL, "Invalid buffer found, not allowing null");
   for (int j = 0; j < q->k; ++j)
@@ -333,6 +335,7 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
 }
 
 int ozec_stripe_queue_flush(ozec_stripe_queue *q) {
+  ozec::StatScope stat_(OZEC_OP_QUEUE, 0);
   if (!q) return set_error(OZEC_EINVAL, "null queue");
   std::lock_guard<std::mutex> lk(q->mu);
   Batch &b = q->batches[q->cur];
@@ -344,6 +347,7 @@ int ozec_stripe_queue_flush(ozec_stripe_queue *q) {
 }
 
 int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket) {
+  ozec::StatScope stat_(OZEC_OP_QUEUE, 0);
   if (!q) return set_error(OZEC_EINVAL, "null queue");
   std::lock_guard<std::mutex> lk(q->mu);
   if (ticket >= q->next_ticket) return set_error(OZEC_EINVAL, "unknown ticket " + std::to_string(ticket));

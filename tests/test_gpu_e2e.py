@@ -203,3 +203,23 @@ def test_two_ranks_split_one_host_batch_on_one_device():
     v = raw[:S * (k + p) * n].reshape(S, k + p, n)
     crcs = raw[S * (k + p) * n:].view(np.uint32)
     _check(v, crcs, "rs", k, p, n, S, ck.ChecksumType.CRC32C, bpc)
+
+
+def test_per_call_counters_on_the_gpu_paths():
+    from ozone_amd import _lib
+    _lib.stats_reset()
+    k, p, n, S = 6, 3, 1 << 16, 5
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    d = cells(SEED, 830000, k, n)
+    out = [np.zeros(n, np.uint8) for _ in range(p)]
+    for _ in range(3):
+        e.encode(d, out)
+    buf, v, us = _batch(S, k, p, n, 831000)
+    crcs = np.zeros(S * (k + p) * (n // 16384), np.uint32)
+    e.encode_crc_host_batch(v.ctypes.data, (k + p) * us, us, v.ctypes.data + k * us, (k + p) * us, us, S, n,
+                            ck.ChecksumType.CRC32C, 16384, crcs, False, 2)
+    st = _lib.stats()
+    assert st["encode"]["calls"] == 3 and st["encode"]["bytes"] == 3 * k * n and st["encode"]["errors"] == 0
+    # the e2e batch counts once, as a host batch, not again for the fused launches it makes
+    assert st["host_batch"]["calls"] == 1 and st["host_batch"]["bytes"] == S * k * n
+    assert st["fused"]["calls"] == 0

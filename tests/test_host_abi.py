@@ -125,3 +125,25 @@ def test_last_error_is_thread_local_message():
     out = ctypes.c_void_p()
     assert L.lib().ozec_encoder_create(7, 3, 2, ctypes.byref(out)) == L.OZEC_EINVAL
     assert "codec" in L.last_error()
+
+
+def test_per_call_counters_record_calls_bytes_and_failures():
+    """ozec_stats (SURVEY §5 metrics): every entry-point family counts calls, data bytes of successful calls,
+    failures and host time; nested calls count once (the outermost)."""
+    import ctypes
+    from ozone_amd import _lib
+    L = _lib.lib()
+    _lib.stats_reset()
+    assert all(v == {"calls": 0, "bytes": 0, "errors": 0, "host_ns": 0} for v in _lib.stats().values())
+    out = (ctypes.c_uint32 * 4)()
+    data = (ctypes.c_uint8 * 64)()
+    assert L.ozec_checksum_windows(3, data, 64, 0, out, 0) == _lib.OZEC_EINVAL  # bpc 0: fails before the device
+    st = ctypes.c_uint32(0xFFFFFFFF)
+    assert L.ozec_crc_update(3, ctypes.byref(st), data, 0) == 0                # empty update: succeeds
+    s = _lib.stats()["checksum"]
+    assert s["calls"] == 2 and s["errors"] == 1 and s["bytes"] == 0 and s["host_ns"] > 0
+    assert L.ozec_encode(None, None, None, 4096) == _lib.OZEC_EINVAL
+    assert _lib.stats()["encode"]["errors"] == 1
+    with pytest.raises(Exception):
+        _lib.check(L.ozec_stats(99, None))
+    _lib.stats_reset()

@@ -7,13 +7,16 @@ import org.apache.ozone.erasurecode.rawcoder.OzecNative;
 /**
  * ChecksumByteBuffer (CM/ChecksumByteBuffer.java:32-44) whose updates run on the GPU through libozec
  * (ozec_crc_update: the raw CRC of the buffer is computed per 16 KiB window in parallel and combined with the
- * running register on the host, so every value equals CrcIntTable's / java.util.zip's).  Updates shorter than
- * {@code ozone.checksum.hip.min.bytes} (default 65536) stay on the CPU with the reflected byte table: below that
- * size a GPU round trip costs more than it saves (bench.py --workload stream).
+ * running register on the host, so every value equals CrcIntTable's / java.util.zip's).  Only updates of at least
+ * {@code ozone.checksum.hip.min.bytes} bytes go to the GPU, and by default none do: for a buffer in host memory one
+ * GPU round trip (staging copy, H2D, kernel, D2H) never beat one core's SSE4.2 CRC32C on MI355X at any size from
+ * 1 B to 16 MiB (bench.py --workload stream, profiles/r02/bench/stream_*.json).  The GPU's CRC pays where the
+ * bytes are on the device anyway: fused with encode (HipStripeQueue, ozec_encode_crc_*), in reconstruction and in
+ * the scanner's batched verify.  Smaller updates use the reflected byte table below.
  * CM/ = hadoop-hdds/common/src/main/java/org/apache/hadoop/ozone/common/
  */
 public final class HipChecksumByteBuffer implements ChecksumByteBuffer {
-  private static final int MIN_GPU_BYTES = Integer.getInteger("ozone.checksum.hip.min.bytes", 65536);
+  private static final int MIN_GPU_BYTES = Integer.getInteger("ozone.checksum.hip.min.bytes", Integer.MAX_VALUE);
   private static final int[] CRC32_TABLE = table(0xEDB88320);
   private static final int[] CRC32C_TABLE = table(0x82F63B78);
 

@@ -664,7 +664,7 @@ def test_host_path_chunked_pipeline(chunk, copy_threads):
             got = [int.from_bytes(b, "big") for b in cd.get_checksums()]
             assert got == [int(x) for x in oracle.crc_windows(oracle.CRC32C, data[2], bpc)]
     finally:
-        L.lib().ozec_set_tuning(b"host_chunk", 256 << 10)
+        L.lib().ozec_set_tuning(b"host_chunk", 4 << 20)
         L.lib().ozec_set_tuning(b"copy_threads", 3)
 
 

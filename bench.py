@@ -224,7 +224,7 @@ class Workload:
             self.k, self.p, self.S = k, p, S
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + p) * n
-            self.kernel = "encode_crc_g26<6,3> via ozec_stripe_queue (+H2D/D2H per cell)"
+            self.kernel = "encode_crc_lv<6,3> via ozec_stripe_queue (+H2D/D2H per cell)"
             self.config = {"workload": f"rs-6-3-1024k + CRC32C/16 KiB through the stripe queue (SURVEY 8(f) row 3) "
                                        f"from {'pinned' if pinned else 'pageable'} host cells, {S} stripes, "
                                        f"batches of 64", "stripes": S}
@@ -348,7 +348,7 @@ class Workload:
             self.mism = torch.empty(S, dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + 4) * n + S * (k + 4) * self.nwin * 4
-            self.kernel = "encode_crc_g26<10,4>"
+            self.kernel = "encode_crc_lv<10,4> (streamed inputs, fused.hip)"
             self.config = {"workload": "rs-10-4-1024k reconstruction: verify CRC32C of 10 read units + decode 4 + "
                                        f"CRC32C of rebuilt units {{{','.join(map(str, self.erased))}}}, {S} stripes, "
                                        "fused, device-resident",
@@ -361,7 +361,7 @@ class Workload:
             self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * units * n + S * units * self.nwin * 4
-            self.kernel = f"encode_crc_g26<{k},{p}>"
+            self.kernel = "encode_crc_g26<2,1>" if k == 2 else f"encode_crc_lv<{k},{p}> (streamed inputs, fused.hip)"
             wl = ("xor-2-1-1024k + CRC32C/16 KiB, stripe-major" if name == "c4s"
                   else "rs-6-3-1024k encode + CRC32C/16 KiB (the C5 kernel without PCIe)")
             self.config = {"workload": f"{wl}, {S} stripes, fused, device-resident", "codec": "xor" if k == 2 else "rs",
@@ -641,8 +641,14 @@ def cpu_baseline(workload, budget_s):
 # ------------------------------------------------------------------------------------------ live PMC traffic
 
 KERNEL_PAT = {"c1": "gf_code_vec<3, 2", "c2": "gf_code_vec<6, 3", "c3": "gf_code_vec<10, 4",
-              "c3r": "encode_crc_g26<10, 4", "c4": "encode_crc_g26<2, 1", "c4s": "encode_crc_g26<2, 1",
-              "c5dev": "encode_crc_g26<6, 3", "crc": "crc_windows_g26s", "verify": "crc_windows_g26s"}
+              "c3r": ("encode_crc_lv<10, 4", "encode_crc_g26<10, 4"), "c4": "encode_crc_g26<2, 1",
+              "c4s": "encode_crc_g26<2, 1", "c5dev": ("encode_crc_lv<6, 3", "encode_crc_g26<6, 3"),
+              "crc": "crc_windows_g26s", "verify": "crc_windows_g26s"}
+
+
+def _kernel_match(pat, name):
+    """pat: a name fragment, or a tuple of fragments (the streamed-input or the per-window fused kernel)."""
+    return any(p in name for p in (pat if isinstance(pat, tuple) else (pat,)))
 
 
 def pmc_traffic(args, alg_bytes):
@@ -675,14 +681,14 @@ def pmc_traffic(args, alg_bytes):
             files = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs]
             if tag == "stats":
                 st = [f for f in files if f.endswith("kernel_stats.csv")]
-                rows = [row for row in csv.DictReader(open(st[0])) if pat in row["Name"]]
+                rows = [row for row in csv.DictReader(open(st[0])) if _kernel_match(pat, row["Name"])]
                 out["rocprof_kernel"] = rows[0]["Name"]
                 out["rocprof_avg_ms"] = round(float(rows[0]["AverageNs"]) / 1e6, 4)
                 out["rocprof_calls"] = int(rows[0]["Calls"])
             else:
                 cc = [f for f in files if f.endswith("counter_collection.csv")]
                 vals = [float(row["Counter_Value"]) for row in csv.DictReader(open(cc[0]))
-                        if pat in row["Kernel_Name"] and row["Counter_Name"] == tag]
+                        if _kernel_match(pat, row["Kernel_Name"]) and row["Counter_Name"] == tag]
                 if not vals:
                     return None, {"error": f"no {tag} rows for kernel {pat}"}
                 out[tag + "_KiB"] = sum(vals) / len(vals)

@@ -1,0 +1,231 @@
+// Fused encode (or reconstruct) + CRC for full windows, built for occupancy: "streamed inputs".
+//
+// The per-window fused kernel in kernels.hip (encode_crc_g26) loads all K input blocks of a step at once and
+// keeps every input, every parity accumulator and the coefficient tables of the step live together: 123 VGPRs
+// for rs-6-3 (4 waves per SIMD) and 160 for rs-10-4 reconstruction (3 waves).  Its time is VALU + LDS issue
+// (DESIGN §2.3), and on gfx950 the VALU issue rate of a SIMD grows with the waves it can pick from (integer ops
+// at 4 waves: 2.2-3.4 cycles per wave-instruction, at 8 waves 1.6-2.7; profiles/r01/session4/valu_rate.log).
+//
+// This kernel does the same arithmetic per 16-B block with a live set of about half that size, so the SIMDs get
+// 5-8 waves:
+//   * inputs stream through a ring of NB block registers: input j of step t is consumed (its CRC, then its GF
+//     contributions to the R parity accumulators) while the loads of the next NB - 1 (step, input) slots are in
+//     flight; one input block is live at a time, not K (the look-ahead past a window's end reads nothing: it is
+//     addressed outside the input descriptor's range, and out-of-range buffer loads return zeros without a memory
+//     access);
+//   * the GF tables of a coefficient come from LDS as one ds_read_b128 broadcast ({lo0, lo1, mid0, mid1}) plus one
+//     ds_read_b128 holding the `top` tables of input j for all R outputs -- nothing from the kernarg segment, so
+//     no SGPR spills into VGPR lanes;
+//   * parity dwords accumulate in three-input XOR chains (1.5 VALU per coefficient and dword) across the K inputs.
+// Windows must be full (len % bpc == 0) and a whole number of D-step groups (bpc % (1024 D) == 0): no virtual
+// blocks, so loads and stores are unconditional (a per-lane predicate makes the compiler wait for every load in
+// flight at every step).  The load cursor runs NB - 1 slots ahead of the compute cursor.
+//
+// Same results as encode_crc_g26 bit for bit (same G26 tables, same per-lane folding, same lane tree); the
+// launcher (launch_encode_crc) picks this kernel for the shapes and geometries above and falls back otherwise.
+#include "device.hpp"
+
+namespace ozec {
+namespace {
+
+// K inputs, R outputs, D steps per CRC group, NB ring slots, WPB waves per block, WAVES minimum waves per SIMD,
+// ACC: parity dwords in plain accumulators (1 VGPR, 2 VALU per coefficient and dword) instead of XOR chains
+// (2 VGPRs, 1.5 VALU)
+template <int K, int R, int D, int NB, int WPB, int WAVES, bool ACC = false>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_lv(
+    const EncCrcArgs e) {
+  static_assert(R >= 1 && R <= 4, "the packed top tables hold up to 4 outputs");
+  static_assert((D * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(D)];
+  __shared__ __attribute__((aligned(16))) uint4 s_q[K * R];  // {lo0, lo1, mid0, mid1} of coefficient r*K + j
+  __shared__ __attribute__((aligned(16))) uint4 s_top[K];    // top tables of input j for outputs 0..3
+  const CodeArgs &a = e.code;
+  const CrcArgs &cr = e.crc;
+  load_tables(s_t, cr.g26[g26_slot(1, D)], g26_words(D));
+  for (int t = threadIdx.x; t < K * R; t += blockDim.x) {
+    const PermTab p = make_tab(a.coef[t]);
+    s_q[t] = make_uint4(p.lo0, p.lo1, p.mid0, p.mid1);
+  }
+  for (int j = threadIdx.x; j < K; j += blockDim.x) {
+    uint32_t tp[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < R; ++r) tp[r] = make_tab(a.coef[r * K + j]).top;
+    s_top[j] = make_uint4(tp[0], tp[1], tp[2], tp[3]);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwin = cr.nwin;
+  const int64_t units = a.nstripes * nwin;
+  const int32_t T = static_cast<int32_t>(cr.bpc >> 10);  // steps per window
+  const int32_t G = T / D;                                // groups per window
+  const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
+  int64_t off_max = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
+  const uint32_t in_extent = static_cast<uint32_t>(off_max + cr.bpc);
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  for (int64_t u = bid * WPB + wave; u < units; u += static_cast<int64_t>(gridDim.x) * WPB) {
+    const int64_t s = u / nwin;
+    const int64_t w = u - s * nwin;
+    // the input descriptor's range ends with the last unit's window (rebase32: in_off + bpc < 2^31); the look-ahead
+    // loads past the window's last step get voffset + 2^31, outside the range: they return zeros and cost no
+    // memory traffic (no 32-bit wrap: 2^31 + 1008 + in_off < 2^32)
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
+    // step part of the address in a VGPR (one add per step), unit offset in soffset: K SGPRs in all, instead of
+    // one SGPR per (step, unit) slot of the unrolled group
+    auto vstep = [&](int32_t t) { return voff + (t < T ? static_cast<uint32_t>(t) * 1024u : 0x80000000u); };
+    auto load = [&](uint32_t vo, int j) {
+      const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, vo, static_cast<int>(a.in_off[j]), 2);
+      return make_uint4(d[0], d[1], d[2], d[3]);
+    };
+    uint32_t S[K + R];
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) S[q] = 0;
+    uint4 ring[NB];
+#pragma unroll
+    for (int i = 0; i + 1 < NB; ++i) ring[i] = load(vstep(i / K), i % K);
+    for (int32_t g = 0; g < G; ++g) {
+#pragma unroll
+      for (int rr = 0; rr < D; ++rr) {
+        const int32_t t = g * D + rr;
+        const uint32_t *tab = s_t + (D - 1 - rr) * kG26Set;
+        const uint32_t vcur = vstep(t), vnext = vstep(t + 1);
+        XorChain ch[R][4];
+        uint32_t acc[R][4];
+        if constexpr (ACC) {
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[r][c] = 0;
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int ii = rr * K + j;  // slot within the group
+          const int ahead = ii + NB - 1;
+          static_assert(NB - 1 <= K, "look-ahead of at most one step");
+          ring[ahead % NB] = load(ahead / K == rr ? vcur : vnext, ahead % K);
+          const uint4 x = ring[ii % NB];
+          asm volatile("" ::: "memory");  // keep this input's LDS table reads here
+          S[j] ^= g26_block<true>(tab, x);
+          __builtin_amdgcn_sched_barrier(0);
+          const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+          Sel sl[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) sl[c] = make_sel(xw[c]);
+          const uint4 tops = s_top[j];
+          const uint32_t top[4] = {tops.x, tops.y, tops.z, tops.w};
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const uint4 q = s_q[r * K + j];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const uint32_t plo = perm_vv(q.y, q.x, sl[c].s0), pmid = perm_vv(q.w, q.z, sl[c].s1),
+                             ptop = perm_vv(top[r], top[r], sl[c].s2);
+              if constexpr (ACC) {
+                acc[r][c] = xor3(acc[r][c], plo, pmid) ^ ptop;
+              } else {
+                ch[r][c].push(plo);
+                ch[r][c].push(pmid);
+                ch[r][c].push(ptop);
+              }
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint4 p = ACC ? make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3])
+                              : make_uint4(ch[r][0].get(), ch[r][1].get(), ch[r][2].get(), ch[r][3].get());
+          __attribute__((ext_vector_type(4))) unsigned int d = {p.x, p.y, p.z, p.w};
+          __builtin_amdgcn_raw_buffer_store_b128(d, rout, vcur, static_cast<int>(a.out_off[r]), 2);
+          store_data_hold(p);
+          S[K + r] ^= g26_block<true>(tab, p);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (g + 1 < G) {
+#pragma unroll
+        for (int q = 0; q < K + R; ++q) S[q] = g5_shift(s_t + g26_gshift(D), S[q]);
+      }
+    }
+    const bool last = w == nwin - 1;
+    const uint32_t init = last ? cr.init_last : cr.init_full;
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) {
+      const uint32_t v = g5_lane_tree(s_t + g26_tree(D) - kG5Tree, S[q], lane);
+      if (lane == q) {
+        if (!e.verify) {
+          cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+        } else if (q >= K) {
+          cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+        } else if (cr.expected) {
+          const int64_t idx = (s * e.exp_units + e.in_unit[q]) * nwin + w;
+          const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
+          if (crc_finish(v, init, 0, 0) != ex) atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
+        }
+      }
+    }
+  }
+}
+
+template <int K, int R, int D, int NB, int WPB, int WAVES, bool ACC = false>
+hipError_t launch_lv(const EncCrcArgs &e, hipStream_t st) {
+  if constexpr ((D * K) % NB != 0) {
+    return launch_lv<K, R, D, 2, WPB, WAVES, ACC>(e, st);  // ring must divide the unrolled group
+  } else {
+    const int64_t units = e.code.nstripes * e.crc.nwin;
+    const int64_t blocks = (units + WPB - 1) / WPB;
+    const int64_t g = g_tune.crc_grid > 0 ? std::min<int64_t>(g_tune.crc_grid, blocks) : blocks;
+    hipLaunchKernelGGL((encode_crc_lv<K, R, D, NB, WPB, WAVES, ACC>),
+                       dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, e);
+    return hipGetLastError();
+  }
+}
+
+// variant (g_tune.crc_variant): 0 default; 50-59 step group / ring / occupancy / accumulator A/B
+template <int K, int R>
+hipError_t launch_lv_kr(const EncCrcArgs &e, hipStream_t st, int v) {
+  switch (v) {
+    case 51: return launch_lv<K, R, 4, 4, 4, 5>(e, st);
+    case 52: return launch_lv<K, R, 4, 4, 4, 6>(e, st);
+    case 53: return launch_lv<K, R, 4, 2, 4, 6>(e, st);
+    case 54: return launch_lv<K, R, 2, 4, 4, 5>(e, st);
+    case 55: return launch_lv<K, R, 2, 2, 4, 5>(e, st);
+    case 56: return launch_lv<K, R, 2, 2, 4, 6>(e, st);
+    case 57: return launch_lv<K, R, 2, 4, 4, 6, true>(e, st);
+    case 58: return launch_lv<K, R, 4, 2, 4, 6, true>(e, st);
+    case 59: return launch_lv<K, R, 2, 2, 4, 7, true>(e, st);
+    default: break;
+  }
+  // measured on MI355X (profiles/r02/lv/ab_variants_lv3.log): rs-6-3 ring of 2 at 6 waves per SIMD (76 VGPRs),
+  // rs-10-4 ring of 4 at 5 waves (95 VGPRs); both with groups of D = 4 steps
+  if constexpr (K + R >= 12) return launch_lv<K, R, 4, 4, 4, 5>(e, st);
+  else return launch_lv<K, R, 4, 2, 4, 6>(e, st);
+}
+
+}  // namespace
+
+bool encode_crc_lv_supported(const EncCrcArgs &e) {
+  const CodeArgs &a = e.code;
+  if (a.all_ones && a.rows == 1) return false;  // the XOR codec has its own register shortcut (encode_crc_g26 XORC)
+  const bool shape = (a.k == 6 && (a.rows == 3 || a.rows == 2)) || (a.k == 10 && a.rows >= 1 && a.rows <= 4) ||
+                     (a.k == 3 && a.rows == 2);
+  return shape && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && a.len % e.crc.bpc == 0;
+}
+
+hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
+  const int k = e.code.k, r = e.code.rows;
+  if (k == 6 && r == 3) return launch_lv_kr<6, 3>(e, st, v);
+  if (k == 6 && r == 2) return launch_lv_kr<6, 2>(e, st, v);
+  if (k == 3 && r == 2) return launch_lv_kr<3, 2>(e, st, v);
+  if (k == 10 && r == 4) return launch_lv_kr<10, 4>(e, st, v);
+  if (k == 10 && r == 3) return launch_lv_kr<10, 3>(e, st, v);
+  if (k == 10 && r == 2) return launch_lv_kr<10, 2>(e, st, v);
+  if (k == 10 && r == 1) return launch_lv_kr<10, 1>(e, st, v);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace ozec

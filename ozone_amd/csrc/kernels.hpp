@@ -147,5 +147,8 @@ hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t nc
                                   uint64_t first_stream, hipStream_t stream);
 // true when the fused kernel supports this (k, rows) pair with the given geometry
 bool encode_crc_supported(const CodeArgs &a, int64_t bpc);
+// the streamed-input fused kernel (fused.hip): RS shapes with full windows, bpc % 4096 == 0; `e` already rebased
+bool encode_crc_lv_supported(const EncCrcArgs &e);
+hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant);
 
 }  // namespace ozec

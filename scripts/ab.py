@@ -12,7 +12,10 @@ wl_name, key, vals = sys.argv[1], sys.argv[2].encode(), [int(v) for v in sys.arg
 rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 5
 torch.cuda.set_device(0)
 lib = L.lib()
-wl = bench.Workload(wl_name, 0, 0)
+wl = bench.Workload(wl_name, 0, 1, None)
+if os.environ.get("ZERO") and hasattr(wl, "units"):  # all-zero data cells: separates data-dependent power/clock effects
+    wl.units.zero_()
+    torch.cuda.synchronize()
 
 
 def outputs():

@@ -30,7 +30,7 @@ def outputs(w):
     return outs
 
 for name in wls:
-    w = bench.Workload(name, 0, 0)
+    w = bench.Workload(name, 0, 1, None)
     setk(combos[0]); w.step(); torch.cuda.synchronize(); ref = outputs(w)
     for c in combos[1:]:
         setk(c); w.step(); torch.cuda.synchronize()

@@ -10,6 +10,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 from ozone_amd import checksum as ck  # noqa: E402
+from ozone_amd import _lib as L  # noqa: E402
 from ozone_amd import rawcoder as rc  # noqa: E402
 
 DEV = "cuda:0"
@@ -64,7 +65,19 @@ def _stripe_units(codec, k, p, n, S, first):
     ("rs", 5, 2, [0, 6], 1 << 16, 16384),         # unfused fallback (shape not instantiated)
     ("rs", 6, 3, [0, 2, 7], 50000, 1000),         # unfused fallback (bpc not a multiple of 16)
 ])
-def test_reconstruct_crc_batch(codec, k, p, erased, n, bpc):
+@pytest.mark.parametrize("variant", [0, 49, 54])
+def test_reconstruct_crc_batch(codec, k, p, erased, n, bpc, variant):
+    """Fused reconstruction (verify + decode + CRC) vs the oracle: default (streamed-input kernel where it applies),
+    49 (the per-window kernel), 54 (streamed-input, 8 waves per SIMD)."""
+    lib = L.lib()
+    assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+    try:
+        _reconstruct_case(codec, k, p, erased, n, bpc)
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+
+
+def _reconstruct_case(codec, k, p, erased, n, bpc):
     S = 4
     units = _stripe_units(codec, k, p, n, S, 70000)
     ctype, otype = ck.ChecksumType.CRC32C, oracle.CRC32C

@@ -347,11 +347,13 @@ def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
             assert (crcs[s, u] == oracle.crc_windows(otype, units[u], bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [11, 12, 13, 14, 15, 16, 17])
-@pytest.mark.parametrize("n,bpc,S", [(1 << 18, 16384, 3), (50000, 4096, 2)])
+@pytest.mark.parametrize("variant", [11, 12, 13, 14, 15, 16, 17, 49, 51, 52, 53, 54, 55, 56, 57, 58])
+@pytest.mark.parametrize("n,bpc,S", [(1 << 18, 16384, 3), (50000, 4096, 2), (1 << 17, 4096, 2), (1 << 17, 65536, 3)])
 def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
-    """Every tuning variant of the rs-6-3 fused encode + CRC32C kernel (D = 4, prefetch, table placements,
-    CRC lookups in two fenced halves at 4 and 5 waves per SIMD) is bit-exact against the oracle."""
+    """Every tuning variant of the rs-6-3 fused encode + CRC32C kernel (per-window kernel: D = 4, prefetch, table
+    placements, CRC lookups in two fenced halves at 4 and 5 waves per SIMD; 49 pins it; streamed-input kernel
+    (fused.hip) at 4-8 waves per SIMD, rings of 2 and 4 blocks, D = 2 and 4: 51-58) is bit-exact against the
+    oracle.  Geometries the streamed kernel does not take (a short last window) go to the per-window kernel."""
     lib = L.lib()
     k, p = 6, 3
     data = np.stack([np.stack(cells(SEED, 52000 + s * k, k, n)) for s in range(S)])
@@ -373,8 +375,8 @@ def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
             assert (crcs[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [0, 11, 17])
-@pytest.mark.parametrize("k,p", [(10, 4), (6, 2), (3, 2)])
+@pytest.mark.parametrize("variant", [0, 11, 17, 49, 51, 54, 55, 57])
+@pytest.mark.parametrize("k,p", [(10, 4), (6, 2), (3, 2), (10, 3), (10, 2), (10, 1)])
 def test_encode_crc_other_shapes_variants_vs_oracle(variant, k, p):
     """Fused encode + CRC32C variants of the other RS shapes (D = 2 default, D = 4, D = 4 with fenced halves)."""
     lib = L.lib()

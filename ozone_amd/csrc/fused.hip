@@ -28,10 +28,18 @@
 namespace ozec {
 namespace {
 
+__device__ __forceinline__ uint32_t and_v(uint32_t a, uint32_t m) {
+  uint32_t d;
+  asm("v_and_b32 %0, %1, %2" : "=v"(d) : "v"(m), "v"(a));
+  return d;
+}
+
 // K inputs, R outputs, D steps per CRC group, NB ring slots, WPB waves per block, WAVES minimum waves per SIMD,
 // ACC: parity dwords in plain accumulators (1 VGPR, 2 VALU per coefficient and dword) instead of XOR chains
-// (2 VGPRs, 1.5 VALU)
-template <int K, int R, int D, int NB, int WPB, int WAVES, bool ACC = false>
+// (2 VGPRs, 1.5 VALU); OPT bit 0: all 12 permutes of a coefficient before their XORs (no consumer right behind its
+// producer: gfx950 pads v_perm -> v_bitop3 back-to-back with s_nop), bit 1: GF selector masks held in VGPRs
+// (plain VOP2 AND instead of the literal-operand form)
+template <int K, int R, int D, int NB, int WPB, int WAVES, bool ACC = false, int OPT = 0>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_lv(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "the packed top tables hold up to 4 outputs");
@@ -61,6 +69,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   const int32_t T = static_cast<int32_t>(cr.bpc >> 10);  // steps per window
   const int32_t G = T / D;                                // groups per window
   const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
+  uint32_t m7 = 0x07070707u, m3 = 0x03030303u;
+  if constexpr (OPT & 2) {  // materialised once, live in VGPRs
+    asm volatile("v_mov_b32 %0, 0x7070707" : "=v"(m7));
+    asm volatile("v_mov_b32 %0, 0x3030303" : "=v"(m3));
+  }
   int64_t off_max = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
@@ -114,12 +127,34 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
           const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
           Sel sl[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) sl[c] = make_sel(xw[c]);
+          for (int c = 0; c < 4; ++c) {
+            if constexpr (OPT & 2) {
+              sl[c].s0 = and_v(xw[c], m7);
+              sl[c].s1 = and_v(xw[c] >> 3, m7);
+              sl[c].s2 = and_v(xw[c] >> 6, m3);
+            } else {
+              sl[c] = make_sel(xw[c]);
+            }
+          }
           const uint4 tops = s_top[j];
           const uint32_t top[4] = {tops.x, tops.y, tops.z, tops.w};
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             const uint4 q = s_q[r * K + j];
+            if constexpr ((OPT & 1) && !ACC) {
+              uint32_t pp[4][3];
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {
+                pp[c][0] = perm_vv(q.y, q.x, sl[c].s0);
+                pp[c][1] = perm_vv(q.w, q.z, sl[c].s1);
+                pp[c][2] = perm_vv(top[r], top[r], sl[c].s2);
+              }
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) ch[r][c].push(pp[c][i]);
+              continue;
+            }
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
               const uint32_t plo = perm_vv(q.y, q.x, sl[c].s0), pmid = perm_vv(q.w, q.z, sl[c].s1),
@@ -171,15 +206,15 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   }
 }
 
-template <int K, int R, int D, int NB, int WPB, int WAVES, bool ACC = false>
+template <int K, int R, int D, int NB, int WPB, int WAVES, bool ACC = false, int OPT = 0>
 hipError_t launch_lv(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((D * K) % NB != 0) {
-    return launch_lv<K, R, D, 2, WPB, WAVES, ACC>(e, st);  // ring must divide the unrolled group
+    return launch_lv<K, R, D, 2, WPB, WAVES, ACC, OPT>(e, st);  // ring must divide the unrolled group
   } else {
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     const int64_t g = g_tune.crc_grid > 0 ? std::min<int64_t>(g_tune.crc_grid, blocks) : blocks;
-    hipLaunchKernelGGL((encode_crc_lv<K, R, D, NB, WPB, WAVES, ACC>),
+    hipLaunchKernelGGL((encode_crc_lv<K, R, D, NB, WPB, WAVES, ACC, OPT>),
                        dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, e);
     return hipGetLastError();
   }
@@ -193,17 +228,18 @@ hipError_t launch_lv_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 52: return launch_lv<K, R, 4, 4, 4, 6>(e, st);
     case 53: return launch_lv<K, R, 4, 2, 4, 6>(e, st);
     case 54: return launch_lv<K, R, 2, 4, 4, 5>(e, st);
-    case 55: return launch_lv<K, R, 2, 2, 4, 5>(e, st);
-    case 56: return launch_lv<K, R, 2, 2, 4, 6>(e, st);
-    case 57: return launch_lv<K, R, 2, 4, 4, 6, true>(e, st);
-    case 58: return launch_lv<K, R, 4, 2, 4, 6, true>(e, st);
-    case 59: return launch_lv<K, R, 2, 2, 4, 7, true>(e, st);
+    case 55: return launch_lv<K, R, 4, 2, 4, 5>(e, st);
+    case 56: return launch_lv<K, R, 4, 4, 4, 5, false, 1>(e, st);
+    case 57: return launch_lv<K, R, 4, 4, 4, 5, false, 2>(e, st);
+    case 58: return launch_lv<K, R, 4, 4, 4, 5, false, 3>(e, st);
+    case 59: return launch_lv<K, R, 4, 2, 4, 6, false, 3>(e, st);
     default: break;
   }
   // measured on MI355X (profiles/r02/lv/ab_variants_lv3.log): rs-6-3 ring of 2 at 6 waves per SIMD (76 VGPRs),
   // rs-10-4 ring of 4 at 5 waves (95 VGPRs); both with groups of D = 4 steps
-  if constexpr (K + R >= 12) return launch_lv<K, R, 4, 4, 4, 5>(e, st);
-  else return launch_lv<K, R, 4, 2, 4, 6>(e, st);
+  // (profiles/r02/lv/ab_opt_lv5.log: permutes before their XORs +0.3 %, selector masks in VGPRs +0.6 %)
+  if constexpr (K + R >= 12) return launch_lv<K, R, 4, 4, 4, 5, false, 1>(e, st);
+  else return launch_lv<K, R, 4, 2, 4, 6, false, 3>(e, st);
 }
 
 }  // namespace

@@ -37,7 +37,9 @@ namespace {
 // (uniform-address broadcasts), which keeps large schemas (rs-10-4 decode) inside 128 VGPRs.
 // VPT vectors of 16 B per lane per unit (a unit = VPT x 4 KiB of every cell of one stripe); LAUX/SAUX are the
 // cache-policy bits of the loads/stores (0 = default, 2 = nt).
-template <int K, int R, bool SREG, int VPT, int LAUX, int SAUX>
+// OPT bit 0: parity dwords in three-input XOR chains across the K inputs (1.5 VALU per coefficient and dword instead
+// of 2); bit 1: selector masks held in VGPRs (plain VOP2 AND instead of the literal-operand form).
+template <int K, int R, bool SREG, int VPT, int LAUX, int SAUX, int OPT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_WAVES, 8))) void gf_code_vec(
     const CodeArgs a, const TabArgs<K * R> tabs) {
   __shared__ __attribute__((aligned(16))) uint32_t s_w[5][K * R];
@@ -54,6 +56,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
     }
   }
 
+  uint32_t m7 = 0x07070707u, m3 = 0x03030303u;
+  if constexpr (OPT & 2) {  // materialised once, live in VGPRs
+    asm volatile("v_mov_b32 %0, 0x7070707" : "=v"(m7));
+    asm volatile("v_mov_b32 %0, 0x3030303" : "=v"(m3));
+  }
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
   constexpr uint32_t kChunk = kBlock * VPT;
   const uint32_t cpc = (nvec + kChunk - 1) / kChunk;  // units per cell
@@ -83,28 +90,54 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
       const uint32_t v = v0 + q * kBlock;
       if (v >= nvec) continue;
       uint4 acc[R];
+      XorChain ch[R][4];
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const Sel sx = make_sel(x[q][j].x), sy = make_sel(x[q][j].y), sz = make_sel(x[q][j].z),
-                  sw = make_sel(x[q][j].w);
+        auto sel = [&](uint32_t w) {
+          if constexpr (OPT & 2) {
+            Sel s;
+            asm("v_and_b32 %0, %1, %2" : "=v"(s.s0) : "v"(m7), "v"(w));
+            asm("v_and_b32 %0, %1, %2" : "=v"(s.s1) : "v"(m7), "v"(w >> 3));
+            asm("v_and_b32 %0, %1, %2" : "=v"(s.s2) : "v"(m3), "v"(w >> 6));
+            return s;
+          } else {
+            return make_sel(w);
+          }
+        };
+        const Sel sl[4] = {sel(x[q][j].x), sel(x[q][j].y), sel(x[q][j].z), sel(x[q][j].w)};
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int t = r * K + j;
+          if constexpr (OPT & 1) {
+            uint32_t lo0, lo1, mid0, mid1, top;
+            if constexpr (SREG) {
+              lo0 = vlo0[t], mid0 = vmid0[t], lo1 = tabs.w[t][1], mid1 = tabs.w[t][3], top = tabs.w[t][4];
+            } else {
+              lo0 = s_w[0][t], lo1 = s_w[1][t], mid0 = s_w[2][t], mid1 = s_w[3][t], top = s_w[4][t];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              ch[r][c].push(SREG ? perm_sv(lo1, lo0, sl[c].s0) : perm_vv(lo1, lo0, sl[c].s0));
+              ch[r][c].push(SREG ? perm_sv(mid1, mid0, sl[c].s1) : perm_vv(mid1, mid0, sl[c].s1));
+              ch[r][c].push(SREG ? perm_top_s(top, sl[c].s2) : perm_vv(top, top, sl[c].s2));
+            }
+            continue;
+          }
           uint4 m;
           if constexpr (SREG) {
             const RegTab tb{vlo0[t], vmid0[t], tabs.w[t][1], tabs.w[t][3], tabs.w[t][4]};
-            m.x = gf_mul4_reg(tb, sx);
-            m.y = gf_mul4_reg(tb, sy);
-            m.z = gf_mul4_reg(tb, sz);
-            m.w = gf_mul4_reg(tb, sw);
+            m.x = gf_mul4_reg(tb, sl[0]);
+            m.y = gf_mul4_reg(tb, sl[1]);
+            m.z = gf_mul4_reg(tb, sl[2]);
+            m.w = gf_mul4_reg(tb, sl[3]);
           } else {
             const PermTab tb{s_w[0][t], s_w[1][t], s_w[2][t], s_w[3][t], s_w[4][t]};
-            m.x = gf_mul4_lds(tb, sx);
-            m.y = gf_mul4_lds(tb, sy);
-            m.z = gf_mul4_lds(tb, sz);
-            m.w = gf_mul4_lds(tb, sw);
+            m.x = gf_mul4_lds(tb, sl[0]);
+            m.y = gf_mul4_lds(tb, sl[1]);
+            m.z = gf_mul4_lds(tb, sl[2]);
+            m.w = gf_mul4_lds(tb, sl[3]);
           }
           acc[r].x ^= m.x;
           acc[r].y ^= m.y;
@@ -113,6 +146,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
         }
         // bound live ranges: input j's selectors (and, in LDS mode, its table reads) stay in this group
         __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (OPT & 1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = make_uint4(ch[r][0].get(), ch[r][1].get(), ch[r][2].get(), ch[r][3].get());
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -992,7 +1029,7 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix64(uint8_t *base, int64_t
   }
 }
 
-template <int K, int R, int VPT, int LAUX, int SAUX>
+template <int K, int R, int VPT, int LAUX, int SAUX, int OPT = 0>
 hipError_t launch_krv(const CodeArgs &a, hipStream_t st, int64_t default_grid) {
   constexpr bool kSreg = K * R <= 18;
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
@@ -1000,7 +1037,7 @@ hipError_t launch_krv(const CodeArgs &a, hipStream_t st, int64_t default_grid) {
   const TabArgs<K * R> tabs = host_tabs<K * R>(a);
   int64_t grid = g_tune.grid > 0 ? g_tune.grid : default_grid;
   grid = std::max<int64_t>(1, std::min<int64_t>(grid, units));
-  hipLaunchKernelGGL((gf_code_vec<K, R, kSreg, VPT, LAUX, SAUX>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0,
+  hipLaunchKernelGGL((gf_code_vec<K, R, kSreg, VPT, LAUX, SAUX, OPT>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0,
                      st, a, tabs);
   return hipGetLastError();
 }
@@ -1023,6 +1060,9 @@ hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
     case 8: return launch_krv<K, R, 1, 2, 18>(a, st, kAll);   // sc1 nt stores
     case 9: return launch_krv<K, R, 1, 18, 18>(a, st, kAll);  // sc1 nt loads and stores
     case 10: return launch_krv<K, R, 1, 16, 2>(a, st, kAll);  // sc1 loads
+    case 11: return launch_krv<K, R, 1, 2, 2, 1>(a, st, kAll);  // XOR chains
+    case 12: return launch_krv<K, R, 1, 2, 2, 2>(a, st, kAll);  // selector masks in VGPRs
+    case 13: return launch_krv<K, R, 1, 2, 2, 3>(a, st, kAll);  // both
     default: break;
   }
   return launch_krv<K, R, 1, 2, 2>(a, st, kAll);

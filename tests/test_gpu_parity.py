@@ -143,6 +143,34 @@ def test_decode_batch_vs_oracle(k, p, erased):
         assert all((got[s, i] == units[s, e]).all() for i, e in enumerate(erased)), s
 
 
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 11, 12, 13])
+@pytest.mark.parametrize("k,p,erased", [(6, 3, None), (3, 2, None), (10, 4, [0, 1, 2, 3]), (10, 4, [1, 4, 10, 13]),
+                                        (6, 3, [0, 2, 7]), (10, 4, [0, 13])])
+def test_coding_kernel_variants_vs_oracle(variant, k, p, erased):
+    """Every coding-kernel tuning variant (gf_variant: chunk size, cache policy, XOR chains, selector masks in VGPRs)
+    is bit-exact against the oracle for encode (erased None) and decode shapes, with a ragged tail."""
+    lib = L.lib()
+    n, S = 3 * 4096 + 48, 5
+    data = [cells(SEED, 24000 + s * k, k, n) for s in range(S)]
+    units = np.stack([np.stack(d + oracle.rs_encode(k, p, d)) for d in data])  # [S][k+p][n]
+    d_in = t(units)
+    try:
+        assert lib.ozec_set_tuning(b"gf_variant", variant) == 0
+        if erased is None:
+            d_out = torch.zeros((S, p, n), dtype=torch.uint8, device=DEV)
+            enc("rs", k, p).encode_batch(d_in, (k + p) * n, n, d_out, p * n, n, S, n)
+            want = units[:, k:]
+        else:
+            present = [u for u in range(k + p) if u not in erased]
+            d_out = torch.zeros((S, len(erased), n), dtype=torch.uint8, device=DEV)
+            dec("rs", k, p).decode_batch(d_in, (k + p) * n, n, present, erased, d_out, len(erased) * n, n, S, n)
+            want = units[:, erased]
+        got = h(d_out)
+    finally:
+        lib.ozec_set_tuning(b"gf_variant", 0)
+    assert (got == want).all()
+
+
 def test_decode_uses_first_k_valid_inputs():
     """RSRawDecoder.java:79-82: with more than k inputs present only the first k are read -- corrupting a later
     one must not change the output."""

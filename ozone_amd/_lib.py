@@ -9,7 +9,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libozec.so")
+# OZEC_LIB_OVERRIDE: another build of the same library (the sanitizer build of tests/test_host_abi_asan.py)
+LIB_PATH = os.environ.get("OZEC_LIB_OVERRIDE") or os.path.join(_HERE, "lib", "libozec.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ozec.h")
 
 OZEC_OK = 0

@@ -1211,7 +1211,7 @@ int ozec_rs_encode_matrix(int k, int p, uint8_t *matrix) {
 }
 
 int ozec_rs_decode_matrix(int k, int p, const int *valid, const int *erased, int n_erased, uint8_t *out) {
-  if (!valid || (n_erased && (!erased || !out)) || k <= 0 || p <= 0 || k + p >= 256)
+  if (!valid || n_erased < 0 || (n_erased && (!erased || !out)) || k <= 0 || p <= 0 || k + p >= 256)
     return fail(OZEC_EINVAL, "invalid arguments");
   for (int i = 0; i < k; ++i)
     if (valid[i] < 0 || valid[i] >= k + p) return fail(OZEC_EINVAL, "valid index out of range");
@@ -1219,7 +1219,7 @@ int ozec_rs_decode_matrix(int k, int p, const int *valid, const int *erased, int
     if (erased[i] < 0 || erased[i] >= k + p) return fail(OZEC_EINVAL, "erased index out of range");
   std::vector<uint8_t> rows;
   if (!ozec::decode_matrix(k, p, valid, erased, n_erased, rows)) return fail(OZEC_ENOTINVERTIBLE, "Not invertible");
-  std::memcpy(out, rows.data(), rows.size());
+  if (!rows.empty()) std::memcpy(out, rows.data(), rows.size());
   return OZEC_OK;
 }
 

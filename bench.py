@@ -759,10 +759,33 @@ def stream_latency(args):
 # ------------------------------------------------------------------------------------------ main
 
 
+_JSON_FD = None
+
+
+def _quiet_stdout():
+    """Keep stdout for the one JSON line: libraries print to fd 1 from C++ (gloo's "Rank 0 is connected to 1 peer
+    ranks"), so fd 1 is pointed at stderr for the whole run and the result goes to a saved copy of it."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj):
+    line = (json.dumps(obj) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line)
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_workers(args)
+    _quiet_stdout()
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -812,16 +835,16 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline("c5", args.cpu_seconds)
         if rank == 0:
-            print(json.dumps(result), flush=True)
+            emit(result)
         if dist is not None:
             dist.destroy_process_group()
         return 0
 
     if args.workload == "stream":
         if rank == 0:
-            print(json.dumps({"metric": "per-call latency of the drop-in entry points (us)", "value": None,
-                              "n_gpus": n_gpus, "dtype": "u8", "config": {"workload": "stream"},
-                              "calls": stream_latency(args)}), flush=True)
+            emit({"metric": "per-call latency of the drop-in entry points (us)", "value": None,
+                  "n_gpus": n_gpus, "dtype": "u8", "config": {"workload": "stream"},
+                  "calls": stream_latency(args)})
         return 0
 
     wl = Workload(args.workload, rank, world, args.stripes, args.threads, erased)
@@ -893,7 +916,7 @@ def main():
             if "e2e" in result and "value" in result["e2e"]:
                 result["e2e"]["cpu_baseline"] = cpu_baseline("c5", args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result)
     if dist is not None:
         dist.destroy_process_group()
     return 0

@@ -9,6 +9,8 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 from ozone_amd.shard import max_over_ranks, stripe_range
 
 
@@ -77,3 +79,19 @@ def test_two_rank_gloo_sharded_encode():
         par = oracle.rs_encode(k, p, cells(SEED, s * k, k, n))
         assert merged[s] == int(np.bitwise_xor.reduce(np.concatenate(par).view(np.uint64)))
     assert slowest == 2.0
+
+
+def test_bench_stdout_holds_only_the_json_line():
+    """bench.py's contract is ONE JSON line on stdout: anything a library writes to fd 1 from native code (gloo's
+    "Rank 0 is connected to 1 peer ranks") goes to stderr instead."""
+    import json
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path.insert(0, %r); import bench; bench._quiet_stdout(); "
+            "os.write(1, b'[Gloo] Rank 0 is connected\\n'); print('python noise'); bench.emit({'metric': 'x', 'value': 1})"
+            % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and json.loads(lines[0]) == {"metric": "x", "value": 1}, r.stdout
+    assert "Gloo" in r.stderr and "python noise" in r.stderr

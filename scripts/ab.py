@@ -13,8 +13,10 @@ rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 5
 torch.cuda.set_device(0)
 lib = L.lib()
 wl = bench.Workload(wl_name, 0, 1, None)
-if os.environ.get("ZERO") and hasattr(wl, "units"):  # all-zero data cells: separates data-dependent power/clock effects
-    wl.units.zero_()
+if os.environ.get("ZERO"):  # all-zero data cells: separates data-dependent power/clock effects
+    for name in ("units", "data", "blocks"):
+        if hasattr(wl, name):
+            getattr(wl, name).zero_()
     torch.cuda.synchronize()
 
 

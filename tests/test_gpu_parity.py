@@ -355,7 +355,12 @@ def test_checksum_impls_compute_same_values_64mib():
                                                (6, 3, "rs", 65536, 4096, 3), (6, 3, "rs", 1040 * 16, 1040, 2),
                                                (6, 3, "rs", 50000, 16384, 2), (5, 2, "rs", 65536, 16384, 2),
                                                (6, 1, "xor", 65536, 4096, 2), (3, 1, "xor", 50000, 16384, 2),
-                                               (10, 1, "xor", 1 << 17, 16384, 2), (6, 1, "rs", 65536, 16384, 2)])
+                                               (10, 1, "xor", 1 << 17, 16384, 2), (6, 1, "rs", 65536, 16384, 2),
+                                               # streamed-input kernel geometries: one 1 MiB window per cell,
+                                               # 8 KiB windows, a single 4 KiB window, 32 KiB windows
+                                               (6, 3, "rs", 1 << 20, 1 << 20, 2), (6, 3, "rs", 3 * 8192, 8192, 3),
+                                               (10, 4, "rs", 4096, 4096, 5), (6, 2, "rs", 1 << 17, 32768, 2),
+                                               (3, 2, "rs", 1 << 16, 4096, 3), (10, 2, "rs", 1 << 16, 16384, 2)])
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
 def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
     data = np.stack([np.stack(cells(SEED, 50000 + s * k, k, n)) for s in range(S)])

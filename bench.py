@@ -46,7 +46,7 @@ MIB = 1 << 20
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED = 0x00EC5EED
 METRIC = "EC encode GB/s (data bytes) rs-6-3-1024k @1/8 GPUs + % HBM roofline"
-WORKLOADS = ["c1", "c2", "c3", "c3r", "c4", "c4s", "c5", "c5dev", "crc", "verify", "host", "queue", "queue_pageable",
+WORKLOADS = ["c1", "c2", "c3", "c3r", "c3r_host", "c4", "c4s", "c5", "c5dev", "crc", "verify", "host", "queue", "queue_pageable",
              "stream"]
 
 
@@ -196,6 +196,51 @@ class Workload:
                 for th in ts:
                     th.join()
             self._step = step
+            return
+        if name == "c3r_host":
+            # reconstruction end to end from pinned host memory: the reconstruction coordinator's read buffers
+            # (ECReconstructionCoordinator.java:240-352) -> H2D of the 10 units read -> fused verify + decode + CRC
+            # -> D2H of the 4 rebuilt units, their CRCs and the per-stripe verdicts
+            from ozone_amd.stripe_queue import host_alloc
+            k, p, S = 10, 4, stripes_override or 512
+            self.erased = sorted(erased)
+            present = [u for u in range(k + p) if u not in self.erased]
+            self.bpc, self.crc_type = 16384, ck.ChecksumType.CRC32C
+            nwin = n // self.bpc
+            dunits = torch.empty((S, k + p, n), dtype=torch.uint8, device=dev)
+            for s0 in range(0, S, 64):  # data cells, then parity on the GPU (the stored stripes)
+                c = min(64, S - s0)
+                for i in range(c):
+                    rc.fill_splitmix64_cells(dunits[s0 + i], n, k, n, SEED, (rank * S + s0 + i) * k)
+            encr = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+            encr.encode_batch(dunits, (k + p) * n, n, dunits[:, k:], (k + p) * n, n, S, n)
+            dstored = torch.empty((S, k + p, nwin), dtype=torch.int32, device=dev)
+            ck.checksum_windows_batch(self.crc_type, dunits, n, S * (k + p), n, self.bpc, dstored)
+            torch.cuda.synchronize()
+            self._pool = [host_alloc(S * (k + p) * n), host_alloc(S * 4 * n), host_alloc(S * 4 * nwin * 4),
+                          host_alloc(S * (k + p) * nwin * 4), host_alloc(S * 4)]
+            hin, hout, hocrc, hexp, hmis = (pb.array for pb in self._pool)
+            torch.from_numpy(hin).copy_(dunits.reshape(-1))
+            torch.from_numpy(hexp).copy_(dstored.reshape(-1).view(torch.uint8))
+            del dunits, dstored
+            torch.cuda.empty_cache()
+            self.k, self.p, self.S = k, p, S
+            self.data_bytes = S * k * n
+            self.alg_bytes = S * (k + 4) * n + S * (k + 4) * nwin * 4
+            self.kernel = "encode_crc_lv<10,4> (+H2D of the 10 units read, D2H of the 4 rebuilt, pipelined)"
+            self.config = {"workload": f"rs-10-4-1024k reconstruction end to end from pinned host memory: H2D of the 10 "
+                                       f"units read, verify CRC32C + decode 4 + CRC32C of rebuilt units "
+                                       f"{{{','.join(map(str, self.erased))}}}, D2H, {S} stripes",
+                           "codec": "rs", "data_units": k, "parity_units": p, "cell_bytes": n, "stripes": S,
+                           "bytes_per_checksum": self.bpc}
+            dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
+            hexp32, hocrc32, hmis32 = hexp.view(np.uint32), hocrc.view(np.uint32), hmis.view(np.int32)
+
+            def step():
+                dec.reconstruct_crc_host_batch(hin, (k + p) * n, n, present, self.erased, hout, 4 * n, n, S, n,
+                                               self.crc_type, self.bpc, hocrc32, h_expected=hexp32, h_mismatch=hmis32)
+            self._step = step
+            self._check = lambda: bool((hmis32 == -1).all())
             return
         if name in ("queue", "queue_pageable"):
             from ozone_amd.stripe_queue import StripeQueue, host_alloc
@@ -621,7 +666,8 @@ CPU_WHAT = {
 def cpu_baseline(workload, budget_s):
     """The reference's CPU path timed on this host's cores (RawErasureCoderBenchmark.java:182-236 definitions:
     threads share one coder, data bytes counted): T = every CPU this process may use, and 1 thread."""
-    wl = {"c4s": "c4", "c5dev": "c5", "host": "c2", "queue": "c5", "queue_pageable": "c5", "stream": "c2"}.get(
+    wl = {"c4s": "c4", "c5dev": "c5", "host": "c2", "queue": "c5", "queue_pageable": "c5", "stream": "c2",
+          "c3r_host": "c3r"}.get(
         workload, workload)
     exe, flags = _cpu_baseline_bin()
     T = usable_cpus()
@@ -894,11 +940,14 @@ def main():
                      "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4), "kernel_ms_reduction": "max over ranks",
                      "alg_bytes_per_launch": wl.alg_bytes, "numa_node": numa_node},
     }
-    if args.workload in ("host", "queue", "queue_pageable"):
-        pc = pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
+    if args.workload in ("host", "queue", "queue_pageable", "c3r_host"):
+        pc = pcie_ceiling(64 * 10 * MIB, 64 * 4 * MIB) if args.workload == "c3r_host" else \
+            pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
         pc["value_frac_of_duplex_h2d"] = round(value / world / pc["duplex_h2d_GBps"], 4)
         result["pcie"] = pc
         result["roofline"]["note"] = "kernel_ms is the whole PCIe-inclusive step; the bound is the link, not HBM"
+    if hasattr(wl, "_check"):
+        result["verified"] = wl._check()
     wl.free()
     del wl
     if args.workload == "c2" and not args.no_e2e:

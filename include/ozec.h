@@ -185,6 +185,18 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
                                size_t num_stripes, size_t len, int checksum_type, size_t bytes_per_checksum,
                                const uint32_t *d_expected, int expected_big_endian, uint32_t *d_out_crcs,
                                int out_big_endian, int32_t *d_mismatch, void *stream);
+/* The same reconstruction for stripes held in HOST memory (the reconstruction coordinator's read buffers,
+ * ECReconstructionCoordinator.java:240-352): same layouts and semantics with host pointers (h_expected
+ * [stripe][k+p][window], h_out_crcs [stripe][num_erased][window], h_mismatch[stripe]; checksum_type CRC32 / CRC32C).
+ * Only the k units the decoder reads are copied to the GPU, one rectangular copy per run of consecutive unit
+ * indexes and chunk of stripes_per_chunk stripes (0 = the "e2e_chunk" knob); chunks are pipelined as in
+ * ozec_encode_crc_host_batch (registered / pinned buffers DMA'd in place, pageable ones staged).  Synchronous. */
+int ozec_reconstruct_crc_host_batch(ozec_coder *dec, const uint8_t *h_in, int64_t in_stripe_stride,
+                                    int64_t in_unit_stride, const int *present, int num_present, const int *erased,
+                                    int num_erased, uint8_t *h_out, int64_t out_stripe_stride, int64_t out_unit_stride,
+                                    size_t num_stripes, size_t len, int checksum_type, size_t bytes_per_checksum,
+                                    const uint32_t *h_expected, int expected_big_endian, uint32_t *h_out_crcs,
+                                    int out_big_endian, int32_t *h_mismatch, size_t stripes_per_chunk);
 
 /* ---- streaming ChecksumByteBuffer (CM/ChecksumByteBuffer.java:32-44): update(ByteBuffer) / getValue /
  *      reset over an opaque 32-bit state.  The GPU computes the raw CRC of the buffer and the host combines

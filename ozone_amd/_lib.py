@@ -91,6 +91,10 @@ _SIGS = {
                                                   ctypes.c_int, c_voidp, c_i64, c_i64, c_size, c_size, ctypes.c_int,
                                                   c_size, c_voidp, ctypes.c_int, c_voidp, ctypes.c_int, c_voidp,
                                                   c_voidp]),
+    "ozec_reconstruct_crc_host_batch": (ctypes.c_int, [c_voidp, c_voidp, c_i64, c_i64, c_intp, ctypes.c_int, c_intp,
+                                                       ctypes.c_int, c_voidp, c_i64, c_i64, c_size, c_size, ctypes.c_int,
+                                                       c_size, c_voidp, ctypes.c_int, c_voidp, ctypes.c_int, c_voidp,
+                                                       c_size]),
     "ozec_crc_reset": (ctypes.c_uint32, [ctypes.c_int]),
     "ozec_crc_update": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), c_voidp, c_size]),
     "ozec_crc_value": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_uint32]),

@@ -1201,6 +1201,215 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
   return OZEC_OK;
 }
 
+// Fused reconstruction of stripes held in HOST memory: the datanode side of ECReconstructionCoordinator, whose read
+// buffers hold the k units it fetched (ECBlockReconstructedStripeInputStream.java:689-694).  The pipeline of
+// ozec_encode_crc_host_batch (ring of E2E::NB device chunk buffers, H2D / kernel / D2H on three streams, the host
+// waiting for a buffer's previous chunk before refilling it) around ozec_reconstruct_crc_batch.  Only the k units the
+// decoder reads cross PCIe, as one rectangular copy per run of consecutive unit indexes per chunk.
+int ozec_reconstruct_crc_host_batch(ozec_coder *dec, const uint8_t *h_in, int64_t in_stripe_stride,
+                                    int64_t in_unit_stride, const int *present_units, int num_present, const int *erased,
+                                    int n_erased, uint8_t *h_out, int64_t out_stripe_stride, int64_t out_unit_stride,
+                                    size_t num_stripes, size_t len, int checksum_type, size_t bpc,
+                                    const uint32_t *h_expected, int expected_big_endian, uint32_t *h_out_crcs,
+                                    int out_big_endian, int32_t *h_mismatch, size_t stripes_per_chunk) {
+  ozec::StatScope stat_(OZEC_OP_HOST_BATCH, dec ? static_cast<uint64_t>(dec->k) * len * num_stripes : 0);
+  if (int rc = check_open(dec, "decode")) return rc;
+  if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
+  const int n_all = dec->k + dec->p;
+  if (num_present < 0 || (num_present > 0 && !present_units)) return fail(OZEC_EINVAL, "invalid present units");
+  bool present[256] = {false};
+  for (int i = 0; i < num_present; ++i) {
+    if (present_units[i] < 0 || present_units[i] >= n_all) return fail(OZEC_EINVAL, "present unit out of range");
+    present[present_units[i]] = true;
+  }
+  std::vector<int> units;
+  std::vector<uint8_t> rows;
+  if (int rc = plan_decode(dec, present, erased, n_erased, units, rows)) return rc;
+  {
+    CrcType t;
+    if (int rc = crc_type_of(checksum_type, &t)) return rc;
+    if (bpc == 0) return fail(OZEC_EINVAL, "bytesPerChecksum must be positive");
+  }
+  if (num_stripes == 0 || len == 0) {
+    if (h_mismatch)
+      for (size_t s = 0; s < num_stripes; ++s) h_mismatch[s] = -1;
+    return OZEC_OK;
+  }
+  if (!h_in || (n_erased && (!h_out || !h_out_crcs))) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  if (h_expected && !h_mismatch) return fail(OZEC_EINVAL, "verification needs a mismatch buffer");
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  E2E &P = ctx->e2e;
+  std::lock_guard<std::mutex> lk(P.mu);
+  const int e = n_erased;
+  const size_t C = std::min(num_stripes, stripes_per_chunk ? stripes_per_chunk
+                                                          : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk)));
+  const size_t nwin = (len + bpc - 1) / bpc;
+  // device layout of one chunk buffer: input slots [C][k+p][len], rebuilt [C][e][len], expected CRCs [C][k+p][nwin],
+  // rebuilt CRCs [C][e][nwin], mismatch [C]
+  const size_t dstripe = static_cast<size_t>(n_all) * len, ostripe = static_cast<size_t>(e) * len;
+  const size_t dout_off = round_up(C * dstripe, kStageAlign);
+  const size_t dexp_off = round_up(dout_off + C * ostripe, kStageAlign);
+  const size_t dexp_bytes = h_expected ? C * n_all * nwin * sizeof(uint32_t) : 0;
+  const size_t docrc_off = round_up(dexp_off + dexp_bytes, kStageAlign);
+  const size_t dmis_off = round_up(docrc_off + C * e * nwin * sizeof(uint32_t), kStageAlign);
+  const size_t dbytes = dmis_off + C * sizeof(int32_t);
+  // runs of consecutive unit indexes among the units read: one rectangular copy per run and chunk
+  std::vector<std::pair<int, int>> runs;
+  for (int u : units) {
+    if (!runs.empty() && runs.back().first + runs.back().second == u) ++runs.back().second;
+    else runs.push_back({u, 1});
+  }
+  const int umax = units.empty() ? 0 : units.back();
+  const size_t in_span = (num_stripes - 1) * static_cast<size_t>(in_stripe_stride) +
+                         static_cast<size_t>(umax) * static_cast<size_t>(in_unit_stride) + len;
+  const size_t out_span = e ? (num_stripes - 1) * static_cast<size_t>(out_stripe_stride) +
+                                  static_cast<size_t>(e - 1) * static_cast<size_t>(out_unit_stride) + len
+                            : 0;
+  const bool in_pinned = range_pinned(h_in, in_span);
+  const bool out_pinned = !e || range_pinned(h_out, out_span);
+  const bool exp_pinned = !h_expected || range_pinned(h_expected, num_stripes * n_all * nwin * sizeof(uint32_t));
+  const bool ocrc_pinned = !e || range_pinned(h_out_crcs, num_stripes * e * nwin * sizeof(uint32_t));
+  const bool mis_pinned = !h_expected || range_pinned(h_mismatch, num_stripes * sizeof(int32_t));
+  const bool staged = !in_pinned || !out_pinned || !exp_pinned || !ocrc_pinned || !mis_pinned;
+  if (!P.h2d) {
+    OZEC_HIP(hipStreamCreateWithFlags(&P.h2d, hipStreamNonBlocking));
+    OZEC_HIP(hipStreamCreateWithFlags(&P.comp, hipStreamNonBlocking));
+    OZEC_HIP(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
+    for (int b = 0; b < E2E::NB; ++b) {
+      OZEC_HIP(hipEventCreateWithFlags(&P.h2d_done[b], hipEventDisableTiming));
+      OZEC_HIP(hipEventCreateWithFlags(&P.comp_done[b], hipEventDisableTiming));
+      OZEC_HIP(hipEventCreateWithFlags(&P.d2h_done[b], hipEventDisableTiming));
+    }
+  }
+  struct DrainOnExit {
+    E2E &P;
+    ~DrainOnExit() {
+      (void)hipStreamSynchronize(P.h2d);
+      (void)hipStreamSynchronize(P.comp);
+      (void)hipStreamSynchronize(P.d2h);
+    }
+  } drain{P};
+  if (dbytes > P.dcap) {
+    for (auto &d : P.dbuf) {
+      if (d) (void)hipFree(d);
+      d = nullptr;
+    }
+    P.dcap = 0;
+    for (auto &d : P.dbuf) OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&d), dbytes));
+    P.dcap = dbytes;
+  }
+  if (staged && dbytes > P.hcap) {
+    for (auto &h : P.hstage) {
+      if (h) (void)ozec::pinned_free(h);
+      h = nullptr;
+    }
+    P.hcap = 0;
+    for (auto &h : P.hstage)
+      if (ozec::pinned_alloc(dbytes, ctx->device, reinterpret_cast<void **>(&h)) != 0)
+        return fail(OZEC_ENOMEM, "cannot pin " + std::to_string(dbytes) + " bytes of staging memory");
+    P.hcap = dbytes;
+  }
+  const size_t nch = (num_stripes + C - 1) / C;
+  auto unstage = [&](size_t c) -> int {
+    const int b = static_cast<int>(c % E2E::NB);
+    OZEC_HIP(hipEventSynchronize(P.d2h_done[b]));
+    const size_t s0 = c * C, cs = std::min(C, num_stripes - s0);
+    std::vector<ozec::CopyTask> tasks;
+    if (!out_pinned)
+      for (size_t i = 0; i < cs; ++i)
+        for (int r = 0; r < e; ++r)
+          tasks.push_back({h_out + (s0 + i) * out_stripe_stride + r * out_unit_stride,
+                           P.hstage[b] + dout_off + i * ostripe + static_cast<size_t>(r) * len, len});
+    if (!ocrc_pinned)
+      tasks.push_back({h_out_crcs + s0 * e * nwin, P.hstage[b] + docrc_off, cs * e * nwin * sizeof(uint32_t)});
+    if (!mis_pinned) tasks.push_back({h_mismatch + s0, P.hstage[b] + dmis_off, cs * sizeof(int32_t)});
+    ozec::parallel_copy(tasks);
+    return OZEC_OK;
+  };
+  for (size_t c = 0; c < nch; ++c) {
+    const int b = static_cast<int>(c % E2E::NB);
+    const size_t s0 = c * C, cs = std::min(C, num_stripes - s0);
+    uint8_t *d = P.dbuf[b];
+    uint8_t *hs = staged ? P.hstage[b] : nullptr;
+    if (staged) {
+      if (c >= static_cast<size_t>(E2E::NB))
+        if (int rc = unstage(c - E2E::NB)) return rc;
+      std::vector<ozec::CopyTask> tasks;
+      if (!in_pinned)
+        for (size_t i = 0; i < cs; ++i)
+          for (int u : units)
+            tasks.push_back({hs + i * dstripe + static_cast<size_t>(u) * len,
+                             h_in + (s0 + i) * in_stripe_stride + u * in_unit_stride, len});
+      if (!exp_pinned)
+        tasks.push_back({hs + dexp_off, h_expected + s0 * n_all * nwin, cs * n_all * nwin * sizeof(uint32_t)});
+      ozec::parallel_copy(tasks);
+    }
+    if (c >= static_cast<size_t>(E2E::NB)) {
+      if (!staged) OZEC_HIP(hipEventSynchronize(P.d2h_done[b]));
+      OZEC_HIP(hipStreamWaitEvent(P.h2d, P.d2h_done[b], 0));
+    }
+    for (const auto &run : runs) {
+      const size_t off = static_cast<size_t>(run.first) * len, width = static_cast<size_t>(run.second) * len;
+      if (!in_pinned) {
+        OZEC_HIP(hipMemcpy2DAsync(d + off, dstripe, hs + off, dstripe, width, cs, hipMemcpyHostToDevice, P.h2d));
+      } else if (in_unit_stride == static_cast<int64_t>(len)) {
+        OZEC_HIP(hipMemcpy2DAsync(d + off, dstripe, h_in + s0 * in_stripe_stride + off,
+                                  static_cast<size_t>(in_stripe_stride), width, cs, hipMemcpyHostToDevice, P.h2d));
+      } else {
+        for (size_t i = 0; i < cs; ++i)
+          for (int u = run.first; u < run.first + run.second; ++u)
+            OZEC_HIP(hipMemcpyAsync(d + i * dstripe + static_cast<size_t>(u) * len,
+                                    h_in + (s0 + i) * in_stripe_stride + u * in_unit_stride, len, hipMemcpyHostToDevice,
+                                    P.h2d));
+      }
+    }
+    if (h_expected)
+      OZEC_HIP(hipMemcpyAsync(d + dexp_off, exp_pinned ? reinterpret_cast<const uint8_t *>(h_expected + s0 * n_all * nwin)
+                                                       : hs + dexp_off,
+                              cs * n_all * nwin * sizeof(uint32_t), hipMemcpyHostToDevice, P.h2d));
+    OZEC_HIP(hipEventRecord(P.h2d_done[b], P.h2d));
+    OZEC_HIP(hipStreamWaitEvent(P.comp, P.h2d_done[b], 0));
+    if (int rc = ozec_reconstruct_crc_batch(
+            dec, d, static_cast<int64_t>(dstripe), static_cast<int64_t>(len), present_units, num_present, erased, e,
+            d + dout_off, static_cast<int64_t>(ostripe), static_cast<int64_t>(len), cs, len, checksum_type, bpc,
+            h_expected ? reinterpret_cast<const uint32_t *>(d + dexp_off) : nullptr, expected_big_endian,
+            reinterpret_cast<uint32_t *>(d + docrc_off), out_big_endian,
+            h_expected ? reinterpret_cast<int32_t *>(d + dmis_off) : nullptr, P.comp))
+      return rc;
+    OZEC_HIP(hipEventRecord(P.comp_done[b], P.comp));
+    OZEC_HIP(hipStreamWaitEvent(P.d2h, P.comp_done[b], 0));
+    if (e) {
+      if (!out_pinned) {
+        OZEC_HIP(hipMemcpyAsync(hs + dout_off, d + dout_off, cs * ostripe, hipMemcpyDeviceToHost, P.d2h));
+      } else if (out_unit_stride == static_cast<int64_t>(len)) {
+        OZEC_HIP(hipMemcpy2DAsync(h_out + s0 * out_stripe_stride, static_cast<size_t>(out_stripe_stride), d + dout_off,
+                                  ostripe, ostripe, cs, hipMemcpyDeviceToHost, P.d2h));
+      } else {
+        for (size_t i = 0; i < cs; ++i)
+          for (int r = 0; r < e; ++r)
+            OZEC_HIP(hipMemcpyAsync(h_out + (s0 + i) * out_stripe_stride + r * out_unit_stride,
+                                    d + dout_off + i * ostripe + static_cast<size_t>(r) * len, len, hipMemcpyDeviceToHost,
+                                    P.d2h));
+      }
+      OZEC_HIP(hipMemcpyAsync(ocrc_pinned ? reinterpret_cast<uint8_t *>(h_out_crcs + s0 * e * nwin) : hs + docrc_off,
+                              d + docrc_off, cs * e * nwin * sizeof(uint32_t), hipMemcpyDeviceToHost, P.d2h));
+    }
+    if (h_expected)
+      OZEC_HIP(hipMemcpyAsync(mis_pinned ? reinterpret_cast<uint8_t *>(h_mismatch + s0) : hs + dmis_off, d + dmis_off,
+                              cs * sizeof(int32_t), hipMemcpyDeviceToHost, P.d2h));
+    OZEC_HIP(hipEventRecord(P.d2h_done[b], P.d2h));
+  }
+  if (staged) {
+    for (size_t c = nch > static_cast<size_t>(E2E::NB) ? nch - E2E::NB : 0; c < nch; ++c)
+      if (int rc = unstage(c)) return rc;
+  }
+  OZEC_HIP(hipStreamSynchronize(P.d2h));
+  if (!h_expected && h_mismatch)
+    for (size_t s = 0; s < num_stripes; ++s) h_mismatch[s] = -1;
+  return OZEC_OK;
+}
+
 // ---- host-side math ----------------------------------------------------------------------------
 
 int ozec_rs_encode_matrix(int k, int p, uint8_t *matrix) {

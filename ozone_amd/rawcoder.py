@@ -442,6 +442,41 @@ class RawErasureDecoder(_Coder):
         if rc != L.OZEC_OK:
             _raise_for(rc)
 
+    def reconstruct_crc_host_batch(self, h_in, in_stripe_stride, in_unit_stride, present_units, erased_indexes, h_out,
+                                   out_stripe_stride, out_unit_stride, num_stripes, length, checksum_type,
+                                   bytes_per_checksum, h_out_crcs, h_expected=None, h_mismatch=None,
+                                   expected_big_endian=False, out_big_endian=False, stripes_per_chunk=0):
+        """reconstruct_crc_batch for stripes in HOST memory (ozec_reconstruct_crc_host_batch): the reconstruction
+        coordinator's read buffers, pipelined over PCIe.  Host addresses (ints) or numpy arrays; a numpy array must be
+        C-contiguous and large enough for the layout it is given as.  Synchronous."""
+        k, p = self._config.data, self._config.parity
+        e = len(erased_indexes)
+        nwin = -(-length // bytes_per_checksum) if bytes_per_checksum > 0 else 0
+        S = num_stripes
+
+        def addr(x, what, need, dtype):
+            if x is None or isinstance(x, int):
+                return x
+            if not isinstance(x, np.ndarray) or not x.flags.c_contiguous or x.dtype != dtype or x.nbytes < need:
+                raise IllegalArgumentException(f"Invalid {what} buffer: a C-contiguous {np.dtype(dtype).name} array of "
+                                               f">= {need} bytes is required")
+            if what != "input" and what != "expected" and not x.flags.writeable:
+                raise IllegalArgumentException(f"Invalid {what} buffer: not writeable")
+            return x.ctypes.data
+        umax = max(present_units) if present_units else 0
+        in_need = (S - 1) * in_stripe_stride + umax * in_unit_stride + length if S else 0
+        out_need = (S - 1) * out_stripe_stride + (e - 1) * out_unit_stride + length if S and e else 0
+        rc = L.lib().ozec_reconstruct_crc_host_batch(
+            self._handle, addr(h_in, "input", in_need, np.uint8), in_stripe_stride, in_unit_stride,
+            L.int_array(list(present_units)), len(present_units), L.int_array(list(erased_indexes)), e,
+            addr(h_out, "output", out_need, np.uint8), out_stripe_stride, out_unit_stride, num_stripes, length,
+            int(checksum_type), bytes_per_checksum,
+            addr(h_expected, "expected", S * (k + p) * nwin * 4, np.uint32), 1 if expected_big_endian else 0,
+            addr(h_out_crcs, "rebuilt CRC", S * e * nwin * 4, np.uint32), 1 if out_big_endian else 0,
+            addr(h_mismatch, "mismatch", S * 4, np.int32), stripes_per_chunk)
+        if rc != L.OZEC_OK:
+            _raise_for(rc)
+
 
 # ---------------------------------------------------------------- dummy coder ----------------------------
 

@@ -11,7 +11,7 @@ grep -v amdgpu.ids $O/smoke.log
 t0=$(date +%s)
 timeout -k 10 600 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { echo "default bench failed"; tail -20 $O/bench_default.err; exit 1; }
 echo "default bench: $(( $(date +%s) - t0 )) s"
-for w in ${WORKLOADS:-c1 c3 c3r c4 c5dev crc verify queue host stream}; do
+for w in ${WORKLOADS:-c1 c3 c3r c3r_host c4 c5dev crc verify queue host stream}; do
   timeout -k 10 300 python bench.py --workload $w > $O/bench_$w.json 2> $O/bench_$w.err || { echo "bench $w failed"; tail $O/bench_$w.err; exit 1; }
   echo "bench $w ok"
 done

@@ -111,6 +111,83 @@ def test_host_batch_errors():
                                 ck.ChecksumType.NONE, 0, None)
 
 
+def _recon_batch(codec, k, p, n, S, first, gap=0):
+    """[S][k+p][n + gap] host stripes, every unit present (parity from the oracle)."""
+    us = n + gap
+    buf = np.full(S * (k + p) * us, 0xA5, np.uint8)
+    v = buf.reshape(S, k + p, us)
+    for s in range(S):
+        d = cells(SEED, first + s * k, k, n)
+        par = oracle.rs_encode(k, p, d) if codec == "rs" else [oracle.xor_encode(d)] + [np.zeros(n, np.uint8)] * (p - 1)
+        for u, x in enumerate(d + par):
+            v[s, u, :n] = x
+    return buf, v, us
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("codec,k,p,erased,n,S,chunk,bpc,gap", [
+    ("rs", 10, 4, [0, 1, 2, 3], 1 << 16, 13, 4, 16384, 0),      # one run of read units {4..13}, 4 chunks
+    ("rs", 10, 4, [1, 4, 10, 13], 1 << 15, 7, 3, 4096, 0),      # four runs {0},{2,3},{5..9},{11,12}
+    ("rs", 6, 3, [0, 2, 7], 1 << 16, 9, 0, 16384, 4096),        # gaps between units: per-cell copies
+    ("rs", 6, 3, [8], 50000, 5, 2, 1000, 0),                    # unfused fallback (len, bpc not 16-aligned)
+    ("xor", 2, 1, [1], 1 << 15, 6, 4, 8192, 0),
+])
+def test_reconstruct_host_batch_vs_oracle(pinned, codec, k, p, erased, n, S, chunk, bpc, gap):
+    """ozec_reconstruct_crc_host_batch: rebuilt units equal the originals, their CRCs equal the stored ones, and a
+    corrupted window of a read unit is reported for its stripe only."""
+    buf, v, us = _recon_batch(codec, k, p, n, S, 830000 + 100 * k, gap)
+    nwin = (n + bpc - 1) // bpc
+    ctype, otype = ck.ChecksumType.CRC32C, oracle.CRC32C
+    stored = np.stack([np.stack([oracle.crc_windows(otype, np.array(v[s, u, :n]), bpc) for u in range(k + p)])
+                       for s in range(S)]).astype(np.uint32).reshape(-1)
+    present = [u for u in range(k + p) if u not in erased]
+    read = present[:k]
+    orig = np.array(v[:, :, :n])
+    v[:, erased, :] = 0xEE                       # erased units hold garbage in the caller's buffers
+    v[2, read[-1], 2 * bpc + 5] ^= 0x01          # stripe 2: silent corruption in the last unit read
+    e = len(erased)
+    out = np.zeros(S * e * n, np.uint8)
+    ocrc = np.zeros(S * e * nwin, np.uint32)
+    mism = np.zeros(S, np.int32)
+    keep = []
+    if pinned:
+        pb, po, pc, pe, pm = (host_alloc(x.nbytes) for x in (buf, out, ocrc, stored, mism))
+        pb.array[:] = buf
+        pe.array[:] = stored.view(np.uint8)
+        keep += [pb, po, pc, pe, pm]
+        v = pb.array.reshape(S, k + p, us)
+        out, ocrc, stored, mism = po.array, pc.array.view(np.uint32), pe.array.view(np.uint32), pm.array.view(np.int32)
+    dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec))
+    dec.reconstruct_crc_host_batch(v.reshape(-1), (k + p) * us, us, present, erased, out, e * n, n, S, n, ctype, bpc,
+                                   ocrc, h_expected=stored, h_mismatch=mism, stripes_per_chunk=chunk)
+    got = out.reshape(S, e, n)
+    oc = ocrc.reshape(S, e, nwin)
+    st = stored.reshape(S, k + p, nwin)
+    assert mism[2] == read[-1] * nwin + 2 and all(mism[s] == -1 for s in range(S) if s != 2), list(mism)
+    for s in range(S):
+        for i, u in enumerate(erased):
+            if s != 2:  # stripe 2's rebuilt units are decoded from the corrupted input
+                assert (got[s, i] == orig[s, u]).all(), (s, u)
+                assert (oc[s, i] == st[s, u]).all(), (s, u)
+            assert (oc[s, i] == oracle.crc_windows(otype, got[s, i], bpc)).all(), (s, u)
+
+
+def test_reconstruct_host_batch_errors():
+    dec = rc.RawErasureDecoder(rc.ECReplicationConfig(6, 3))
+    buf = np.zeros(9 * 4096, np.uint8)
+    out = np.zeros(4096, np.uint8)
+    crc = np.zeros(1, np.uint32)
+    with pytest.raises(rc.IllegalArgumentException):  # output array too small for the layout
+        dec.reconstruct_crc_host_batch(buf, 9 * 4096, 4096, list(range(1, 9)), [0], np.zeros(100, np.uint8), 4096,
+                                       4096, 1, 4096, ck.ChecksumType.CRC32C, 4096, crc)
+    with pytest.raises(rc.IllegalArgumentException):  # verification without a mismatch buffer
+        dec.reconstruct_crc_host_batch(buf, 9 * 4096, 4096, list(range(1, 9)), [0], out, 4096, 4096, 1, 4096,
+                                       ck.ChecksumType.CRC32C, 4096, crc, h_expected=np.zeros(9, np.uint32))
+    with pytest.raises(rc.IllegalArgumentException):  # too many erased
+        dec.reconstruct_crc_host_batch(buf, 9 * 4096, 4096, [4, 5, 6, 7, 8, 3], [0, 1, 2, 3], np.zeros(4 * 4096, np.uint8),
+                                       4 * 4096, 4096, 1, 4096, ck.ChecksumType.CRC32C, 4096, np.zeros(4, np.uint32))
+
+
 def test_pinned_memory_is_numa_local():
     """ozec_host_alloc places its pages on the GPU's NUMA node (mbind before the pinning touch)."""
     node = device_numa_node(0)

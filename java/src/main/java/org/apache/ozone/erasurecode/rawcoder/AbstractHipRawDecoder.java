@@ -1,6 +1,7 @@
 package org.apache.ozone.erasurecode.rawcoder;
 
 import java.io.IOException;
+import java.nio.ByteBuffer;
 import java.util.concurrent.locks.ReentrantReadWriteLock;
 
 import org.apache.hadoop.hdds.client.ECReplicationConfig;
@@ -55,6 +56,27 @@ abstract class AbstractHipRawDecoder extends RawErasureDecoder {
     try {
       OzecNative.decodeArrays(handleOrThrow(), state.inputs, state.inputOffsets, state.decodeLength,
           state.erasedIndexes, state.outputs, state.outputOffsets);
+    } finally {
+      lock.readLock().unlock();
+    }
+  }
+
+  /**
+   * Reconstruct many stripes in one call (ECReconstructionCoordinator's read buffers): verify the stored checksums of
+   * the units read, rebuild the erased units and checksum them, pipelined over PCIe (ozec_reconstruct_crc_host_batch).
+   * All buffers are direct (OzecNative.allocatePinned for DMA in place) and read from their start:
+   * stripes [numStripes][k+p][cellLength] at stripeStride / unitStride; out [numStripes][erased][cellLength];
+   * outChecksums [numStripes][erased][windows] and expectedChecksums [numStripes][k+p][windows] as 4-byte big-endian
+   * values (the ByteStrings of ChecksumData); mismatch [numStripes] native-order ints, -1 or the first failing
+   * unit * windows + window.  expectedChecksums and mismatch may be null (no verification).
+   */
+  public void reconstructBatch(ByteBuffer stripes, long stripeStride, long unitStride, int[] presentUnits,
+      int[] erasedIndexes, ByteBuffer out, int numStripes, int cellLength, int checksumType, int bytesPerChecksum,
+      ByteBuffer expectedChecksums, ByteBuffer outChecksums, ByteBuffer mismatch) throws IOException {
+    lock.readLock().lock();
+    try {
+      OzecNative.reconstructHostBatch(handleOrThrow(), stripes, stripeStride, unitStride, presentUnits, erasedIndexes,
+          out, numStripes, cellLength, checksumType, bytesPerChecksum, expectedChecksums, outChecksums, mismatch);
     } finally {
       lock.readLock().unlock();
     }

@@ -96,4 +96,9 @@ public final class OzecNative {
   static native void queueWait(long queue, long ticket);
 
   static native void queueFree(long queue);
+
+  // ---- batch reconstruction from host buffers (ozec_reconstruct_crc_host_batch, SURVEY §8(f) row 1)
+  static native void reconstructHostBatch(long decoder, ByteBuffer stripes, long stripeStride, long unitStride,
+      int[] presentUnits, int[] erasedIndexes, ByteBuffer out, int numStripes, int cellLength, int checksumType,
+      int bytesPerChecksum, ByteBuffer expectedChecksums, ByteBuffer outChecksums, ByteBuffer mismatch);
 }

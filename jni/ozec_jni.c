@@ -393,3 +393,43 @@ JNIEXPORT void JNICALL JNI_FN(queueFree)(JNIEnv *env, jclass cls, jlong q) {
   int rc = ozec_stripe_queue_free((ozec_stripe_queue *)(intptr_t)q);
   if (rc) throw_rc(env, rc);
 }
+
+/* ---------------------------------------------------------------- batch reconstruction (§8(f) row 1 on host buffers) */
+
+/* a direct buffer as an ozm_buf from its start (the Java side slices it; no buffer position is read here) */
+static ozm_buf direct_buf(JNIEnv *env, jobject b) {
+  ozm_buf r = {NULL, 0, -1, 0};
+  if (!b) return r;
+  r.base = (*env)->GetDirectBufferAddress(env, b);
+  r.capacity = (*env)->GetDirectBufferCapacity(env, b);
+  r.present = 1;
+  return r;
+}
+
+/* reconstructHostBatch(decoder, stripes, stripeStride, unitStride, present[], erased[], out, numStripes, cellLen,
+ * checksumType, bytesPerChecksum, expected, outCrcs, mismatch): every buffer direct (allocatePinned for DMA in
+ * place); CRC buffers hold big-endian ints as ChecksumData's ByteStrings do. */
+JNIEXPORT void JNICALL JNI_FN(reconstructHostBatch)(JNIEnv *env, jclass cls, jlong dec, jobject stripes,
+                                                    jlong stripeStride, jlong unitStride, jintArray present,
+                                                    jintArray erased, jobject out, jint numStripes, jint cellLen,
+                                                    jint type, jint bpc, jobject expected, jobject outCrcs,
+                                                    jobject mismatch) {
+  (void)cls;
+  ozm_status st;
+  int pr[MAX_BUFS], er[MAX_BUFS], npr = 0, ner = 0;
+  if (int_array(env, present, pr, MAX_BUFS, &npr, &st) || int_array(env, erased, er, MAX_BUFS, &ner, &st)) {
+    throw_status(env, &st);
+    return;
+  }
+  const ozm_buf sb = direct_buf(env, stripes), ob = direct_buf(env, out), eb = direct_buf(env, expected),
+                cb = direct_buf(env, outCrcs), mb = direct_buf(env, mismatch);
+  if ((stripes && !sb.base) || (out && !ob.base) || (expected && !eb.base) || (outCrcs && !cb.base) ||
+      (mismatch && !mb.base)) {
+    ozm_fail(OZEC_EINVAL, "reconstructHostBatch needs direct buffers", &st);
+    throw_status(env, &st);
+    return;
+  }
+  if (ozm_reconstruct_host_batch((ozec_coder *)(intptr_t)dec, &sb, stripeStride, unitStride, pr, npr, er, ner, &ob,
+                                 numStripes, cellLen, type, bpc, &eb, &cb, &mb, &st))
+    throw_status(env, &st);
+}

@@ -124,3 +124,51 @@ int ozm_checksum_windows(int checksum_type, const ozm_buf *buf, int64_t len, int
   if (written) *written = 4 * nwin;
   return ok(st);
 }
+
+/* bytes a buffer must hold from its offset, or fail */
+static int need(const ozm_buf *b, int64_t bytes, const char *what, const uint8_t **out, ozm_status *st) {
+  char msg[128];
+  if (!b || !b->present || !b->base) {
+    snprintf(msg, sizeof(msg), "%s buffer missing", what);
+    return ozm_fail(OZEC_EINVAL, msg, st);
+  }
+  if (b->offset < 0 || (b->capacity >= 0 && b->offset + bytes > b->capacity)) {
+    snprintf(msg, sizeof(msg), "%s buffer too small: %lld bytes needed", what, (long long)bytes);
+    return ozm_fail(OZEC_EINVAL, msg, st);
+  }
+  *out = (const uint8_t *)b->base + b->offset;
+  return ok(st);
+}
+
+int ozm_reconstruct_host_batch(ozec_coder *dec, const ozm_buf *stripes, int64_t stripe_stride, int64_t unit_stride,
+                               const int *present, int npresent, const int *erased, int nerased, const ozm_buf *out,
+                               int64_t num_stripes, int64_t cell_len, int checksum_type, int64_t bpc,
+                               const ozm_buf *expected, const ozm_buf *out_crcs, const ozm_buf *mismatch,
+                               ozm_status *st) {
+  int k = 0, p = 0;
+  if (coder_shape(dec, 1, &k, &p, st)) return st ? st->code : OZEC_EINVAL;
+  if (num_stripes < 0 || cell_len < 0 || stripe_stride < 0 || unit_stride < 0)
+    return ozm_fail(OZEC_EINVAL, "negative size or stride", st);
+  if (bpc <= 0) return ozm_fail(OZEC_EINVAL, "bytesPerChecksum must be positive", st);
+  if (nerased < 0 || (nerased > 0 && !erased) || npresent < 0 || (npresent > 0 && !present))
+    return ozm_fail(OZEC_EINVAL, "erasedIndexes and outputs mismatch in length", st);
+  if (nerased > p) return ozm_fail(OZEC_EINVAL, "Too many erased, not recoverable", st);
+  if (num_stripes == 0 || cell_len == 0) return ok(st);
+  const int64_t nwin = (cell_len + bpc - 1) / bpc, S = num_stripes;
+  const uint8_t *in = NULL, *o = NULL, *oc = NULL, *ex = NULL, *mm = NULL;
+  if (need(stripes, (S - 1) * stripe_stride + (int64_t)(k + p - 1) * unit_stride + cell_len, "stripe", &in, st))
+    return st ? st->code : OZEC_EINVAL;
+  if (nerased && (need(out, S * nerased * cell_len, "output", &o, st) ||
+                  need(out_crcs, S * nerased * nwin * 4, "checksum output", &oc, st)))
+    return st ? st->code : OZEC_EINVAL;
+  if (expected && expected->present) {
+    if (need(expected, S * (k + p) * nwin * 4, "expected checksum", &ex, st) ||
+        need(mismatch, S * 4, "mismatch", &mm, st))
+      return st ? st->code : OZEC_EINVAL;
+  }
+  int rc = ozec_reconstruct_crc_host_batch(dec, in, stripe_stride, unit_stride, present, npresent, erased, nerased,
+                                           (uint8_t *)o, nerased * cell_len, cell_len, (size_t)S, (size_t)cell_len,
+                                           checksum_type, (size_t)bpc, (const uint32_t *)ex, 1, (uint32_t *)oc, 1,
+                                           (int32_t *)mm, 0);
+  return rc ? ozm_fail(rc, NULL, st) : ok(st);
+}

@@ -72,6 +72,18 @@ int ozm_crc_update(int checksum_type, uint32_t *state, const ozm_buf *buf, int64
 int ozm_checksum_windows(int checksum_type, const ozm_buf *buf, int64_t len, int64_t bytes_per_checksum,
                          uint8_t *out, int64_t out_cap, int64_t *written, ozm_status *st);
 
+/* Batch reconstruction of stripes held in direct buffers (ECReconstructionCoordinator's read buffers; libozec
+ * ozec_reconstruct_crc_host_batch).  stripes: [S][k+p][cell_len] at stripe_stride / unit_stride (absent and erased
+ * units are never read); out: [S][nerased][cell_len]; out_crcs: [S][nerased][nwin] and expected: [S][k+p][nwin]
+ * 4-byte big-endian values (Ints.toByteArray, Checksum.java:59-70); mismatch: [S] native-order ints, -1 or the first
+ * failing unit * nwin + window.  expected (and mismatch) may be absent: no verification.  Every buffer's capacity is
+ * checked against its layout before anything runs. */
+int ozm_reconstruct_host_batch(ozec_coder *dec, const ozm_buf *stripes, int64_t stripe_stride, int64_t unit_stride,
+                               const int *present, int npresent, const int *erased, int nerased, const ozm_buf *out,
+                               int64_t num_stripes, int64_t cell_len, int checksum_type, int64_t bytes_per_checksum,
+                               const ozm_buf *expected, const ozm_buf *out_crcs, const ozm_buf *mismatch,
+                               ozm_status *st);
+
 #ifdef __cplusplus
 }
 #endif

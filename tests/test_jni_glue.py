@@ -52,7 +52,8 @@ def J():
         (P + "allocatePinned", vp, [vp, vp, i32]), (P + "freePinned", None, [vp, vp, vp]),
         (P + "queueCreate", i64, [vp, vp, i64, i32, i32, i32, i32]),
         (P + "queueSubmit", i64, [vp, vp, i64, vp, vp, vp, vp, i32, vp]),
-        (P + "queueWait", None, [vp, vp, i64, i64]), (P + "queueFree", None, [vp, vp, i64])]:
+        (P + "queueWait", None, [vp, vp, i64, i64]), (P + "queueFree", None, [vp, vp, i64]),
+        (P + "reconstructHostBatch", None, [vp, vp, i64, vp, i64, i64, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp])]:
         fn = getattr(L, name)
         fn.restype, fn.argtypes = res, args
     L.env = L.mock_env()
@@ -274,3 +275,76 @@ def test_pinned_buffers_and_stripe_queue_through_jni(J, java):
             J.mock_free(pb)
         call(J, "coderRelease", h)
     assert java.exception() is None
+
+
+def test_reconstruct_batch_argument_errors(J, java):
+    """reconstructHostBatch: heap buffers and a closed handle raise the reference's exceptions before anything runs
+    (size checks against a live decoder: test_reconstruct_batch_through_jni)."""
+    k, p, n, S, bpc = 6, 3, 4096, 2, 4096
+    stripes = np.zeros(S * (k + p) * n, np.uint8)
+    out, crc = np.zeros(S * n, np.uint8), np.zeros(S * 4, np.uint8)
+    present, erased = list(range(1, 9)), [0]
+    call(J, "reconstructHostBatch", 0, java.heap(stripes), (k + p) * n, n, java.ints(present), java.ints(erased),
+         java.direct(out), S, n, 3, bpc, None, java.direct(crc), None)
+    assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"  # not a direct buffer
+    call(J, "reconstructHostBatch", 0, java.direct(stripes), (k + p) * n, n, java.ints(present), java.ints(erased),
+         java.direct(out), S, n, 3, bpc, None, java.direct(crc), None)
+    ex = java.exception()
+    assert ex and ex[0] == "java/io/IOException" and "closed" in ex[1]
+
+
+@pytest.mark.gpu
+def test_reconstruct_batch_through_jni(J, java):
+    """reconstructHostBatch over pinned direct buffers vs the oracle: rebuilt units, their big-endian CRCs and the
+    per-stripe verdicts (one stripe corrupted)."""
+    k, p, n, S, bpc = 10, 4, 1 << 15, 5, 4096
+    nwin = n // bpc
+    h = call(J, "coderCreate", 1, 0, k, p)
+    pbs = []
+    try:
+        def pinned(nbytes):
+            pb = call(J, "allocatePinned", nbytes)
+            assert java.exception() is None and pb
+            pbs.append(pb)
+            return pb, np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(J.mock_data(pb)))
+        sb, sv = pinned(S * (k + p) * n)
+        eb, ev = pinned(S * (k + p) * nwin * 4)
+        ob, ov = pinned(S * 4 * n)
+        cb, cv = pinned(S * 4 * nwin * 4)
+        mb, mv = pinned(S * 4)
+        stripes = sv.reshape(S, k + p, n)
+        for s in range(S):
+            d = cells(SEED, 745000 + s * k, k, n)
+            for u, x in enumerate(d + oracle.rs_encode(k, p, d)):
+                stripes[s, u] = x
+        orig = stripes.copy()
+        ev.view(np.uint32)[:] = np.concatenate([oracle.crc_windows(oracle.CRC32C, orig[s, u], bpc)
+                                                for s in range(S) for u in range(k + p)]).byteswap()
+        erased = [1, 4, 10, 13]
+        present = [u for u in range(k + p) if u not in erased]
+        small = java.direct(np.zeros(n, np.uint8))
+        call(J, "reconstructHostBatch", h, sb, (k + p) * n, n, java.ints(present), java.ints(erased), small, S, n, 3,
+             bpc, eb, cb, mb)
+        ex = java.exception()
+        assert ex[0] == "org/apache/hadoop/HadoopIllegalArgumentException" and "too small" in ex[1]
+        call(J, "reconstructHostBatch", h, sb, (k + p) * n, n, java.ints(present[:9]), java.ints(erased + [0]), ob, S,
+             n, 3, bpc, eb, cb, mb)
+        assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"  # 5 erased of 4 parity
+        stripes[:, erased] = 0
+        stripes[3, 12, 5] ^= 0x80                 # stripe 3: the last unit read is corrupted in window 0
+        call(J, "reconstructHostBatch", h, sb, (k + p) * n, n, java.ints(present), java.ints(erased), ob, S, n, 3, bpc,
+             eb, cb, mb)
+        assert java.exception() is None
+        got, crcs, mism = ov.reshape(S, 4, n), cv.view(np.uint32).reshape(S, 4, nwin), mv.view(np.int32)
+        assert list(mism) == [-1, -1, -1, 12 * nwin + 0, -1]
+        for s in (0, 1, 2, 4):
+            for i, u in enumerate(erased):
+                assert (got[s, i] == orig[s, u]).all(), (s, u)
+                assert (crcs[s, i].byteswap() == oracle.crc_windows(oracle.CRC32C, orig[s, u], bpc)).all(), (s, u)
+    finally:
+        for pb in pbs:
+            call(J, "freePinned", pb)
+            J.mock_free(pb)
+        call(J, "coderRelease", h)
+    assert java.exception() is None
+

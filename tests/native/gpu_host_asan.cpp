@@ -226,6 +226,55 @@ static void stripe_queue() {
   ozec_coder_free(enc);
 }
 
+// reconstruction host batch (the new pipeline): pageable exact-size buffers, mixed erasures (several runs)
+static void recon_batch(bool register_in) {
+  ozec_coder *enc = nullptr, *dec = nullptr;
+  const int k = 10, p = 4;
+  CHECK(ozec_encoder_create(OZEC_CODEC_RS, k, p, &enc) == OZEC_OK, "encoder");
+  CHECK(ozec_decoder_create(OZEC_CODEC_RS, k, p, &dec) == OZEC_OK, "decoder");
+  const size_t len = 1 << 15, bpc = 4096, S = 11, nwin = len / bpc;
+  const int64_t unit = len, stripe = (k + p) * unit;
+  Buf batch(S * stripe, 0);
+  batch.fill();
+  for (size_t s = 0; s < S; ++s) {  // parity of every stripe from the oracle: the stored stripes are consistent
+    const uint8_t *in[10];
+    uint8_t *out[4];
+    for (int j = 0; j < k; ++j) in[j] = batch.p + s * stripe + j * unit;
+    for (int r = 0; r < p; ++r) out[r] = batch.p + s * stripe + (k + r) * unit;
+    oracle_rs_encode(k, p, static_cast<int>(len), in, out);
+  }
+  std::vector<uint32_t> stored(S * (k + p) * nwin);
+  for (size_t s = 0; s < S; ++s)
+    for (int u = 0; u < k + p; ++u) oracle_crc_windows(1, batch.p + s * stripe + u * unit, len, bpc, &stored[(s * (k + p) + u) * nwin]);
+  std::vector<uint8_t> orig(batch.p, batch.p + S * stripe);
+  const int erased[4] = {1, 4, 10, 13};
+  int present[10], np_ = 0;
+  for (int u = 0; u < k + p; ++u)
+    if (u != 1 && u != 4 && u != 10 && u != 13) present[np_++] = u;
+  for (size_t s = 0; s < S; ++s)
+    for (int e : erased) std::memset(batch.p + s * stripe + e * unit, 0xEE, len);
+  Buf exp(S * (k + p) * nwin * 4, 1), out(S * 4 * len, 2), ocrc(S * 4 * nwin * 4, 3), mism(S * 4, 1);
+  std::memcpy(exp.p, stored.data(), exp.n);
+  if (register_in) CHECK(ozec_host_register(batch.p, batch.n, 0) == OZEC_OK, "register");
+  CHECK(ozec_reconstruct_crc_host_batch(dec, batch.p, stripe, unit, present, np_, erased, 4, out.p, 4 * len, len, S, len,
+                                        OZEC_CHECKSUM_CRC32C, bpc, reinterpret_cast<uint32_t *>(exp.p), 0,
+                                        reinterpret_cast<uint32_t *>(ocrc.p), 0, reinterpret_cast<int32_t *>(mism.p),
+                                        3) == OZEC_OK,
+        "reconstruct host batch");
+  if (register_in) CHECK(ozec_host_unregister(batch.p) == OZEC_OK, "unregister");
+  for (size_t s = 0; s < S; ++s) {
+    int32_t m;
+    std::memcpy(&m, mism.p + 4 * s, 4);  // the caller's buffer is misaligned on purpose
+    CHECK(m == -1, "stripe %zu mismatch %d", s, m);
+    for (int i = 0; i < 4; ++i) {
+      CHECK(!std::memcmp(out.p + (s * 4 + i) * len, orig.data() + s * stripe + erased[i] * unit, len), "rebuilt %zu/%d", s, i);
+      CHECK(!std::memcmp(ocrc.p + (s * 4 + i) * nwin * 4, &stored[(s * (k + p) + erased[i]) * nwin], nwin * 4), "crc %zu/%d", s, i);
+    }
+  }
+  ozec_coder_free(enc);
+  ozec_coder_free(dec);
+}
+
 int main() {
   if (ozec_device_count() < 1) {
     std::printf("no GPU\n");
@@ -242,6 +291,8 @@ int main() {
   host_batch(false);
   host_batch(true);
   stripe_queue();
+  recon_batch(false);
+  recon_batch(true);
   std::printf("gpu host paths under ASan+UBSan: %s\n", g_fail ? "FAILED" : "ok");
   return g_fail ? 1 : 0;
 }

@@ -112,7 +112,8 @@ struct DevCtx {
   std::vector<std::unique_ptr<Slot>> slots;
   std::vector<Slot *> free_slots;
   uint32_t *crc_tables[2][3] = {};  // [type][B = 1, 2, 4]
-  uint32_t *g26_tables[2][5] = {};  // [type][kG26Cfg slot]
+  uint32_t *g26_tables[2][ozec::kG26Slots] = {};  // [type][kG26Cfg slot]
+  uint32_t *nib_tables[2] = {};                   // [type]
 
   int acquire(Slot **out) {
     std::unique_lock<std::mutex> lk(pool_mu);
@@ -176,11 +177,16 @@ int get_ctx(DevCtx **out) {
         OZEC_HIP(hipMemcpy(c->crc_tables[t][b], blob.data(), blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
       }
     for (int t = 0; t < 2; ++t)
-      for (int i = 0; i < 5; ++i) {
+      for (int i = 0; i < ozec::kG26Slots; ++i) {
         const auto &blob = CrcMath::get(static_cast<CrcType>(t)).g26_tables(i);
         OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->g26_tables[t][i]), blob.size() * sizeof(uint32_t)));
         OZEC_HIP(hipMemcpy(c->g26_tables[t][i], blob.data(), blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
       }
+    for (int t = 0; t < 2; ++t) {
+      const auto &blob = CrcMath::get(static_cast<CrcType>(t)).nib_tables();
+      OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->nib_tables[t]), blob.size() * sizeof(uint32_t)));
+      OZEC_HIP(hipMemcpy(c->nib_tables[t], blob.data(), blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     g_ctx[dev] = std::move(c);
   }
   *out = g_ctx[dev].get();
@@ -661,7 +667,8 @@ static int make_crc_args(DevCtx *ctx, int checksum_type, const uint8_t *d_base, 
   a->out = d_out;
   a->out_cell_stride = out_cell_stride;
   for (int b = 0; b < 3; ++b) a->tables[b] = ctx->crc_tables[static_cast<int>(t)][b];
-  for (int i = 0; i < 5; ++i) a->g26[i] = ctx->g26_tables[static_cast<int>(t)][i];
+  for (int i = 0; i < ozec::kG26Slots; ++i) a->g26[i] = ctx->g26_tables[static_cast<int>(t)][i];
+  a->nib = ctx->nib_tables[static_cast<int>(t)];
   a->init_full = cm.shift(0xffffffffu, bpc);
   a->init_last = cm.shift(0xffffffffu, len - (a->nwin ? (a->nwin - 1) * bpc : 0));
   a->big_endian = big_endian;

@@ -40,7 +40,19 @@ CrcMath::CrcMath(uint32_t poly) : poly_(poly) {
   blob_b1_ = build_blob(1);
   blob_b2_ = build_blob(2);
   blob_b4_ = build_blob(4);
-  for (int i = 0; i < 5; ++i) g26_[i] = build_g26(kG26Cfg[i][0], kG26Cfg[i][1]);
+  for (int i = 0; i < kG26Slots; ++i) g26_[i] = build_g26(kG26Cfg[i][0], kG26Cfg[i][1]);
+  // nibble tables: the G26 block map split into 32 nibble-indexed tables per distance set
+  nib_.assign(kNibWords, 0);
+  uint32_t bit[128];
+  for (int p = 0; p < 128; ++p) bit[p] = shift(t0_[1u << (p & 7)], 15 - (p >> 3));
+  for (int e = 0; e < kNibSets; ++e)
+    for (int p = 0; p < 32; ++p)
+      for (uint32_t n = 0; n < 16; ++n) {
+        uint32_t acc = 0;
+        for (int i = 0; i < 4; ++i)
+          if ((n >> i) & 1) acc ^= bit[4 * p + i];
+        nib_[(e * 32 + p) * 16 + n] = shift(acc, static_cast<uint64_t>(e) * 1024);
+      }
 }
 
 // Block bit (0..127; dword d bit k = 32d + k, i.e. byte p/8 bit p%8) that index bit i of G26 table g reads,

@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <vector>
 
+#include "kernels.hpp"
+
 namespace ozec {
 
 enum class CrcType { kCrc32 = 0, kCrc32c = 1 };
@@ -21,6 +23,8 @@ class CrcMath {
   const std::vector<uint32_t> &device_tables(int B) const { return B == 1 ? blob_b1_ : B == 2 ? blob_b2_ : blob_b4_; }
   // the device G26 table blob (kernels.hpp kG26*) for slot `slot` of kG26Cfg
   const std::vector<uint32_t> &g26_tables(int slot) const { return g26_[slot]; }
+  // the device nibble blob (kernels.hpp kNib*)
+  const std::vector<uint32_t> &nib_tables() const { return nib_; }
   uint32_t byte_table(int v) const { return t0_[v]; }
   uint32_t poly() const { return poly_; }
   // x^(8n) mod P in CrcUtil's reversed representation (CrcUtil.getMonomial)
@@ -43,7 +47,8 @@ class CrcMath {
   // op_[i] = operator for 2^i zero BYTES as a 32x32 GF(2) matrix (column c = image of bit c)
   uint32_t op_[64][32];
   std::vector<uint32_t> blob_b1_, blob_b2_, blob_b4_;
-  std::vector<uint32_t> g26_[5];
+  std::vector<uint32_t> g26_[kG26Slots];
+  std::vector<uint32_t> nib_;
   std::vector<uint32_t> build_blob(int B) const;
   std::vector<uint32_t> build_g26(int B, int D) const;
 };

@@ -242,6 +242,245 @@ hipError_t launch_lv_kr(const EncCrcArgs &e, hipStream_t st, int v) {
   else return launch_lv<K, R, 4, 2, 4, 6, false, 3>(e, st);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Nibble-table fused kernel: the GF products and the CRC of every input share their LDS lookups.
+//
+// encode_crc_lv spends ~23 VALU per input dword on the GF part (5 selector ops + 3 v_perm + 1.5 XOR per output)
+// and ~12 per input dword on the CRC index math, and is VALU-issue bound.  Here every nibble n of
+// every input byte is looked up ONCE, with one ds_read_b64, in a table whose 8-B entry holds
+//   .x = the products c_rj * n (n shifted to its nibble half) for the R outputs, byte r = output r,
+//   .y = the raw-CRC contribution of n at its nibble position in the 16-B block (kNib* tables, distance set d).
+// Per input block: 32 index ops (one SDWA op each: (byte << 4) & 0xf0 and byte & 0xf0), 32 lookups, 16 XORs
+// into per-byte-position GF accumulators A[i] and 16 into the unit's CRC register -- 64 VALU against ~141 for
+// rs-10-4 in encode_crc_lv.  A[i] holds the R output bytes of byte position i; a 4x4 byte transpose (8 v_perm per
+// dword for R = 4) turns them into the R output dwords, whose CRCs use the G26 lookups as before.
+//
+// Tables: for each distance set d (D of them), input j and nibble position p, 16 entries of 8 B at a 16-B stride
+// with the tables of p and p ^ 1 interleaved (+0 / +8): under ds_read_b64 banking ((a/4) mod 64) the 16 entries
+// of a table cover 32 distinct banks, so random nibbles never conflict.  K*D*4 KiB of LDS (40 KiB for rs-10-4 at
+// D = 1), built once per workgroup; the grid is persistent (one resident set of workgroups).
+// Windows must be full and a whole number of D-step groups, as for encode_crc_lv.
+__device__ __forceinline__ uint32_t nib_lo_idx(uint32_t w, int q, uint32_t v4) {  // ((byte_q << 4) & 0xf0)
+  uint32_t d;
+  switch (q) {
+    case 0: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(d) : "v"(v4), "v"(w)); break;
+    case 1: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(d) : "v"(v4), "v"(w)); break;
+    case 2: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(d) : "v"(v4), "v"(w)); break;
+    default: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(d) : "v"(v4), "v"(w)); break;
+  }
+  return d;
+}
+__device__ __forceinline__ uint32_t nib_hi_idx(uint32_t w, int q, uint32_t vf0) {  // (byte_q & 0xf0)
+  uint32_t d;
+  switch (q) {
+    case 0: asm("v_and_b32 %0, %1, %2" : "=v"(d) : "v"(vf0), "v"(w)); break;
+    case 1: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(d) : "v"(w), "v"(vf0)); break;
+    case 2: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "=v"(d) : "v"(w), "v"(vf0)); break;
+    default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(d) : "v"(w), "v"(vf0)); break;
+  }
+  return d;
+}
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32));
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+__device__ __forceinline__ uint2 lds64(const void *base, uint32_t byte_off) {
+  return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + byte_off);
+}
+
+// byte offset of the entry region of (distance set d, input j, byte i): lo-nibble table at +0, hi at +8
+template <int K>
+constexpr uint32_t nb_region(int d, int j, int i) {
+  return static_cast<uint32_t>(((d * K + j) * 16 + i) * 256);
+}
+
+// K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
+// HALF: lookups of a block in two fenced halves of 8 bytes (at most 16 results live)
+template <int K, int R, int D, int NB, int WPB, int WAVES, bool HALF = true>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
+    const EncCrcArgs e) {
+  static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
+  static_assert(D <= kNibSets, "distance sets of the nibble blob");
+  static_assert((D * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
+  static_assert(K * D * 4096 + g26_words(D) * 4 <= 65536, "LDS offsets must fit the ds_read offset field");
+  __shared__ __attribute__((aligned(256))) uint2 s_c[K * D * 512];  // (d, j, p) tables, 16 entries each
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(D)];
+  __shared__ uint32_t s_gf[K * 32];  // GF dword of (j, nibble half h, n)
+  const CodeArgs &a = e.code;
+  const CrcArgs &cr = e.crc;
+  for (int t = threadIdx.x; t < K * 32; t += blockDim.x) {
+    const int j = t >> 5, h = (t >> 4) & 1, n = t & 15;
+    uint32_t dw = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) dw |= gf_mul_byte(a.coef[r * K + j], static_cast<uint32_t>(n) << (4 * h)) << (8 * r);
+    s_gf[t] = dw;
+  }
+  load_tables(s_t, cr.g26[g26_slot(1, D)], g26_words(D));
+  __syncthreads();
+  for (int q = threadIdx.x; q < K * D * 512; q += blockDim.x) {
+    const int t = q >> 4, n = q & 15, p = t & 31, dj = t >> 5, j = dj % K, d = dj / K;
+    const uint32_t off = static_cast<uint32_t>((t >> 1) * 256 + n * 16 + (t & 1) * 8);
+    s_c[off >> 3] = make_uint2(s_gf[j * 32 + (p & 1) * 16 + n], cr.nib[(d * 32 + p) * 16 + n]);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwin = cr.nwin;
+  const int64_t units = a.nstripes * nwin;
+  const int32_t T = static_cast<int32_t>(cr.bpc >> 10);  // steps per window
+  const int32_t G = T / D;                                // groups per window
+  const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
+  uint32_t v4, vf0;  // index-op operands in VGPRs (VOP2/SDWA with no SGPR or literal operand issue fastest)
+  asm volatile("v_mov_b32 %0, 4" : "=v"(v4));
+  asm volatile("v_mov_b32 %0, 0xf0" : "=v"(vf0));
+  int64_t off_max = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
+  const uint32_t in_extent = static_cast<uint32_t>(off_max + cr.bpc);
+  for (int64_t u = static_cast<int64_t>(blockIdx.x) * WPB + wave; u < units; u += static_cast<int64_t>(gridDim.x) * WPB) {
+    // wave-uniform by construction; said explicitly so the descriptors below stay in SGPRs (the 64-bit division
+    // runs in the VALU, and without this the buffer accesses were wrapped in waterfall loops)
+    const int64_t s = uniform64(u / nwin);
+    const int64_t w = uniform64(u - s * nwin);
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
+    auto vstep = [&](int32_t t) { return voff + (t < T ? static_cast<uint32_t>(t) * 1024u : 0x80000000u); };
+    auto load = [&](uint32_t vo, int j) {
+      const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, vo, static_cast<int>(a.in_off[j]), 2);
+      return make_uint4(d[0], d[1], d[2], d[3]);
+    };
+    uint32_t S[K + R];
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) S[q] = 0;
+    uint4 ring[NB];
+#pragma unroll
+    for (int i = 0; i + 1 < NB; ++i) ring[i] = load(vstep(i / K), i % K);
+    for (int32_t g = 0; g < G; ++g) {
+#pragma unroll
+      for (int rr = 0; rr < D; ++rr) {
+        const int32_t t = g * D + rr;
+        const int d = D - 1 - rr;  // distance set of this step
+        const uint32_t vcur = vstep(t), vnext = vstep(t + 1);
+        uint32_t A[16];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int ii = rr * K + j;
+          const int ahead = ii + NB - 1;
+          static_assert(NB - 1 <= K, "look-ahead of at most one step");
+          ring[ahead % NB] = load(ahead / K == rr ? vcur : vnext, ahead % K);
+          const uint4 x = ring[ii % NB];
+          const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+          XorChain ch;
+          ch.push(S[j]);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (HALF && c == 2) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int i = 4 * c + q;
+              const uint2 lo = lds64(s_c, nb_region<K>(d, j, i) + nib_lo_idx(xw[c], q, v4));
+              const uint2 hi = lds64(s_c, nb_region<K>(d, j, i) + 8 + nib_hi_idx(xw[c], q, vf0));
+              A[i] = j == 0 ? (lo.x ^ hi.x) : xor3(A[i], lo.x, hi.x);
+              ch.push(lo.y);
+              ch.push(hi.y);
+            }
+          }
+          S[j] = ch.get();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // 4x4 byte transposes: A[4c + q] byte r -> output r, dword c, byte q
+        uint32_t o[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t a0 = A[4 * c], a1 = A[4 * c + 1], a2 = A[4 * c + 2], a3 = A[4 * c + 3];
+          const uint32_t l01 = __builtin_amdgcn_perm(a1, a0, 0x05010400u), l23 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
+          o[0][c] = __builtin_amdgcn_perm(l23, l01, 0x05040100u);
+          if constexpr (R > 1) o[1][c] = __builtin_amdgcn_perm(l23, l01, 0x07060302u);
+          if constexpr (R > 2) {
+            const uint32_t h01 = __builtin_amdgcn_perm(a1, a0, 0x07030602u), h23 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+            o[2][c] = __builtin_amdgcn_perm(h23, h01, 0x05040100u);
+            if constexpr (R > 3) o[3][c] = __builtin_amdgcn_perm(h23, h01, 0x07060302u);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint4 p = make_uint4(o[r][0], o[r][1], o[r][2], o[r][3]);
+          __attribute__((ext_vector_type(4))) unsigned int dv = {p.x, p.y, p.z, p.w};
+          __builtin_amdgcn_raw_buffer_store_b128(dv, rout, vcur, static_cast<int>(a.out_off[r]), 2);
+          store_data_hold(p);
+          S[K + r] ^= g26_block<true>(s_t + d * kG26Set, p);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (g + 1 < G) {
+#pragma unroll
+        for (int q = 0; q < K + R; ++q) S[q] = g5_shift(s_t + g26_gshift(D), S[q]);
+      }
+    }
+    const bool last = w == nwin - 1;
+    const uint32_t init = last ? cr.init_last : cr.init_full;
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) {
+      const uint32_t v = g5_lane_tree(s_t + g26_tree(D) - kG5Tree, S[q], lane);
+      if (lane == q) {
+        if (!e.verify) {
+          cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+        } else if (q >= K) {
+          cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+        } else if (cr.expected) {
+          const int64_t idx = (s * e.exp_units + e.in_unit[q]) * nwin + w;
+          const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
+          if (crc_finish(v, init, 0, 0) != ex) atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
+        }
+      }
+    }
+  }
+}
+
+template <int K, int R, int D, int NB, int WPB, int WAVES, bool HALF = true>
+hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
+  if constexpr ((D * K) % NB != 0) {
+    return launch_nb<K, R, D, 2, WPB, WAVES, HALF>(e, st);
+  } else {
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, HALF>;
+    // persistent grid: every workgroup builds K*D*4 KiB of tables once, so launch one resident set
+    static int resident = 0;  // workgroups per CU x CUs, per instantiation and process (one device type)
+    if (resident == 0) {
+      int dev = 0, cus = 0, per_cu = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WPB * 64, 0) != hipSuccess)
+        return hipErrorInvalidValue;
+      resident = std::max(1, cus * std::max(1, per_cu));
+    }
+    const int64_t units = e.code.nstripes * e.crc.nwin;
+    const int64_t blocks = (units + WPB - 1) / WPB;
+    const int64_t g = std::min<int64_t>(g_tune.crc_grid > 0 ? g_tune.crc_grid : resident, blocks);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, e);
+    return hipGetLastError();
+  }
+}
+
+// variant (g_tune.crc_variant): 60-69 nibble-table kernel step groups / ring / occupancy A/B
+template <int K, int R>
+hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
+  constexpr int kD2 = K * 2 * 4096 + g26_words(2) * 4 <= 65536 ? 2 : 1;  // D = 2 where its tables fit
+  constexpr int kNB = K % 2 == 0 && K > 2 ? K / 2 : K;                    // a deeper ring dividing the group
+  switch (v) {
+    case 61: return launch_nb<K, R, 1, 2, 8, 4>(e, st);
+    case 62: return launch_nb<K, R, 1, kNB, 8, 4>(e, st);
+    case 63: return launch_nb<K, R, kD2, 2, 8, 4>(e, st);
+    case 64: return launch_nb<K, R, kD2, kNB, 8, 4>(e, st);
+    case 65: return launch_nb<K, R, 1, 2, 8, 5>(e, st);
+    case 66: return launch_nb<K, R, 1, 2, 8, 4, false>(e, st);
+    case 67: return launch_nb<K, R, 1, 2, 4, 4>(e, st);
+    default: break;
+  }
+  return launch_nb<K, R, 1, 2, 8, 4>(e, st);
+}
+
 }  // namespace
 
 bool encode_crc_lv_supported(const EncCrcArgs &e) {
@@ -254,6 +493,16 @@ bool encode_crc_lv_supported(const EncCrcArgs &e) {
 
 hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   const int k = e.code.k, r = e.code.rows;
+  if (v >= 60 && v < 70) {
+    if (k == 6 && r == 3) return launch_nb_kr<6, 3>(e, st, v);
+    if (k == 6 && r == 2) return launch_nb_kr<6, 2>(e, st, v);
+    if (k == 3 && r == 2) return launch_nb_kr<3, 2>(e, st, v);
+    if (k == 10 && r == 4) return launch_nb_kr<10, 4>(e, st, v);
+    if (k == 10 && r == 3) return launch_nb_kr<10, 3>(e, st, v);
+    if (k == 10 && r == 2) return launch_nb_kr<10, 2>(e, st, v);
+    if (k == 10 && r == 1) return launch_nb_kr<10, 1>(e, st, v);
+    return hipErrorInvalidValue;
+  }
   if (k == 6 && r == 3) return launch_lv_kr<6, 3>(e, st, v);
   if (k == 6 && r == 2) return launch_lv_kr<6, 2>(e, st, v);
   if (k == 3 && r == 2) return launch_lv_kr<3, 2>(e, st, v);

@@ -44,7 +44,8 @@ struct CrcArgs {
   uint32_t *out;           // out[c * out_cell_stride + w]
   int64_t out_cell_stride; // in uint32 elements
   const uint32_t *tables[3];  // device G5 table blobs for this CRC type, B = 1, 2, 4 blocks per lane per step
-  const uint32_t *g26[5];     // device G26 table blobs for this CRC type, one per kG26Cfg entry
+  const uint32_t *g26[6];     // device G26 table blobs for this CRC type, one per kG26Cfg entry
+  const uint32_t *nib;        // device nibble table blob for this CRC type (kNib* layout)
   uint32_t init_full;      // shift(0xFFFFFFFF, bpc bytes)
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
@@ -102,10 +103,23 @@ constexpr int g26_tree(int E) { return E * kG26Set + 224; }
 constexpr int g26_t0(int E) { return E * kG26Set + 224 + 1344; }
 constexpr int g26_words(int E) { return E * kG26Set + 224 + 1344 + 256; }
 // (B, D) of each G26 blob slot
-constexpr int kG26Cfg[5][2] = {{1, 4}, {2, 2}, {1, 2}, {2, 4}, {1, 8}};
+constexpr int kG26Slots = 6;
+constexpr int kG26Cfg[kG26Slots][2] = {{1, 4}, {2, 2}, {1, 2}, {2, 4}, {1, 8}, {1, 1}};
 constexpr int g26_slot(int B, int D) {
-  return B == 1 && D == 4 ? 0 : B == 2 && D == 2 ? 1 : B == 1 && D == 2 ? 2 : B == 2 && D == 4 ? 3 : 4;
+  return B == 1 && D == 4   ? 0
+         : B == 2 && D == 2 ? 1
+         : B == 1 && D == 2 ? 2
+         : B == 2 && D == 4 ? 3
+         : B == 1 && D == 1 ? 5
+                            : 4;
 }
+
+// Device CRC "nibble" blob for the nibble-table fused kernel (fused.hip encode_crc_nb): entry
+// [e * 512 + p * 16 + n] = raw-CRC contribution of a 16-B block whose only non-zero nibble is n at nibble position p
+// (block bits 4p..4p+3, i.e. byte p / 2, low nibble for even p), advanced by e * 1024 zero bytes (the block is e
+// steps of a 64-lane wave before the end of its step group).  Same map as the G26 set e of (B = 1, D > e).
+constexpr int kNibSets = 4;
+constexpr int kNibWords = kNibSets * 32 * 16;
 
 // Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.
 struct TuneKnobs {

@@ -380,7 +380,34 @@ def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
             assert (crcs[s, u] == oracle.crc_windows(otype, units[u], bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [11, 12, 13, 14, 15, 16, 17, 49, 51, 52, 53, 54, 55, 56, 57, 58])
+@pytest.mark.parametrize("variant", [61, 63])
+@pytest.mark.parametrize("k,p,n,bpc,S", [(6, 3, 1 << 17, 16384, 3), (10, 4, 1 << 16, 4096, 2), (3, 2, 1 << 17, 8192, 3),
+                                         (6, 2, 1 << 15, 32768, 2), (10, 1, 1 << 16, 16384, 2)])
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
+def test_encode_crc_nibble_kernel_vs_oracle(variant, k, p, n, bpc, S, ctype, otype):
+    """The nibble-table fused kernel (fused.hip encode_crc_nb; 61: one-step groups, 63: two-step groups where the
+    tables fit) for both CRC types and every RS shape it takes, bit-exact vs the oracle."""
+    lib = L.lib()
+    data = np.stack([np.stack(cells(SEED, 54000 + s * k, k, n)) for s in range(S)])
+    nwin = n // bpc
+    d_out = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    try:
+        assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+        e.encode_crc_batch(t(data), k * n, n, d_out, p * n, n, S, n, ctype, bpc, d_crc)
+        par, crcs = h(d_out), h(d_crc).view(np.uint32)
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+    for s in range(S):
+        ref = oracle.rs_encode(k, p, list(data[s]))
+        assert all((par[s, r] == ref[r]).all() for r in range(p)), s
+        for u, cell in enumerate(list(data[s]) + ref):
+            assert (crcs[s, u] == oracle.crc_windows(otype, cell, bpc)).all(), (s, u)
+
+
+@pytest.mark.parametrize("variant", [11, 12, 13, 14, 15, 16, 17, 49, 51, 52, 53, 54, 55, 56, 57, 58,
+                                     61, 62, 63, 64, 65, 66, 67])
 @pytest.mark.parametrize("n,bpc,S", [(1 << 18, 16384, 3), (50000, 4096, 2), (1 << 17, 4096, 2), (1 << 17, 65536, 3)])
 def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
     """Every tuning variant of the rs-6-3 fused encode + CRC32C kernel (per-window kernel: D = 4, prefetch, table
@@ -408,7 +435,7 @@ def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
             assert (crcs[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [0, 11, 17, 49, 51, 54, 55, 57])
+@pytest.mark.parametrize("variant", [0, 11, 17, 49, 51, 54, 55, 57, 61, 62, 63, 64, 65, 66, 67])
 @pytest.mark.parametrize("k,p", [(10, 4), (6, 2), (3, 2), (10, 3), (10, 2), (10, 1)])
 def test_encode_crc_other_shapes_variants_vs_oracle(variant, k, p):
     """Fused encode + CRC32C variants of the other RS shapes (D = 2 default, D = 4, D = 4 with fenced halves)."""

@@ -227,7 +227,7 @@ class Workload:
             self.k, self.p, self.S = k, p, S
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + 4) * n + S * (k + 4) * nwin * 4
-            self.kernel = "encode_crc_lv<10,4> (+H2D of the 10 units read, D2H of the 4 rebuilt, pipelined)"
+            self.kernel = "encode_crc_nb<10,4> (+H2D of the 10 units read, D2H of the 4 rebuilt, pipelined)"
             self.config = {"workload": f"rs-10-4-1024k reconstruction end to end from pinned host memory: H2D of the 10 "
                                        f"units read, verify CRC32C + decode 4 + CRC32C of rebuilt units "
                                        f"{{{','.join(map(str, self.erased))}}}, D2H, {S} stripes",
@@ -271,7 +271,7 @@ class Workload:
             self.k, self.p, self.S = k, p, S
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + p) * n
-            self.kernel = "encode_crc_lv<6,3> via ozec_stripe_queue (+H2D/D2H per cell)"
+            self.kernel = "encode_crc_nb<6,3> via ozec_stripe_queue (+H2D/D2H per cell)"
             self.config = {"workload": f"rs-6-3-1024k + CRC32C/16 KiB through the stripe queue (SURVEY 8(f) row 3) "
                                        f"from {'pinned' if pinned else 'pageable'} host cells, {S} stripes, "
                                        f"batches of 64", "stripes": S}
@@ -395,7 +395,7 @@ class Workload:
             self.mism = torch.empty(S, dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + 4) * n + S * (k + 4) * self.nwin * 4
-            self.kernel = "encode_crc_lv<10,4> (streamed inputs, fused.hip)"
+            self.kernel = "encode_crc_nb<10,4> (nibble tables, fused.hip)"
             self.config = {"workload": "rs-10-4-1024k reconstruction: verify CRC32C of 10 read units + decode 4 + "
                                        f"CRC32C of rebuilt units {{{','.join(map(str, self.erased))}}}, {S} stripes, "
                                        "fused, device-resident",
@@ -408,7 +408,7 @@ class Workload:
             self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
             self.alg_bytes = S * units * n + S * units * self.nwin * 4
-            self.kernel = "encode_crc_g26<2,1>" if k == 2 else f"encode_crc_lv<{k},{p}> (streamed inputs, fused.hip)"
+            self.kernel = "encode_crc_g26<2,1>" if k == 2 else f"encode_crc_nb<{k},{p}> (nibble tables, fused.hip)"
             wl = ("xor-2-1-1024k + CRC32C/16 KiB, stripe-major" if name == "c4s"
                   else "rs-6-3-1024k encode + CRC32C/16 KiB (the C5 kernel without PCIe)")
             self.config = {"workload": f"{wl}, {S} stripes, fused, device-resident", "codec": "xor" if k == 2 else "rs",
@@ -689,13 +689,13 @@ def cpu_baseline(workload, budget_s):
 # ------------------------------------------------------------------------------------------ live PMC traffic
 
 KERNEL_PAT = {"c1": "gf_code_vec<3, 2", "c2": "gf_code_vec<6, 3", "c3": "gf_code_vec<10, 4",
-              "c3r": ("encode_crc_lv<10, 4", "encode_crc_g26<10, 4"), "c4": "encode_crc_g26<2, 1",
-              "c4s": "encode_crc_g26<2, 1", "c5dev": ("encode_crc_lv<6, 3", "encode_crc_g26<6, 3"),
+              "c3r": ("encode_crc_nb<10, 4", "encode_crc_lv<10, 4", "encode_crc_g26<10, 4"), "c4": "encode_crc_g26<2, 1",
+              "c4s": "encode_crc_g26<2, 1", "c5dev": ("encode_crc_nb<6, 3", "encode_crc_lv<6, 3", "encode_crc_g26<6, 3"),
               "crc": "crc_windows_g26s", "verify": "crc_windows_g26s"}
 
 
 def _kernel_match(pat, name):
-    """pat: a name fragment, or a tuple of fragments (the streamed-input or the per-window fused kernel)."""
+    """pat: a name fragment, or a tuple of fragments (the nibble-table, streamed-input or per-window fused kernel)."""
     return any(p in name for p in (pat if isinstance(pat, tuple) else (pat,)))
 
 

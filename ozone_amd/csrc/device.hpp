@@ -307,6 +307,50 @@ __device__ __forceinline__ uint32_t byte_and_v(uint32_t w, uint32_t vmask) {
   return d;
 }
 
+// Lane tree for U registers at once, as reduce-scatter: at level m the lanes whose bit m is set keep the upper
+// half of their register list and the others the lower half, and each kept register is merged with the partner's
+// copy of it (one exchange + one shift per kept register).  After log2(NP) levels (NP = U rounded up to a power of
+// two) every lane holds one register, then the remaining levels merge it as g5_lane_tree does.  Shifts per lane:
+// NP - 1 + (6 - log2 NP) instead of 6 U -- 17 instead of 84 for the 14 registers of rs-10-4.  Returns the merged
+// register of unit `unit` = sum over m < log2 NP of bit m of the lane times NP >> (m + 1) (equal in all lanes that
+// agree on those bits; unit >= U is padding).
+constexpr int tree_np(int U) { return U <= 1 ? 1 : U <= 2 ? 2 : U <= 4 ? 4 : U <= 8 ? 8 : U <= 16 ? 16 : 32; }
+template <int U>
+__device__ __forceinline__ uint32_t g5_lane_tree_rs(const uint32_t *T, const uint32_t (&S)[U], int lane, int &unit) {
+  static_assert(U <= 32, "at most 32 registers");
+  constexpr int NP = tree_np(U);
+  constexpr int L = NP == 1 ? 0 : NP == 2 ? 1 : NP == 4 ? 2 : NP == 8 ? 3 : NP == 16 ? 4 : 5;
+  uint32_t r[NP];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) r[i] = i < U ? S[i] : 0u;
+  unit = 0;
+#pragma unroll
+  for (int m = 0; m < L; ++m) {
+    const int h = (NP >> m) >> 1;
+    const bool upper = (lane >> m) & 1;
+    const uint32_t um = upper ? 0xffffffffu : 0u;  // selects below through a mask register (bitop3), so that the
+                                                  // register list is never turned into a dynamically indexed array
+    unit += upper ? h : 0;
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t send = bsel(r[i], r[h + i], um);  // the half the partner keeps
+      const uint32_t keep = bsel(r[h + i], r[i], um);
+      const uint32_t recv = static_cast<uint32_t>(__shfl_xor(static_cast<int>(send), 1 << m, 64));
+      r[i] = g5_shift(T + kG5Tree + m * 224, bsel(recv, keep, um)) ^ bsel(keep, recv, um);
+    }
+  }
+  uint32_t v = r[0];
+#pragma unroll
+  for (int m = L; m < 6; ++m) {
+    const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), 1 << m, 64));
+    const bool upper = (lane >> m) & 1;
+    v = g5_shift(T + kG5Tree + m * 224, upper ? other : v) ^ (upper ? v : other);
+  }
+  return v;
+}
+
 // XOR of the 26 lookups of block b in the table set at T (26 x 32 words).  VMASK: byte_and_v with vm = 0x7c in
 // a VGPR instead of the SGPR / literal mask.
 template <bool HALVES = false, bool VMASK = false>

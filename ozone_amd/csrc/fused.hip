@@ -295,9 +295,25 @@ constexpr uint32_t nb_region(int d, int j, int i) {
   return static_cast<uint32_t>(((d * K + j) * 16 + i) * 256);
 }
 
+// store (or, reconstructing, check) the finished window CRC of unit q (inputs 0..K-1, then the R outputs)
+template <int K, int R>
+__device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t w, int q, uint32_t v, uint32_t init) {
+  const CrcArgs &cr = e.crc;
+  const int64_t nwin = cr.nwin;
+  if (!e.verify) {
+    cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+  } else if (q >= K) {
+    cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+  } else if (cr.expected) {
+    const int64_t idx = (s * e.exp_units + e.in_unit[q]) * nwin + w;
+    const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
+    if (crc_finish(v, init, 0, 0) != ex) atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
+  }
+}
+
 // K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
-// HALF: lookups of a block in two fenced halves of 8 bytes (at most 16 results live)
-template <int K, int R, int D, int NB, int WPB, int WAVES, bool HALF = true>
+// HALF: lookups of a block in two fenced halves of 8 bytes (at most 16 results live); RS: reduce-scatter lane tree
+template <int K, int R, int D, int NB, int WPB, int WAVES, bool HALF = true, bool RS = true>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -421,30 +437,32 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     }
     const bool last = w == nwin - 1;
     const uint32_t init = last ? cr.init_last : cr.init_full;
+    if constexpr (RS) {
+      int q = 0;
+      const uint32_t v = g5_lane_tree_rs<K + R>(s_t + g26_tree(D) - kG5Tree, S, lane, q);
+      if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
 #pragma unroll
-    for (int q = 0; q < K + R; ++q) {
-      const uint32_t v = g5_lane_tree(s_t + g26_tree(D) - kG5Tree, S[q], lane);
-      if (lane == q) {
-        if (!e.verify) {
-          cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
-        } else if (q >= K) {
-          cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
-        } else if (cr.expected) {
-          const int64_t idx = (s * e.exp_units + e.in_unit[q]) * nwin + w;
-          const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
-          if (crc_finish(v, init, 0, 0) != ex) atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
-        }
+        for (int qq = 0; qq < K + R; ++qq)
+          if (q == qq) nb_emit<K, R>(e, s, w, qq, v, init);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < K + R; ++q) {
+        const uint32_t v = g5_lane_tree(s_t + g26_tree(D) - kG5Tree, S[q], lane);
+        if (lane == q) nb_emit<K, R>(e, s, w, q, v, init);
       }
     }
   }
 }
 
-template <int K, int R, int D, int NB, int WPB, int WAVES, bool HALF = true>
+template <int K, int R, int D, int NB, int WPB, int WAVES, bool HALF = true, bool RS = true>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
-  if constexpr ((D * K) % NB != 0) {
-    return launch_nb<K, R, D, 2, WPB, WAVES, HALF>(e, st);
+  if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
+    constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
+    static_assert(kNB != NB, "fallback ring must differ");
+    return launch_nb<K, R, D, kNB, WPB, WAVES, HALF, RS>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, HALF>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, HALF, RS>;
     // persistent grid: every workgroup builds K*D*4 KiB of tables once, so launch one resident set
     static int resident = 0;  // workgroups per CU x CUs, per instantiation and process (one device type)
     if (resident == 0) {
@@ -476,6 +494,15 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 65: return launch_nb<K, R, 1, 2, 8, 5>(e, st);
     case 66: return launch_nb<K, R, 1, 2, 8, 4, false>(e, st);
     case 67: return launch_nb<K, R, 1, 2, 4, 4>(e, st);
+    case 68: return launch_nb<K, R, kD2, 2, 16, 4>(e, st);
+    case 69: return launch_nb<K, R, kD2, 2, 12, 4>(e, st);
+    case 70: return launch_nb<K, R, 1, 2, 8, 6>(e, st);
+    case 71: return launch_nb<K, R, 1, 2, 8, 8>(e, st);
+    case 72: return launch_nb<K, R, kD2, 2, 16, 8>(e, st);
+    case 73: return launch_nb<K, R, 1, kNB, 8, 5>(e, st);
+    case 74: return launch_nb<K, R, 1, 2, 8, 4, true, false>(e, st);
+    case 75: return launch_nb<K, R, 1, kNB, 8, 4, true, false>(e, st);
+    case 76: return launch_nb<K, R, kD2, 2, 16, 4, true, false>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);
@@ -493,7 +520,11 @@ bool encode_crc_lv_supported(const EncCrcArgs &e) {
 
 hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   const int k = e.code.k, r = e.code.rows;
-  if (v >= 60 && v < 70) {
+  // default: the nibble-table kernel (same-process A/Bs on MI355X, profiles/r02/nb/): rs-10-x with a ring of 5
+  // input blocks and one-step groups (62: C3r 56.1 % vs 52.5 % for encode_crc_lv), rs-6-x / rs-3-x with two-step
+  // groups in 16-wave workgroups (68: C5dev 59.2 % vs 57.9 %); 56 / 59 pin the streamed-input kernel's defaults
+  if (v == 0) v = k == 10 ? 62 : 68;
+  if (v >= 60 && v < 80) {
     if (k == 6 && r == 3) return launch_nb_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_nb_kr<6, 2>(e, st, v);
     if (k == 3 && r == 2) return launch_nb_kr<3, 2>(e, st, v);

@@ -312,17 +312,23 @@ __device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t 
 }
 
 // K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
-// HALF: lookups of a block in two fenced halves of 8 bytes (at most 16 results live); RS: reduce-scatter lane tree
-template <int K, int R, int D, int NB, int WPB, int WAVES, bool HALF = true, bool RS = true>
+// FENCE: dwords of a block whose lookups go between scheduling fences (2: halves, at most 16 results live; 1:
+// quarters; 4: none); RS: reduce-scatter lane tree
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
   static_assert(D <= kNibSets, "distance sets of the nibble blob");
   static_assert((D * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
-  static_assert(K * D * 4096 + g26_words(D) * 4 <= 65536, "LDS offsets must fit the ds_read offset field");
-  __shared__ __attribute__((aligned(256))) uint2 s_c[K * D * 512];  // (d, j, p) tables, 16 entries each
-  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(D)];
-  __shared__ uint32_t s_gf[K * 32];  // GF dword of (j, nibble half h, n)
+  // one LDS block: G26 blob, then the (d, j, p) nibble tables, then the GF dwords of the setup.  Table regions
+  // past the 16-bit ds_read offset range are reached with bit 15 set in the index register (one v_or_b32)
+  constexpr uint32_t kTB = (g26_words(D) * 4 + 255) / 256 * 256;  // byte offset of the nibble tables
+  constexpr uint32_t kLds = kTB + K * D * 4096 + K * 32 * 4;
+  static_assert(kLds <= 160 * 1024, "LDS per workgroup");
+  __shared__ __attribute__((aligned(256))) uint8_t s_all[kLds];
+  uint32_t *const s_t = reinterpret_cast<uint32_t *>(s_all);
+  uint2 *const s_c = reinterpret_cast<uint2 *>(s_all + kTB);
+  uint32_t *const s_gf = reinterpret_cast<uint32_t *>(s_all + kTB + K * D * 4096);
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
   for (int t = threadIdx.x; t < K * 32; t += blockDim.x) {
@@ -392,12 +398,19 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
           ch.push(S[j]);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            if (HALF && c == 2) __builtin_amdgcn_sched_barrier(0);
+            if (c > 0 && c % FENCE == 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int i = 4 * c + q;
-              const uint2 lo = lds64(s_c, nb_region<K>(d, j, i) + nib_lo_idx(xw[c], q, v4));
-              const uint2 hi = lds64(s_c, nb_region<K>(d, j, i) + 8 + nib_hi_idx(xw[c], q, vf0));
+              const uint32_t reg = kTB + nb_region<K>(d, j, i);
+              uint2 lo, hi;
+              if (reg + 256 <= 65536) {
+                lo = lds64(s_all, reg + nib_lo_idx(xw[c], q, v4));
+                hi = lds64(s_all, reg + 8 + nib_hi_idx(xw[c], q, vf0));
+              } else {
+                lo = lds64(s_all, (reg - 0x8000u) + (nib_lo_idx(xw[c], q, v4) | 0x8000u));
+                hi = lds64(s_all, (reg + 8 - 0x8000u) + (nib_hi_idx(xw[c], q, vf0) | 0x8000u));
+              }
               A[i] = j == 0 ? (lo.x ^ hi.x) : xor3(A[i], lo.x, hi.x);
               ch.push(lo.y);
               ch.push(hi.y);
@@ -455,14 +468,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   }
 }
 
-template <int K, int R, int D, int NB, int WPB, int WAVES, bool HALF = true, bool RS = true>
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
     static_assert(kNB != NB, "fallback ring must differ");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, HALF, RS>(e, st);
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, HALF, RS>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS>;
     // persistent grid: every workgroup builds K*D*4 KiB of tables once, so launch one resident set
     static int resident = 0;  // workgroups per CU x CUs, per instantiation and process (one device type)
     if (resident == 0) {
@@ -492,7 +505,7 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 63: return launch_nb<K, R, kD2, 2, 8, 4>(e, st);
     case 64: return launch_nb<K, R, kD2, kNB, 8, 4>(e, st);
     case 65: return launch_nb<K, R, 1, 2, 8, 5>(e, st);
-    case 66: return launch_nb<K, R, 1, 2, 8, 4, false>(e, st);
+    case 66: return launch_nb<K, R, 1, 2, 8, 4, 4>(e, st);
     case 67: return launch_nb<K, R, 1, 2, 4, 4>(e, st);
     case 68: return launch_nb<K, R, kD2, 2, 16, 4>(e, st);
     case 69: return launch_nb<K, R, kD2, 2, 12, 4>(e, st);
@@ -500,9 +513,25 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 71: return launch_nb<K, R, 1, 2, 8, 8>(e, st);
     case 72: return launch_nb<K, R, kD2, 2, 16, 8>(e, st);
     case 73: return launch_nb<K, R, 1, kNB, 8, 5>(e, st);
-    case 74: return launch_nb<K, R, 1, 2, 8, 4, true, false>(e, st);
-    case 75: return launch_nb<K, R, 1, kNB, 8, 4, true, false>(e, st);
-    case 76: return launch_nb<K, R, kD2, 2, 16, 4, true, false>(e, st);
+    case 74: return launch_nb<K, R, 1, 2, 8, 4, 2, false>(e, st);
+    case 75: return launch_nb<K, R, 1, kNB, 8, 4, 2, false>(e, st);
+    case 76: return launch_nb<K, R, kD2, 2, 16, 4, 2, false>(e, st);
+    // two-step groups for every K (tables past the 64 KiB offset range), four-step groups where they fit
+    case 77: return launch_nb<K, R, 2, kNB, 16, 4>(e, st);
+    case 78: return launch_nb<K, R, 2, 2, 16, 4>(e, st);
+    case 79: return launch_nb<K, R, K <= 6 ? 4 : 2, 2, 16, 4>(e, st);
+    // lookups fenced per dword (8 results live) for occupancy
+    case 80: return launch_nb<K, R, 1, kNB, 8, 4, 1>(e, st);
+    case 81: return launch_nb<K, R, 1, kNB, 8, 6, 1>(e, st);
+    case 82: return launch_nb<K, R, kD2, 2, 16, 4, 1>(e, st);
+    case 83: return launch_nb<K, R, kD2, 2, 16, 8, 1>(e, st);
+    case 84: return launch_nb<K, R, 1, 2, 8, 6, 1>(e, st);
+    // workgroup sizes that fill the VGPR-limited wave slots (occupancy is per workgroup)
+    case 85: return launch_nb<K, R, 1, kNB, 10, 4>(e, st);
+    case 86: return launch_nb<K, R, kD2, 2, 14, 4>(e, st);
+    case 87: return launch_nb<K, R, kD2, 2, 12, 4>(e, st);
+    case 88: return launch_nb<K, R, 1, kNB, 10, 5>(e, st);
+    case 89: return launch_nb<K, R, 1, kNB, 12, 4>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);
@@ -524,7 +553,7 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // input blocks and one-step groups (62: C3r 56.1 % vs 52.5 % for encode_crc_lv), rs-6-x / rs-3-x with two-step
   // groups in 16-wave workgroups (68: C5dev 59.2 % vs 57.9 %); 56 / 59 pin the streamed-input kernel's defaults
   if (v == 0) v = k == 10 ? 62 : 68;
-  if (v >= 60 && v < 80) {
+  if (v >= 60 && v < 90) {
     if (k == 6 && r == 3) return launch_nb_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_nb_kr<6, 2>(e, st, v);
     if (k == 3 && r == 2) return launch_nb_kr<3, 2>(e, st, v);

@@ -361,7 +361,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
   for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
   const uint32_t in_extent = static_cast<uint32_t>(off_max + cr.bpc);
-  for (int64_t u = static_cast<int64_t>(blockIdx.x) * WPB + wave; u < units; u += static_cast<int64_t>(gridDim.x) * WPB) {
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  for (int64_t u = bid * WPB + wave; u < units; u += static_cast<int64_t>(gridDim.x) * WPB) {
     // wave-uniform by construction; said explicitly so the descriptors below stay in SGPRs (the 64-bit division
     // runs in the VALU, and without this the buffer accesses were wrapped in waterfall loops)
     const int64_t s = uniform64(u / nwin);
@@ -476,19 +477,12 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
     return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS>(e, st);
   } else {
     auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS>;
-    // persistent grid: every workgroup builds K*D*4 KiB of tables once, so launch one resident set
-    static int resident = 0;  // workgroups per CU x CUs, per instantiation and process (one device type)
-    if (resident == 0) {
-      int dev = 0, cus = 0, per_cu = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WPB * 64, 0) != hipSuccess)
-        return hipErrorInvalidValue;
-      resident = std::max(1, cus * std::max(1, per_cu));
-    }
+    // one wave per (stripe, window) unit, no grid-stride: every workgroup builds its K*D*4 KiB of tables, and the
+    // dispatcher's refill of finished workgroups balances the CUs.  Measured on MI355X against a persistent grid
+    // of one resident set (profiles/r02/nb/ab_grid_*.log): C3r 56.2 % -> 63.5 %, C5dev 60.1 % -> 65.7 %.
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
-    const int64_t g = std::min<int64_t>(g_tune.crc_grid > 0 ? g_tune.crc_grid : resident, blocks);
+    const int64_t g = std::min<int64_t>(g_tune.crc_grid > 0 ? g_tune.crc_grid : blocks, blocks);
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, e);
     return hipGetLastError();
   }
@@ -549,10 +543,11 @@ bool encode_crc_lv_supported(const EncCrcArgs &e) {
 
 hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   const int k = e.code.k, r = e.code.rows;
-  // default: the nibble-table kernel (same-process A/Bs on MI355X, profiles/r02/nb/): rs-10-x with a ring of 5
-  // input blocks and one-step groups (62: C3r 56.1 % vs 52.5 % for encode_crc_lv), rs-6-x / rs-3-x with two-step
-  // groups in 16-wave workgroups (68: C5dev 59.2 % vs 57.9 %); 56 / 59 pin the streamed-input kernel's defaults
-  if (v == 0) v = k == 10 ? 62 : 68;
+  // default: the nibble-table kernel, one wave per window (same-process A/Bs on MI355X, profiles/r02/nb/): rs-10-x
+  // with a ring of 5 input blocks and one-step groups (62: C3r 62.9 %; encode_crc_lv 52.5 %), rs-6-x / rs-3-x with
+  // two-step groups in 12-wave workgroups (87: C5dev 66.9 %; encode_crc_lv 57.9 %); 56 / 59 pin the streamed-input
+  // kernel's defaults
+  if (v == 0) v = k == 10 ? 62 : 87;
   if (v >= 60 && v < 90) {
     if (k == 6 && r == 3) return launch_nb_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_nb_kr<6, 2>(e, st, v);

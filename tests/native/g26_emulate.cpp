@@ -41,7 +41,7 @@ int main() {
   int checked = 0;
   for (int ty = 0; ty < 2; ++ty) {
     const CrcMath &cm = CrcMath::get(static_cast<CrcType>(ty));
-    for (int slot = 0; slot < 5; ++slot) {
+    for (int slot = 0; slot < kG26Slots; ++slot) {
       const int B = kG26Cfg[slot][0], D = kG26Cfg[slot][1], E = B * D;
       const std::vector<uint32_t> &T = cm.g26_tables(slot);
       if (static_cast<int>(T.size()) != g26_words(E)) {
@@ -80,6 +80,34 @@ int main() {
       }
     }
   }
-  printf("g26 emulation: %d windows bit-exact\n", checked);
+  // nibble tables of the nibble-table fused kernel (fused.hip encode_crc_nb): the XOR over a block's 32 nibbles of
+  // nib[e][p][nibble] must be the block's raw CRC advanced by e KiB
+  int nib_checked = 0;
+  for (int ty = 0; ty < 2; ++ty) {
+    const CrcMath &cm = CrcMath::get(static_cast<CrcType>(ty));
+    const std::vector<uint32_t> &N = cm.nib_tables();
+    if (static_cast<int>(N.size()) != kNibWords) {
+      printf("nibble blob size mismatch\n");
+      return 1;
+    }
+    for (int e = 0; e < kNibSets; ++e)
+      for (int it = 0; it < 2000; ++it) {
+        uint8_t b[16];
+        for (auto &x : b) x = static_cast<uint8_t>(rand());
+        if (it == 0) memset(b, 0, 16);
+        if (it == 1) memset(b, 0xff, 16);
+        uint32_t reg = 0;
+        for (uint8_t x : b) reg = (reg >> 8) ^ cm.byte_table((reg ^ x) & 0xff);
+        const uint32_t ref = cm.shift(reg, static_cast<uint64_t>(e) * 1024);
+        uint32_t got = 0;
+        for (int p = 0; p < 32; ++p) got ^= N[(e * 32 + p) * 16 + ((b[p >> 1] >> (4 * (p & 1))) & 15)];
+        if (got != ref) {
+          printf("FAIL nibble tables crc type %d set %d: %08x vs %08x\n", ty, e, got, ref);
+          return 1;
+        }
+        ++nib_checked;
+      }
+  }
+  printf("g26 emulation: %d windows bit-exact; nibble tables: %d blocks bit-exact\n", checked, nib_checked);
   return 0;
 }

@@ -34,7 +34,7 @@ for v in vals:
         ref = got
     ok = all(torch.equal(a, b) for a, b in zip(ref, got))
     print(json.dumps({"variant": v, "bit_exact_vs_first": ok}), flush=True)
-    if not ok:
+    if not ok and not os.environ.get("NOCHECK"):  # NOCHECK: timing probes that compute wrong results on purpose
         sys.exit(2)
 times = {v: [] for v in vals}
 for _ in range(rounds):

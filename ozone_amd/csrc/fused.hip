@@ -313,7 +313,7 @@ __device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t 
 
 // K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
 // FENCE: dwords of a block whose lookups go between scheduling fences (2: halves, at most 16 results live; 1:
-// quarters; 4: none); RS: reduce-scatter lane tree
+// quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
           ch.push(S[j]);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            if (c > 0 && c % FENCE == 0) __builtin_amdgcn_sched_barrier(0);
+            if (FENCE > 0 && c > 0 && c % (FENCE > 0 ? FENCE : 1) == 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int i = 4 * c + q;
@@ -418,7 +418,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             }
           }
           S[j] = ch.get();
-          __builtin_amdgcn_sched_barrier(0);
+          if (FENCE > 0) __builtin_amdgcn_sched_barrier(0);
         }
         // 4x4 byte transposes: A[4c + q] byte r -> output r, dword c, byte q
         uint32_t o[4][4];
@@ -526,6 +526,9 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 87: return launch_nb<K, R, kD2, 2, 12, 4>(e, st);
     case 88: return launch_nb<K, R, 1, kNB, 10, 5>(e, st);
     case 89: return launch_nb<K, R, 1, kNB, 12, 4>(e, st);
+    case 93: return launch_nb<K, R, K == 10 ? 1 : kD2, K == 10 ? kNB : 2, K == 10 ? 8 : 12, 4, 0>(e, st);
+    case 94: return launch_nb<K, R, K == 10 ? 1 : kD2, K == 10 ? kNB : 2, K == 10 ? 8 : 12, 4, 4>(e, st);
+    case 95: return launch_nb<K, R, K == 10 ? 1 : kD2, 2, K == 10 ? 8 : 12, 4, 0>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);
@@ -548,7 +551,7 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // two-step groups in 12-wave workgroups (87: C5dev 66.9 %; encode_crc_lv 57.9 %); 56 / 59 pin the streamed-input
   // kernel's defaults
   if (v == 0) v = k == 10 ? 62 : 87;
-  if (v >= 60 && v < 90) {
+  if (v >= 60 && v < 100) {
     if (k == 6 && r == 3) return launch_nb_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_nb_kr<6, 2>(e, st, v);
     if (k == 3 && r == 2) return launch_nb_kr<3, 2>(e, st, v);

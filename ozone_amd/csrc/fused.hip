@@ -1,4 +1,5 @@
-// Fused encode (or reconstruct) + CRC for full windows, built for occupancy: "streamed inputs".
+// Fused encode (or reconstruct) + CRC for full windows: encode_crc_nb (nibble tables, the default, further below) and
+// encode_crc_lv ("streamed inputs", variants 50-59), described here first.
 //
 // The per-window fused kernel in kernels.hip (encode_crc_g26) loads all K input blocks of a step at once and
 // keeps every input, every parity accumulator and the coefficient tables of the step live together: 123 VGPRs

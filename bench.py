@@ -85,19 +85,26 @@ def _free_port():
     return port
 
 
+def worker_specs(n, argv, environ, port):
+    """(argv, env, keep_stdout) of each of the n rank processes launch_workers starts: the same command line, the
+    torchrun variables of rank r (RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = n, rendezvous on
+    127.0.0.1:port), and only rank 0's stdout kept (it prints the one JSON line)."""
+    specs = []
+    for r in range(n):
+        env = dict(environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        specs.append(([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env, r == 0))
+    return specs
+
+
 def launch_workers(args):
     """--gpus N without torchrun: start N rank processes (this process never touches a GPU) and wait."""
     same = os.environ.get("OZEC_BENCH_SAME_DEVICE") == "1"
     ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
     if not same and ndev < args.gpus:
         raise SystemExit(f"--gpus {args.gpus}: only {ndev} visible GPU(s)")
-    port = _free_port()
-    procs = []
-    for r in range(args.gpus):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    procs = [subprocess.Popen(cmd, env=env, stdout=None if keep else subprocess.DEVNULL)
+             for cmd, env, keep in worker_specs(args.gpus, sys.argv[1:], os.environ, _free_port())]
     rc = 0
     for p in procs:
         rc = max(rc, p.wait())
@@ -583,6 +590,10 @@ def e2e_leg(args, rank, world, dist, dev, backend):
                "numa": {"gpu_node": None, "data_page_nodes": hb.placement()}}
         from ozone_amd.stripe_queue import device_numa_node
         res["numa"]["gpu_node"] = device_numa_node(dev)
+        res["per_rank"] = gather_per_rank({"elapsed_s": round(el, 4), "stripes": mine,
+                                           "GBps": round(mine * k * n * args.e2e_steps / el / 1e9, 2),
+                                           "register_s": round(hb.register_s, 3), "gpu_node": res["numa"]["gpu_node"],
+                                           "data_page_nodes": res["numa"]["data_page_nodes"]}, dist)
         if dist is not None:
             allr = [None] * world
             dist.all_gather_object(allr, {"mine": mine, "numa": res["numa"], "ok": ok})
@@ -709,8 +720,11 @@ def pmc_traffic(args, alg_bytes):
     prof = shutil.which("rocprofv3")
     if not pat or not prof:
         return None, {"error": "no kernel pattern / rocprofv3 for this workload"}
-    base = [sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--steps", "3", "--warmup", "1",
-            "--no-cpu", "--no-e2e", "--no-pmc"] + (["--stripes", str(args.stripes)] if args.stripes else [])
+    # the child runs exactly the main run's warm-up and timed steps, so the rocprof durations of the timed dispatches
+    # are taken at the same clock state as the HIP events (a 3-step child ran 11-20 % slow)
+    base = [sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--steps", str(args.steps),
+            "--warmup", str(args.warmup), "--no-cpu", "--no-e2e", "--no-pmc"] + \
+        (["--stripes", str(args.stripes)] if args.stripes else [])
     for kv in args.tune:
         base += ["--tune", kv]
     out = {}
@@ -731,8 +745,20 @@ def pmc_traffic(args, alg_bytes):
                 st = [f for f in files if f.endswith("kernel_stats.csv")]
                 rows = [row for row in csv.DictReader(open(st[0])) if _kernel_match(pat, row["Name"])]
                 out["rocprof_kernel"] = rows[0]["Name"]
-                out["rocprof_avg_ms"] = round(float(rows[0]["AverageNs"]) / 1e6, 4)
                 out["rocprof_calls"] = int(rows[0]["Calls"])
+                out["rocprof_avg_all_calls_ms"] = round(float(rows[0]["AverageNs"]) / 1e6, 4)
+                out["rocprof_min_ms"] = round(float(rows[0]["MinNs"]) / 1e6, 4)
+                # the timed dispatches: the last `steps` of the kernel in the trace (the warm-up's come first)
+                tr = [f for f in files if f.endswith("kernel_trace.csv")]
+                disp = [row for row in csv.DictReader(open(tr[0])) if _kernel_match(pat, row["Kernel_Name"])]
+                disp.sort(key=lambda row: int(row["Start_Timestamp"]))
+                timed = disp[-args.steps:]
+                dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
+                out["rocprof_avg_ms"] = round(float(np.mean(dur)), 4)
+                out["rocprof_timed_dispatches"] = len(dur)
+                out["kernel_vgpr"] = int(timed[-1].get("VGPR_Count") or 0)
+                out["kernel_lds_bytes"] = int(timed[-1].get("LDS_Block_Size") or 0)
+                out["kernel_scratch_bytes"] = int(timed[-1].get("Scratch_Size") or 0)
             else:
                 cc = [f for f in files if f.endswith("counter_collection.csv")]
                 vals = [float(row["Counter_Value"]) for row in csv.DictReader(open(cc[0]))
@@ -798,7 +824,53 @@ def stream_latency(args):
         if cross is None and g < c:
             cross = nb
     rows["crc_update_gpu_wins_from_bytes"] = cross
-    rows["cpu"] = f"1 thread, oracle/cpu_baseline.c percall_*, {flags}"
+    # Checksum.computeChecksum of one host buffer (Checksum.java:157-179) through ozec_checksum_windows, the batch
+    # entry the Java hook would call: CRC32C per 16 KiB window, from 1 and from T threads (each its own buffer),
+    # beside the CPU doing the same per-window CRC32C (SSE4.2, what the JDK's CRC32C intrinsic does)
+    T = usable_cpus()
+    bpc = 16384
+    cross = {}
+    for nb in (16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+        for th in (1, T):
+            bufs = [rng.integers(0, 256, nb, dtype=np.uint8) for _ in range(th)]
+            outs = [np.empty(nb // bpc, np.uint32) for _ in range(th)]
+
+            def one(i):
+                rc_ = L.ozec_checksum_windows(3, bufs[i].ctypes.data, nb, bpc, outs[i].ctypes.data, 0)
+                assert rc_ == 0
+
+            one(0)
+            counts = [0] * th
+            t_end = time.perf_counter() + 0.3
+
+            def loop(i):
+                while time.perf_counter() < t_end:
+                    one(i)
+                    counts[i] += 1
+
+            t0 = time.perf_counter()
+            if th == 1:
+                loop(0)
+            else:
+                ts = [threading.Thread(target=loop, args=(i,)) for i in range(th)]
+                for x in ts:
+                    x.start()
+                for x in ts:
+                    x.join()
+            el = time.perf_counter() - t0
+            calls = sum(counts)
+            out = subprocess.run([exe, "percall_windows", str(nb), "0.3", str(th)], capture_output=True, text=True,
+                                 timeout=60)
+            c = json.loads(out.stdout)
+            g_gbps = calls * nb / el / 1e9
+            rows[f"checksum_windows_{nb >> 10}KiB_{th}thr"] = {
+                "gpu_us": round(el / (calls / th) * 1e6, 1), "gpu_GBps": round(g_gbps, 2),
+                "cpu_us": round(c["us_per_call"], 1), "cpu_GBps": round(c["GBps"], 2)}
+            if g_gbps > c["GBps"] and th not in cross:
+                cross[th] = nb
+    rows["checksum_windows_gpu_wins_from_bytes"] = {f"{th}thr": cross.get(th) for th in (1, T)}
+    rows["cpu"] = (f"oracle/cpu_baseline.c percall_* (1 thread; checksum_windows rows: per-window CRC32C on 1 / {T} "
+                   f"threads, each its own buffer), {flags}")
     return rows
 
 
@@ -816,6 +888,16 @@ def _quiet_stdout():
         sys.stdout.flush()
         _JSON_FD = os.dup(1)
         os.dup2(2, 1)
+
+
+def gather_per_rank(rec, dist):
+    """{key: [value of rank 0, 1, ...]} of one record per rank (the max-over-ranks figures hide which rank, NUMA node
+    or link is the straggler of an N-GPU run)."""
+    recs = [rec]
+    if dist is not None:
+        recs = [None] * dist.get_world_size()
+        dist.all_gather_object(recs, rec)
+    return {k: [r[k] for r in recs] for k in rec}
 
 
 def emit(obj):
@@ -914,6 +996,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    per_rank = gather_per_rank({"elapsed_s": round(elapsed, 5), "kernel_ms": round(kern_ms, 4), "numa_node": numa_node,
+                                "device": dev_id, "cpus": len(os.sched_getaffinity(0))}, dist)
     elapsed = max_over_ranks(elapsed, dist, device=red_dev)
     kern_ms = max_over_ranks(kern_ms, dist, device=red_dev)
     value = wl.data_bytes * world * args.steps / elapsed / 1e9
@@ -939,6 +1023,7 @@ def main():
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
                      "kernel": wl.kernel, "kernel_ms": round(kern_ms, 4), "kernel_ms_reduction": "max over ranks",
                      "alg_bytes_per_launch": wl.alg_bytes, "numa_node": numa_node},
+        "per_rank": per_rank,
     }
     if args.workload in ("host", "queue", "queue_pageable", "c3r_host"):
         pc = pcie_ceiling(64 * 10 * MIB, 64 * 4 * MIB) if args.workload == "c3r_host" else \
@@ -960,6 +1045,16 @@ def main():
             traffic, detail = pmc_traffic(args, result["roofline"]["alg_bytes_per_launch"])
             result["roofline"]["traffic"] = traffic
             result["roofline"]["pmc"] = detail
+            if "rocprof_avg_ms" in detail:
+                rf = result["roofline"]
+                alg = rf["alg_bytes_per_launch"]
+                rf["rocprof_avg_ms"] = detail["rocprof_avg_ms"]
+                rf["rocprof_min_ms"] = detail["rocprof_min_ms"]
+                rf["frac_rocprof_avg"] = round(alg / (detail["rocprof_avg_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+                rf["rocprof_avg_over_events"] = round(detail["rocprof_avg_ms"] / rf["kernel_ms"], 4)
+                rf["clocks"] = ("kernel_ms: HIP events around each timed step on the launch stream (mean of the timed "
+                                "steps); rocprof_avg_ms: rocprofv3 durations of the same kernel's timed dispatches in a "
+                                "child run with the same warm-up and steps; frac uses kernel_ms")
         if not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
             if "e2e" in result and "value" in result["e2e"]:

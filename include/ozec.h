@@ -62,6 +62,10 @@ int ozec_device_count(void);
 int ozec_set_device(int device);
 /* wait for all work queued on the calling thread's current device (host-buffer calls are already synchronous) */
 int ozec_synchronize(void);
+/* give back the host-batch pipeline's chunk buffers (4 device + 4 pinned buffers of one chunk each: about 1.1 GiB
+ * of HBM and, for pageable callers, of pinned memory with rs-6-3 1 MiB cells and 32-stripe chunks) and the staging
+ * buffers of the idle host-call slots of the current device; the next call allocates again */
+int ozec_release_staging(void);
 
 /* ---- coder lifecycle: RawErasureCoderFactory.createEncoder/createDecoder
  *      (EC/rawcoder/RawErasureCoderFactory.java:29-56), RSRawEncoder/RSRawDecoder ctors
@@ -71,8 +75,14 @@ int ozec_encoder_create(int codec, int num_data, int num_parity, ozec_coder **ou
 int ozec_decoder_create(int codec, int num_data, int num_parity, ozec_coder **out);
 /* RawErasureEncoder.release / RawErasureDecoder.release: idempotent; later calls return OZEC_ECLOSED */
 int ozec_coder_release(ozec_coder *coder);
-/* free the handle itself (the Java object's cleaner / Python __del__) */
+/* drop the caller's ownership of the handle (the Java object's cleaner / Python __del__); the memory goes with
+ * the last owner: a stripe queue created on an encoder owns it too until ozec_stripe_queue_free, so releasing and
+ * freeing the encoder first leaves the queue's calls failing with OZEC_ECLOSED, never touching freed memory */
 void ozec_coder_free(ozec_coder *coder);
+/* one more owner of the handle, to be dropped with one more ozec_coder_free */
+int ozec_coder_retain(ozec_coder *coder);
+/* 1 after ozec_coder_release, else 0 */
+int ozec_coder_is_closed(const ozec_coder *coder);
 int ozec_coder_info(const ozec_coder *coder, int *codec, int *num_data, int *num_parity, int *is_decoder);
 
 /* ---- encode: RawErasureEncoder.doEncode -> RSUtil.encodeData (EC/rawcoder/util/RSUtil.java:87-133),
@@ -237,8 +247,11 @@ int ozec_device_numa_node(int device, int *node);
 /* NUMA node holding the (touched) page at p, -1 if unknown -- placement diagnostics */
 int ozec_host_page_node(const void *p, int *node);
 /* pin caller-owned memory for DMA (e.g. one rank's stripe range of a batch shared between processes), placing
- * its pages on `device`'s NUMA node first (device < 0: no placement); ozec_host_unregister undoes the pinning */
+ * its pages on `device`'s NUMA node first (device < 0: no placement; only pages wholly inside the range move).
+ * Placement is best effort: where the kernel refuses it the memory is pinned where it lies, and
+ * ozec_host_placement_failures() counts such calls.  ozec_host_unregister undoes the pinning */
 int ozec_host_register(void *p, size_t bytes, int device);
+uint64_t ozec_host_placement_failures(void);
 int ozec_host_unregister(void *p);
 typedef struct ozec_stripe_queue ozec_stripe_queue;
 /* checksum_type OZEC_CHECKSUM_NONE: parity only; CRC32 / CRC32C: also the bpc-window CRCs of all k+p units,
@@ -253,6 +266,10 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
 int ozec_stripe_queue_flush(ozec_stripe_queue *q);
 /* block until every stripe up to and including `ticket` has its parity (and CRCs) in the caller's buffers */
 int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket);
+/* the queue's shape: data / parity units, coded parity rows (XOR: 1), cell length, checksum type and bpc (any may
+ * be NULL) -- what a binding checks a submit's buffers against */
+int ozec_stripe_queue_info(const ozec_stripe_queue *q, int *num_data, int *num_parity, int *rows, size_t *cell_len,
+                           int *checksum_type, size_t *bytes_per_checksum);
 /* introspection: batches in flight, first ticket of the oldest one (UINT64_MAX if none), stripes in filling batches */
 int ozec_stripe_queue_state(ozec_stripe_queue *q, size_t *in_flight, uint64_t *oldest_in_flight_ticket,
                             size_t *filling);
@@ -301,7 +318,7 @@ int ozec_crc_compose_windows_batch(int checksum_type, const uint32_t *d_crcs, in
 #define OZEC_OP_ENCODE_DEVICE 2   /* ozec_encode_device / ozec_encode_batch                                 */
 #define OZEC_OP_DECODE_DEVICE 3   /* ozec_decode_device / ozec_decode_batch                                 */
 #define OZEC_OP_FUSED 4           /* ozec_encode_crc_batch / _block_groups / ozec_reconstruct_crc_batch      */
-#define OZEC_OP_HOST_BATCH 5      /* ozec_encode_crc_host_batch                                             */
+#define OZEC_OP_HOST_BATCH 5      /* ozec_encode_crc_host_batch / ozec_reconstruct_crc_host_batch           */
 #define OZEC_OP_CHECKSUM 6        /* ozec_checksum_windows / _verify / ozec_crc_update (host buffers)       */
 #define OZEC_OP_CHECKSUM_DEVICE 7 /* ozec_checksum_windows_batch / _device / ozec_checksum_verify_batch     */
 #define OZEC_OP_QUEUE 8           /* ozec_stripe_queue_submit / _flush / _wait                              */

@@ -10,7 +10,9 @@ import java.util.ArrayDeque;
  * with this queue the writer hands a full stripe over and keeps filling the next one, and the GPU encodes
  * stripesPerBatch stripes (+ their window CRCs) per fused launch with the copies of three batches overlapped.
  * Cells and CRC buffers must be direct buffers; the ones from {@link OzecNative#allocatePinned} are DMA'd without
- * staging.  Buffers stay referenced (and must stay unmodified) until waitFor returns for their ticket.
+ * staging.  Buffers stay referenced (and must stay unmodified) until waitFor returns for their ticket.  The native
+ * queue co-owns the encoder's native handle (ozec_coder_retain), so releasing the encoder first only makes later
+ * submits fail with "closed"; the handle's memory goes with close().
  */
 public final class HipStripeQueue implements AutoCloseable {
   private final int numData;
@@ -50,7 +52,8 @@ public final class HipStripeQueue implements AutoCloseable {
     for (int i = 0; i < numParity; i++) {
       parityOffsets[i] = parityCells[i].position();
     }
-    long ticket = OzecNative.queueSubmit(queue, dataCells, dataOffsets, parityCells, parityOffsets, length, crcs);
+    long ticket = OzecNative.queueSubmit(queue, dataCells, dataOffsets, parityCells, parityOffsets, length, crcs,
+        crcs == null ? 0 : crcs.position());
     held.addLast(new Object[] {ticket, dataCells, parityCells, crcs});
     return ticket;
   }

@@ -1,5 +1,6 @@
 package org.apache.ozone.erasurecode.rawcoder;
 
+import java.io.IOException;
 import java.nio.ByteBuffer;
 
 /**
@@ -91,7 +92,7 @@ public final class OzecNative {
       int bytesPerChecksum);
 
   static native long queueSubmit(long queue, ByteBuffer[] data, int[] dataOffsets, ByteBuffer[] parity,
-      int[] parityOffsets, int length, ByteBuffer crcs);
+      int[] parityOffsets, int length, ByteBuffer crcs, int crcsOffset);
 
   static native void queueWait(long queue, long ticket);
 
@@ -101,4 +102,28 @@ public final class OzecNative {
   static native void reconstructHostBatch(long decoder, ByteBuffer stripes, long stripeStride, long unitStride,
       int[] presentUnits, int[] erasedIndexes, ByteBuffer out, int numStripes, int cellLength, int checksumType,
       int bytesPerChecksum, ByteBuffer expectedChecksums, ByteBuffer outChecksums, ByteBuffer mismatch);
+
+  // ---- COMPOSITE_CRC (ozec_crc_monomial / ozec_crc_compose / ozec_crc_composer_* / ozec_crc_compose_windows_batch;
+  //      CrcUtil.java:74-127, CrcComposer.java:44-215 under hadoop-ozone/common/.../ozone/client/checksum/)
+  public static native int crcMonomial(int type, long lengthBytes);
+
+  public static native int crcCompose(int type, int crcA, int crcB, long lengthB);
+
+  public static native long composerCreate(int type, long bytesPerCrcHint, long stripeLength) throws IOException;
+
+  public static native void composerUpdate(long composer, int crc, long bytesPerCrc) throws IOException;
+
+  public static native void composerUpdateBytes(long composer, byte[] crcBuffer, int offset, int length,
+      long bytesPerCrc) throws IOException;
+
+  public static native int composerPending(long composer);
+
+  public static native int composerDigest(long composer, byte[] out);
+
+  public static native void composerFree(long composer);
+
+  /** Device pointers and stream as longs: for callers that keep the window CRCs in HBM. */
+  public static native void composeWindowsBatch(int type, long deviceCrcs, long crcCellStride, long numCells,
+      long numWindows, long bytesPerCrc, long lastLength, boolean crcsBigEndian, long deviceOut,
+      boolean outBigEndian, long stream);
 }

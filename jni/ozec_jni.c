@@ -355,30 +355,35 @@ JNIEXPORT jlong JNICALL JNI_FN(queueCreate)(JNIEnv *env, jclass cls, jlong enc, 
 }
 
 /* submit(data cells, parity cells, len, crcs): direct buffers at their positions; returns the stripe's ticket.
- * The Java side keeps the buffers referenced until waitFor(ticket) returns (HipStripeQueue). */
+ * The Java side keeps the buffers referenced until waitFor(ticket) returns (HipStripeQueue).  Cell counts, lengths
+ * and the CRC buffer's room from crcsOffset are checked against the queue by ozm_queue_submit. */
 JNIEXPORT jlong JNICALL JNI_FN(queueSubmit)(JNIEnv *env, jclass cls, jlong q, jobjectArray data, jintArray dataOff,
-                                            jobjectArray parity, jintArray parityOff, jint len, jobject crcs) {
+                                            jobjectArray parity, jintArray parityOff, jint len, jobject crcs,
+                                            jint crcsOffset) {
   (void)cls;
-  ozm_buf db[MAX_BUFS], pb[MAX_BUFS];
-  const uint8_t *dp[MAX_BUFS], *pp[MAX_BUFS];
+  ozm_buf db[MAX_BUFS], pb[MAX_BUFS], cb = {0};
   int nd = 0, np = 0;
   ozm_status st;
   uint64_t ticket = 0;
-  if (collect_direct(env, data, dataOff, db, &nd, &st) || collect_direct(env, parity, parityOff, pb, &np, &st) ||
-      ozm_resolve(db, nd, 0, len, dp, &st) || ozm_resolve(pb, np, 0, len, pp, &st)) {
+  if (collect_direct(env, data, dataOff, db, &nd, &st) || collect_direct(env, parity, parityOff, pb, &np, &st)) {
     throw_status(env, &st);
     return 0;
   }
-  uint32_t *cp = crcs ? (uint32_t *)(*env)->GetDirectBufferAddress(env, crcs) : NULL;
-  if (crcs && !cp) {
-    ozm_fail(OZEC_EINVAL, "crcs must be a direct buffer", &st);
+  if (crcs) {
+    cb.present = 1;
+    cb.base = (*env)->GetDirectBufferAddress(env, crcs);
+    cb.capacity = (int64_t)(*env)->GetDirectBufferCapacity(env, crcs);
+    cb.offset = crcsOffset;
+    if (!cb.base) {
+      ozm_fail(OZEC_EINVAL, "crcs must be a direct buffer", &st);
+      throw_status(env, &st);
+      return 0;
+    }
+  }
+  if (ozm_queue_submit((ozec_stripe_queue *)(intptr_t)q, db, nd, pb, np, len, &cb, &ticket, &st)) {
     throw_status(env, &st);
     return 0;
   }
-  int rc = len < 0 ? OZEC_EINVAL
-                   : ozec_stripe_queue_submit((ozec_stripe_queue *)(intptr_t)q, dp, (uint8_t *const *)pp, (size_t)len,
-                                              cp, &ticket);
-  if (rc) throw_rc(env, rc);
   return (jlong)ticket;
 }
 
@@ -432,4 +437,97 @@ JNIEXPORT void JNICALL JNI_FN(reconstructHostBatch)(JNIEnv *env, jclass cls, jlo
   if (ozm_reconstruct_host_batch((ozec_coder *)(intptr_t)dec, &sb, stripeStride, unitStride, pr, npr, er, ner, &ob,
                                  numStripes, cellLen, type, bpc, &eb, &cb, &mb, &st))
     throw_status(env, &st);
+}
+
+/* ---------------------------------------------------------------- COMPOSITE_CRC (§8(f) row 4) */
+/* CrcUtil.getMonomial / CrcUtil.compose (OC/CrcUtil.java:74-127) and CrcComposer (OC/CrcComposer.java:44-215) over
+ * ozec_crc_monomial / ozec_crc_compose / ozec_crc_composer_*; OC/ = hadoop-ozone/common/src/main/java/org/apache/
+ * hadoop/ozone/client/checksum/.  HipCrcUtil / HipCrcComposer (java/.../ozone/client/checksum/) are the callers. */
+
+JNIEXPORT jint JNICALL JNI_FN(crcMonomial)(JNIEnv *env, jclass cls, jint type, jlong lengthBytes) {
+  (void)cls;
+  ozm_status st;
+  uint32_t v = 0;
+  if (ozm_crc_monomial(type, lengthBytes, &v, &st)) throw_status(env, &st);
+  return (jint)v;
+}
+
+JNIEXPORT jint JNICALL JNI_FN(crcCompose)(JNIEnv *env, jclass cls, jint type, jint crcA, jint crcB, jlong lengthB) {
+  (void)cls;
+  ozm_status st;
+  uint32_t v = 0;
+  if (ozm_crc_compose(type, (uint32_t)crcA, (uint32_t)crcB, lengthB, &v, &st)) throw_status(env, &st);
+  return (jint)v;
+}
+
+JNIEXPORT jlong JNICALL JNI_FN(composerCreate)(JNIEnv *env, jclass cls, jint type, jlong bytesPerCrcHint,
+                                               jlong stripeLength) {
+  (void)cls;
+  ozm_status st;
+  ozec_crc_composer *c = NULL;
+  if (ozm_composer_create(type, bytesPerCrcHint, stripeLength, &c, &st)) {
+    throw_status(env, &st);
+    return 0;
+  }
+  return (jlong)(intptr_t)c;
+}
+
+JNIEXPORT void JNICALL JNI_FN(composerUpdate)(JNIEnv *env, jclass cls, jlong c, jint crc, jlong bytesPerCrc) {
+  (void)cls;
+  ozm_status st;
+  if (ozm_composer_update((ozec_crc_composer *)(intptr_t)c, (uint32_t)crc, bytesPerCrc, &st)) throw_status(env, &st);
+}
+
+/* update(byte[] crcBuffer, int offset, int length, long bytesPerCrc): big-endian CRCs read in place */
+JNIEXPORT void JNICALL JNI_FN(composerUpdateBytes)(JNIEnv *env, jclass cls, jlong c, jbyteArray buf, jint offset,
+                                                   jint length, jlong bytesPerCrc) {
+  (void)cls;
+  ozm_status st;
+  const jsize cap = buf ? (*env)->GetArrayLength(env, buf) : 0;
+  const uint8_t *b = buf ? (const uint8_t *)(*env)->GetPrimitiveArrayCritical(env, buf, NULL) : NULL;
+  int rc = ozm_composer_update_bytes((ozec_crc_composer *)(intptr_t)c, b, cap, offset, length, bytesPerCrc, &st);
+  if (b) (*env)->ReleasePrimitiveArrayCritical(env, buf, (void *)b, JNI_ABORT);
+  if (rc) throw_status(env, &st);
+}
+
+/* bytes the next digest returns (the Java side sizes its array with it) */
+JNIEXPORT jint JNICALL JNI_FN(composerPending)(JNIEnv *env, jclass cls, jlong c) {
+  (void)env;
+  (void)cls;
+  return (jint)ozec_crc_composer_pending((const ozec_crc_composer *)(intptr_t)c);
+}
+
+/* digest() into out; returns its length */
+JNIEXPORT jint JNICALL JNI_FN(composerDigest)(JNIEnv *env, jclass cls, jlong c, jbyteArray out) {
+  (void)cls;
+  ozm_status st;
+  int64_t written = 0;
+  const jsize cap = out ? (*env)->GetArrayLength(env, out) : 0;
+  uint8_t *o = out ? (uint8_t *)(*env)->GetPrimitiveArrayCritical(env, out, NULL) : NULL;
+  int rc = ozm_composer_digest((ozec_crc_composer *)(intptr_t)c, o, cap, &written, &st);
+  if (o) (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
+  if (rc) throw_status(env, &st);
+  return (jint)written;
+}
+
+JNIEXPORT void JNICALL JNI_FN(composerFree)(JNIEnv *env, jclass cls, jlong c) {
+  (void)env;
+  (void)cls;
+  ozec_crc_composer_free((ozec_crc_composer *)(intptr_t)c);
+}
+
+/* ozec_crc_compose_windows_batch for a caller that holds device pointers (a GPU pipeline's window CRCs): the
+ * composite CRC of every cell from its window CRCs, on `stream` (0 = the default stream), asynchronous */
+JNIEXPORT void JNICALL JNI_FN(composeWindowsBatch)(JNIEnv *env, jclass cls, jint type, jlong dCrcs, jlong crcCellStride,
+                                                   jlong numCells, jlong numWindows, jlong bpc, jlong lastLen,
+                                                   jboolean crcsBigEndian, jlong dOut, jboolean outBigEndian,
+                                                   jlong stream) {
+  (void)cls;
+  int rc = numCells < 0 || numWindows < 0 || bpc < 0 || lastLen < 0
+               ? OZEC_EINVAL
+               : ozec_crc_compose_windows_batch(type, (const uint32_t *)(intptr_t)dCrcs, crcCellStride, (size_t)numCells,
+                                                (size_t)numWindows, (size_t)bpc, (size_t)lastLen, crcsBigEndian ? 1 : 0,
+                                                (uint32_t *)(intptr_t)dOut, outBigEndian ? 1 : 0,
+                                                (void *)(intptr_t)stream);
+  if (rc) throw_rc(env, rc);
 }

@@ -140,6 +140,42 @@ static int need(const ozm_buf *b, int64_t bytes, const char *what, const uint8_t
   return ok(st);
 }
 
+/* a * b + c in int64 without wrapping; 0 on overflow or a negative term */
+static int span(int64_t a, int64_t b, int64_t c, int64_t *out) {
+  int64_t m;
+  if (a < 0 || b < 0 || c < 0 || __builtin_mul_overflow(a, b, &m) || __builtin_add_overflow(m, c, out)) return 0;
+  return 1;
+}
+
+int ozm_queue_submit(ozec_stripe_queue *q, const ozm_buf *data, int nd, const ozm_buf *parity, int np, int64_t len,
+                     const ozm_buf *crcs, uint64_t *ticket, ozm_status *st) {
+  int k = 0, p = 0, rows = 0, ctype = 0;
+  size_t cell = 0, bpc = 0;
+  char msg[128];
+  if (!q) return ozm_fail(OZEC_ECLOSED, "HipStripeQueue closed", st);
+  int rc = ozec_stripe_queue_info(q, &k, &p, &rows, &cell, &ctype, &bpc);
+  if (rc) return ozm_fail(rc, NULL, st);
+  if (nd != k || np != p) {
+    snprintf(msg, sizeof(msg), "Invalid inputs/outputs length %d/%d != %d/%d", nd, np, k, p);
+    return ozm_fail(OZEC_EINVAL, msg, st);
+  }
+  if (len <= 0 || (uint64_t)len > cell) {
+    snprintf(msg, sizeof(msg), "stripe length %lld not in [1, %zu]", (long long)len, cell);
+    return ozm_fail(OZEC_EINVAL, msg, st);
+  }
+  const uint8_t *dp[OZEC_MAX_K], *pp[256], *cp = NULL;
+  if (k > OZEC_MAX_K || p > 256) return ozm_fail(OZEC_EUNSUPPORTED, "schema exceeds the kernel limits", st);
+  if (ozm_resolve(data, nd, 0, len, dp, st) || ozm_resolve(parity, np, 0, len, pp, st)) return st ? st->code : OZEC_EINVAL;
+  if (ctype != OZEC_CHECKSUM_NONE && crcs && crcs->present) {
+    const int64_t nwin = ((int64_t)len + (int64_t)bpc - 1) / (int64_t)bpc;
+    int64_t bytes;
+    if (!span((int64_t)(k + rows) * nwin, 4, 0, &bytes)) return ozm_fail(OZEC_EINVAL, "checksum size overflows", st);
+    if (need(crcs, bytes, "checksum", &cp, st)) return st ? st->code : OZEC_EINVAL;
+  }
+  rc = ozec_stripe_queue_submit(q, dp, (uint8_t *const *)pp, (size_t)len, (uint32_t *)cp, ticket);
+  return rc ? ozm_fail(rc, NULL, st) : ok(st);
+}
+
 int ozm_reconstruct_host_batch(ozec_coder *dec, const ozm_buf *stripes, int64_t stripe_stride, int64_t unit_stride,
                                const int *present, int npresent, const int *erased, int nerased, const ozm_buf *out,
                                int64_t num_stripes, int64_t cell_len, int checksum_type, int64_t bpc,
@@ -156,19 +192,106 @@ int ozm_reconstruct_host_batch(ozec_coder *dec, const ozm_buf *stripes, int64_t 
   if (num_stripes == 0 || cell_len == 0) return ok(st);
   const int64_t nwin = (cell_len + bpc - 1) / bpc, S = num_stripes;
   const uint8_t *in = NULL, *o = NULL, *oc = NULL, *ex = NULL, *mm = NULL;
-  if (need(stripes, (S - 1) * stripe_stride + (int64_t)(k + p - 1) * unit_stride + cell_len, "stripe", &in, st))
-    return st ? st->code : OZEC_EINVAL;
-  if (nerased && (need(out, S * nerased * cell_len, "output", &o, st) ||
-                  need(out_crcs, S * nerased * nwin * 4, "checksum output", &oc, st)))
+  /* every layout size in checked arithmetic: a huge Java stride must not wrap past the capacity check */
+  int64_t last_unit, in_bytes, out_bytes, crc_bytes, exp_bytes, ner_cells, ner_crcs, units_crcs, out_stride;
+  if (!span((int64_t)(k + p - 1), unit_stride, cell_len, &last_unit) ||
+      !span(S - 1, stripe_stride, last_unit, &in_bytes) || !span(S, nerased, 0, &ner_cells) ||
+      !span(ner_cells, cell_len, 0, &out_bytes) || !span(ner_cells, nwin, 0, &ner_crcs) ||
+      !span(ner_crcs, 4, 0, &crc_bytes) || !span(S, (int64_t)(k + p) * nwin, 0, &units_crcs) ||
+      !span(units_crcs, 4, 0, &exp_bytes) || !span(nerased, cell_len, 0, &out_stride))
+    return ozm_fail(OZEC_EINVAL, "buffer layout size overflows", st);
+  if (need(stripes, in_bytes, "stripe", &in, st)) return st ? st->code : OZEC_EINVAL;
+  if (nerased && (need(out, out_bytes, "output", &o, st) || need(out_crcs, crc_bytes, "checksum output", &oc, st)))
     return st ? st->code : OZEC_EINVAL;
   if (expected && expected->present) {
-    if (need(expected, S * (k + p) * nwin * 4, "expected checksum", &ex, st) ||
-        need(mismatch, S * 4, "mismatch", &mm, st))
+    if (need(expected, exp_bytes, "expected checksum", &ex, st) || need(mismatch, S * 4, "mismatch", &mm, st))
       return st ? st->code : OZEC_EINVAL;
   }
   int rc = ozec_reconstruct_crc_host_batch(dec, in, stripe_stride, unit_stride, present, npresent, erased, nerased,
-                                           (uint8_t *)o, nerased * cell_len, cell_len, (size_t)S, (size_t)cell_len,
+                                           (uint8_t *)o, out_stride, cell_len, (size_t)S, (size_t)cell_len,
                                            checksum_type, (size_t)bpc, (const uint32_t *)ex, 1, (uint32_t *)oc, 1,
                                            (int32_t *)mm, 0);
   return rc ? ozm_fail(rc, NULL, st) : ok(st);
+}
+
+/* ---------------------------------------------------------------- COMPOSITE_CRC */
+
+/* like ozm_fail, with the reference's exception class instead of the status's default */
+static int fail_as(int rc, const char *cls, const char *msg, ozm_status *st) {
+  ozm_fail(rc, msg, st);
+  if (st) snprintf(st->exception_class, sizeof(st->exception_class), "%s", cls);
+  return rc;
+}
+
+static int crc_type_ok(int checksum_type, ozm_status *st) {
+  char msg[96];
+  if (checksum_type == OZEC_CHECKSUM_CRC32 || checksum_type == OZEC_CHECKSUM_CRC32C) return ok(st);
+  snprintf(msg, sizeof(msg), "No CRC polynomial could be associated with type: %d", checksum_type);
+  return fail_as(OZEC_EINVAL, "java/io/IOException", msg, st);
+}
+
+int ozm_crc_monomial(int checksum_type, int64_t len_bytes, uint32_t *out, ozm_status *st) {
+  if (crc_type_ok(checksum_type, st)) return st ? st->code : OZEC_EINVAL;
+  int rc = ozec_crc_monomial(checksum_type, len_bytes, out);
+  return rc ? fail_as(rc, "java/lang/IllegalArgumentException", NULL, st) : ok(st);
+}
+
+int ozm_crc_compose(int checksum_type, uint32_t crc_a, uint32_t crc_b, int64_t len_b, uint32_t *out, ozm_status *st) {
+  if (crc_type_ok(checksum_type, st)) return st ? st->code : OZEC_EINVAL;
+  int rc = ozec_crc_compose(checksum_type, crc_a, crc_b, len_b, out);
+  return rc ? fail_as(rc, "java/lang/IllegalArgumentException", NULL, st) : ok(st);
+}
+
+int ozm_composer_create(int checksum_type, int64_t bytes_per_crc_hint, int64_t stripe_length,
+                        ozec_crc_composer **out, ozm_status *st) {
+  if (crc_type_ok(checksum_type, st)) return st ? st->code : OZEC_EINVAL;
+  /* newStripedCrcComposer's getMonomial(bytesPerCrcHint) rejects a negative hint */
+  if (bytes_per_crc_hint < 0) {
+    char msg[96];
+    snprintf(msg, sizeof(msg), "lengthBytes must be positive, got %lld", (long long)bytes_per_crc_hint);
+    return fail_as(OZEC_EINVAL, "java/lang/IllegalArgumentException", msg, st);
+  }
+  int rc = ozec_crc_composer_create(checksum_type, bytes_per_crc_hint, stripe_length, out);
+  return rc ? ozm_fail(rc, NULL, st) : ok(st);
+}
+
+int ozm_composer_update(ozec_crc_composer *c, uint32_t crc, int64_t bytes_per_crc, ozm_status *st) {
+  if (!c) return fail_as(OZEC_ECLOSED, "java/io/IOException", "CrcComposer closed", st);
+  int rc = ozec_crc_composer_update(c, crc, bytes_per_crc);
+  if (rc == OZEC_EMISMATCH) return fail_as(rc, "java/io/IOException", NULL, st);
+  return rc ? fail_as(rc, "java/lang/IllegalArgumentException", NULL, st) : ok(st);
+}
+
+int ozm_composer_update_bytes(ozec_crc_composer *c, const uint8_t *buf, int64_t cap, int64_t offset, int64_t length,
+                              int64_t bytes_per_crc, ozm_status *st) {
+  char msg[160];
+  if (!c) return fail_as(OZEC_ECLOSED, "java/io/IOException", "CrcComposer closed", st);
+  if (length % 4 != 0) {
+    snprintf(msg, sizeof(msg),
+             "Trying to update CRC from byte array with length '%lld' at offset '%lld' which is not a multiple of 4!",
+             (long long)length, (long long)offset);
+    return fail_as(OZEC_EINVAL, "java/io/IOException", msg, st);
+  }
+  if (length <= 0) return ok(st);
+  if (!buf || offset < 0 || offset + length > cap) {
+    snprintf(msg, sizeof(msg), "Index %lld out of bounds for length %lld",
+             (long long)(offset < 0 ? offset : offset + length - 1), (long long)cap);
+    return fail_as(OZEC_EINVAL, "java/lang/ArrayIndexOutOfBoundsException", msg, st);
+  }
+  for (int64_t i = 0; i < length; i += 4) { /* one CRC at a time, so a stripe overrun stops where the reference does */
+    const uint8_t *b = buf + offset + i;
+    const uint32_t v = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+    if (ozm_composer_update(c, v, bytes_per_crc, st)) return st ? st->code : OZEC_EINVAL;
+  }
+  return ok(st);
+}
+
+int ozm_composer_digest(ozec_crc_composer *c, uint8_t *out, int64_t cap, int64_t *written, ozm_status *st) {
+  size_t len = 0;
+  if (written) *written = 0;
+  if (!c) return fail_as(OZEC_ECLOSED, "java/io/IOException", "CrcComposer closed", st);
+  int rc = ozec_crc_composer_digest(c, out, cap < 0 ? 0 : (size_t)cap, &len);
+  if (rc) return ozm_fail(rc, NULL, st);
+  if (written) *written = (int64_t)len;
+  return ok(st);
 }

@@ -84,6 +84,29 @@ int ozm_reconstruct_host_batch(ozec_coder *dec, const ozm_buf *stripes, int64_t 
                                const ozm_buf *expected, const ozm_buf *out_crcs, const ozm_buf *mismatch,
                                ozm_status *st);
 
+/* HipStripeQueue.submit (ozec_stripe_queue_submit): nd == k data cells and np == p parity cells of len bytes from
+ * their offsets; crcs (absent = no CRCs wanted) must hold (k + coded rows) * ceil(len / bpc) 4-byte values from its
+ * offset when the queue computes checksums.  *ticket identifies the stripe. */
+int ozm_queue_submit(ozec_stripe_queue *q, const ozm_buf *data, int nd, const ozm_buf *parity, int np, int64_t len,
+                     const ozm_buf *crcs, uint64_t *ticket, ozm_status *st);
+
+/* ---- COMPOSITE_CRC: CrcUtil / CrcComposer (OC/CrcUtil.java:74-127, OC/CrcComposer.java:44-215; OC/ =
+ * hadoop-ozone/common/src/main/java/org/apache/hadoop/ozone/client/checksum/) with the reference's exceptions:
+ * a negative length -> java.lang.IllegalArgumentException (CrcUtil.getMonomial), an unsupported type or a composer
+ * position past its stripe -> java.io.IOException (CrcUtil.getCrcPolynomialForType, CrcComposer.update), a CRC
+ * byte run whose length is not a multiple of 4 -> java.io.IOException, one past the array ->
+ * java.lang.ArrayIndexOutOfBoundsException (CrcUtil.readInt). */
+int ozm_crc_monomial(int checksum_type, int64_t len_bytes, uint32_t *out, ozm_status *st);
+int ozm_crc_compose(int checksum_type, uint32_t crc_a, uint32_t crc_b, int64_t len_b, uint32_t *out, ozm_status *st);
+int ozm_composer_create(int checksum_type, int64_t bytes_per_crc_hint, int64_t stripe_length,
+                        ozec_crc_composer **out, ozm_status *st);
+int ozm_composer_update(ozec_crc_composer *c, uint32_t crc, int64_t bytes_per_crc, ozm_status *st);
+/* update(byte[] crcBuffer, int offset, int length, long bytesPerCrc): buf is the array, cap its length */
+int ozm_composer_update_bytes(ozec_crc_composer *c, const uint8_t *buf, int64_t cap, int64_t offset, int64_t length,
+                              int64_t bytes_per_crc, ozm_status *st);
+/* digest() into out (cap bytes; at least ozec_crc_composer_pending()); *written = digest length */
+int ozm_composer_digest(ozec_crc_composer *c, uint8_t *out, int64_t cap, int64_t *written, ozm_status *st);
+
 #ifdef __cplusplus
 }
 #endif

@@ -203,6 +203,25 @@ static int run_unit(struct job *j) {
 
 static double g_stop;
 
+/* one percall_windows thread: its own buffer, every 16 KiB window CRC32C'd, until `secs` have passed */
+static void *percall_windows_thread(void *arg) {
+  struct pw { size_t n; double secs; long calls; double t; uint32_t sink; } *j = arg;
+  uint8_t *buf = aligned_alloc(4096, (j->n + 4095) / 4096 * 4096);
+  fill(buf, j->n, 31);
+  const double t0 = now();
+  double t = t0;
+  uint32_t sink = 0;
+  do {
+    for (size_t off = 0; off < j->n; off += BPC) sink ^= crc32c_hw(buf + off, j->n - off < BPC ? j->n - off : BPC);
+    j->calls++;
+    t = now();
+  } while (t - t0 < j->secs);
+  j->t = t - t0;
+  j->sink = sink;
+  free(buf);
+  return NULL;
+}
+
 static void *worker(void *arg) {
   struct job *j = arg;
   while (now() < g_stop) {
@@ -221,6 +240,33 @@ int main(int argc, char **argv) {
     return 2;
   }
   g_workload = argv[1];
+  if (!strcmp(g_workload, "percall_windows")) {
+    /* Checksum.computeChecksum of one n-byte buffer: CRC32C of every 16 KiB window (the JDK-class SSE4.2 CRC per
+     * window), from T threads at once, each on its own buffer: usage percall_windows <bytes> <seconds> [threads] */
+    const size_t n = (size_t)atol(argv[2]);
+    const double secs = atof(argv[3]);
+    const int T = argc > 4 && atoi(argv[4]) > 0 ? atoi(argv[4]) : 1;
+    pthread_t th[256];
+    struct pw { size_t n; double secs; long calls; double t; uint32_t sink; } jobs[256];
+    void *(*run)(void *) = percall_windows_thread;
+    for (int i = 0; i < T && i < 256; i++) {
+      jobs[i] = (struct pw){n, secs, 0, 0, 0};
+      pthread_create(&th[i], NULL, run, &jobs[i]);
+    }
+    long calls = 0;
+    double tmax = 0;
+    uint32_t sink = 0;
+    for (int i = 0; i < T && i < 256; i++) {
+      pthread_join(th[i], NULL);
+      calls += jobs[i].calls;
+      tmax = jobs[i].t > tmax ? jobs[i].t : tmax;
+      sink ^= jobs[i].sink;
+    }
+    printf("{\"workload\": \"%s\", \"bytes\": %zu, \"threads\": %d, \"calls\": %ld, \"us_per_call\": %.3f, "
+           "\"GBps\": %.3f, \"sink\": %u}\n", g_workload, n, T, calls, tmax / ((double)calls / T) * 1e6,
+           (double)calls * n / tmax / 1e9, sink);
+    return 0;
+  }
   if (!strcmp(g_workload, "percall_crc32c") || !strcmp(g_workload, "percall_encode")) {
     /* per-call cost of one ChecksumByteBuffer.update(n bytes) / one rs-6-3 stripe encode of n-byte cells,
      * single thread (the JDK intrinsic / rs_java call a Java writer makes): usage percall_* <bytes> <seconds> */

@@ -67,6 +67,9 @@ _SIGS = {
     "ozec_decoder_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_voidp)]),
     "ozec_coder_release": (ctypes.c_int, [c_voidp]),
     "ozec_coder_free": (None, [c_voidp]),
+    "ozec_coder_retain": (ctypes.c_int, [c_voidp]),
+    "ozec_release_staging": (ctypes.c_int, []),
+    "ozec_coder_is_closed": (ctypes.c_int, [c_voidp]),
     "ozec_coder_info": (ctypes.c_int, [c_voidp, c_intp, c_intp, c_intp, c_intp]),
     "ozec_encode": (ctypes.c_int, [c_voidp, c_ptrs, c_ptrs, c_size]),
     "ozec_decode": (ctypes.c_int, [c_voidp, c_ptrs, c_intp, ctypes.c_int, c_ptrs, c_size]),
@@ -110,11 +113,15 @@ _SIGS = {
     "ozec_device_numa_node": (ctypes.c_int, [ctypes.c_int, c_intp]),
     "ozec_host_page_node": (ctypes.c_int, [c_voidp, c_intp]),
     "ozec_host_register": (ctypes.c_int, [c_voidp, c_size, ctypes.c_int]),
+    "ozec_host_placement_failures": (ctypes.c_uint64, []),
     "ozec_host_unregister": (ctypes.c_int, [c_voidp]),
     "ozec_encode_crc_block_groups": (ctypes.c_int, [c_voidp, c_voidp, c_i64, c_i64, c_size, c_size, c_size,
                                                     ctypes.c_int, c_size, c_voidp, ctypes.c_int, c_voidp]),
     "ozec_encode_crc_host_batch": (ctypes.c_int, [c_voidp, c_voidp, c_i64, c_i64, c_voidp, c_i64, c_i64, c_size,
                                                   c_size, ctypes.c_int, c_size, c_voidp, ctypes.c_int, c_size]),
+    "ozec_stripe_queue_info": (ctypes.c_int, [c_voidp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(c_size),
+                                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(c_size)]),
     "ozec_stripe_queue_state": (ctypes.c_int, [c_voidp, ctypes.POINTER(c_size), ctypes.POINTER(ctypes.c_uint64),
                                                ctypes.POINTER(c_size)]),
     "ozec_stripe_queue_create": (ctypes.c_int, [c_voidp, c_size, c_size, ctypes.c_int, c_size, ctypes.c_int,

@@ -87,6 +87,15 @@ struct Slot {
     }
     return OZEC_OK;
   }
+
+  // give the staging buffers back (an idle slot: its stream has drained)
+  void shrink() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (pinned) (void)ozec::pinned_free(pinned);
+    if (dbuf) (void)hipFree(dbuf);
+    pinned = dbuf = nullptr;
+    pinned_cap = dbuf_cap = 0;
+  }
 };
 
 // End-to-end pipeline of ozec_encode_crc_host_batch: a ring of NB device chunk buffers; the chunk's H2D copies,
@@ -101,6 +110,19 @@ struct E2E {
   size_t dcap = 0;
   uint8_t *hstage[NB] = {};  // pinned staging, only for pageable caller buffers
   size_t hcap = 0;
+
+  // give the chunk buffers back; caller holds mu (the last call's streams were drained before it returned)
+  void shrink() {
+    for (auto &d : dbuf) {
+      if (d) (void)hipFree(d);
+      d = nullptr;
+    }
+    for (auto &h : hstage) {
+      if (h) (void)ozec::pinned_free(h);
+      h = nullptr;
+    }
+    dcap = hcap = 0;
+  }
 };
 
 struct DevCtx {
@@ -226,6 +248,7 @@ struct ozec_coder {
   int k = 0, p = 0;
   bool decoder = false;
   std::atomic<bool> closed{false};
+  std::atomic<int> refs{1};  // owners: the creator, plus one per ozec_coder_retain (a stripe queue holds one)
   std::vector<uint8_t> parity_rows;  // p x k (RS) -- RSRawEncoder's encodeMatrix rows k..k+p-1
   // decode cache on (erased, valid) like RSRawDecoder.prepareDecoding (RSRawDecoder.java:103-115)
   std::mutex cache_mu;
@@ -444,7 +467,29 @@ int ozec_coder_release(ozec_coder *c) {
   return OZEC_OK;
 }
 
-void ozec_coder_free(ozec_coder *c) { delete c; }
+void ozec_coder_free(ozec_coder *c) {
+  if (c && c->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete c;
+}
+
+int ozec_release_staging(void) {
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  {
+    std::lock_guard<std::mutex> lk(ctx->e2e.mu);
+    ctx->e2e.shrink();
+  }
+  std::lock_guard<std::mutex> lk(ctx->pool_mu);
+  for (Slot *s : ctx->free_slots) s->shrink();  // leased slots keep theirs until their call returns
+  return OZEC_OK;
+}
+
+int ozec_coder_retain(ozec_coder *c) {
+  if (!c) return fail(OZEC_EINVAL, "null coder");
+  c->refs.fetch_add(1, std::memory_order_relaxed);
+  return OZEC_OK;
+}
+
+int ozec_coder_is_closed(const ozec_coder *c) { return c && c->closed.load() ? 1 : 0; }
 
 int ozec_coder_info(const ozec_coder *c, int *codec, int *k, int *p, int *is_decoder) {
   if (!c) return fail(OZEC_EINVAL, "null coder");

@@ -24,6 +24,10 @@
 //
 // Same results as encode_crc_g26 bit for bit (same G26 tables, same per-lane folding, same lane tree); the
 // launcher (launch_encode_crc) picks this kernel for the shapes and geometries above and falls back otherwise.
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "device.hpp"
 
 namespace ozec {
@@ -290,6 +294,55 @@ __device__ __forceinline__ uint2 lds64(const void *base, uint32_t byte_off) {
   return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + byte_off);
 }
 
+// Dynamic work distribution of the persistent nibble kernel (DYN variants).  The (stripe, window) units are cut into
+// 8 contiguous ranges, one per XCD (the dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b starts
+// on range b % 8: each XCD streams one contiguous eighth of the batch), and a wave takes the next unit of its range
+// with one atomicAdd (a vector-memory atomic issued by lane 0 and broadcast with readfirstlane); a wave whose range is
+// used up moves on to the next range, so every unit is taken exactly once whatever the grid size or placement.  The
+// counters are a per-stream slot (launch_nb): launches on one stream run in order, and the last wave of a launch to
+// finish puts the slot back to zero for the next one.
+constexpr int kWqStride = 16;                 // ints between counters (64 B: one counter per cache line)
+constexpr int kWqDone = 8 * kWqStride;        // finished-wave counter
+constexpr int kWqInts = kWqDone + kWqStride;  // ints per slot
+struct WorkQueue {
+  int32_t *ctr;
+  int64_t units;
+  int q0, qi;
+  int64_t cur, end;  // claimed units [cur, end) not yet handed out (chunked claims)
+  int32_t seen;      // the own range's counter after this wave's last claim
+  int32_t per_range; // waves per range (chunk size of a guided claim: what is left / 2 per wave)
+  __device__ __forceinline__ int64_t next(int lane, bool guided) {
+    if (cur < end) return cur++;
+    while (qi < 8) {
+      const int q = (q0 + qi) & 7;
+      const int64_t lo = units * q / 8, hi = units * (q + 1) / 8;
+      int32_t c = 1;
+      if (guided && qi == 0) {
+        const int64_t left = hi - lo - seen;
+        c = static_cast<int32_t>(std::min<int64_t>(8, std::max<int64_t>(1, left / (2 * per_range))));
+      }
+      int32_t t = 0;
+      if (lane == 0) t = atomicAdd(ctr + q * kWqStride, c);
+      t = __builtin_amdgcn_readfirstlane(t);
+      seen = t + c;
+      if (lo + t < hi) {
+        cur = lo + t;
+        end = std::min<int64_t>(hi, cur + c);
+        return cur++;
+      }
+      ++qi;
+    }
+    return units;
+  }
+  // every wave calls this once after its last unit: the last of `waves` resets the slot
+  __device__ __forceinline__ void finish(int lane, int32_t waves) {
+    if (lane == 0 && atomicAdd(ctr + kWqDone, 1) == waves - 1) {
+      for (int q = 0; q < 8; ++q) atomicExch(ctr + q * kWqStride, 0);
+      atomicExch(ctr + kWqDone, 0);
+    }
+  }
+};
+
 // byte offset of the entry region of (distance set d, input j, byte i): lo-nibble table at +0, hi at +8
 template <int K>
 constexpr uint32_t nb_region(int d, int j, int i) {
@@ -314,8 +367,11 @@ __device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t 
 
 // K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
 // FENCE: dwords of a block whose lookups go between scheduling fences (2: halves, at most 16 results live; 1:
-// quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree
-template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true>
+// quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree;
+// DYN: 0 one wave per unit, no grid-stride; persistent grid (one resident set of workgroups, tables built once per
+// workgroup) fed by the WorkQueue with 1 a claim per unit, made one unit ahead, 3 guided claims of up to 8 units, 4 a
+// claim per unit made when it is needed; 2 persistent grid with the static grid-stride order
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -363,7 +419,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
   const uint32_t in_extent = static_cast<uint32_t>(off_max + cr.bpc);
   const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
-  for (int64_t u = bid * WPB + wave; u < units; u += static_cast<int64_t>(gridDim.x) * WPB) {
+  constexpr bool kQueue = DYN == 1 || DYN == 3 || DYN == 4;
+  WorkQueue wq{e.work, units, static_cast<int>(blockIdx.x & 7), 0, 0, 0, 0, static_cast<int32_t>(gridDim.x * WPB / 8)};
+  int64_t u = kQueue ? wq.next(lane, DYN == 3) : bid * WPB + wave;
+  while (u < units) {
+    // DYN 1 / 3: the next unit is claimed before this one is worked on, so the atomic's round trip overlaps the work
+    const int64_t u_next = DYN == 1 || DYN == 3 ? wq.next(lane, DYN == 3) : u + static_cast<int64_t>(gridDim.x) * WPB;
     // wave-uniform by construction; said explicitly so the descriptors below stay in SGPRs (the 64-bit division
     // runs in the VALU, and without this the buffer accesses were wrapped in waterfall loops)
     const int64_t s = uniform64(u / nwin);
@@ -467,24 +528,68 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         if (lane == q) nb_emit<K, R>(e, s, w, q, v, init);
       }
     }
+    u = DYN == 4 ? wq.next(lane, false) : u_next;
   }
+  if constexpr (kQueue) wq.finish(lane, static_cast<int32_t>(gridDim.x) * WPB);
 }
 
-template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true>
+// Counter slot of the WorkQueue for launches on `st` (per device and stream, zeroed once on that stream; launches
+// on one stream run in order and each leaves its slot at zero).  Null when no slot can be had.
+int32_t *work_slot(hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, int32_t *> slots;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = slots.find({dev, st});
+  if (it != slots.end()) return it->second;
+  if (slots.size() >= 4096) return nullptr;
+  void *p = nullptr;
+  if (hipMalloc(&p, kWqInts * sizeof(int32_t)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, kWqInts * sizeof(int32_t), st) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  slots[{dev, st}] = static_cast<int32_t *>(p);
+  return static_cast<int32_t *>(p);
+}
+
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
+    // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
+    // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
     constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
-    static_assert(kNB != NB, "fallback ring must differ");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS>(e, st);
+    static_assert(kNB != NB && (D * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS>;
-    // one wave per (stripe, window) unit, no grid-stride: every workgroup builds its K*D*4 KiB of tables, and the
-    // dispatcher's refill of finished workgroups balances the CUs.  Measured on MI355X against a persistent grid
-    // of one resident set (profiles/r02/nb/ab_grid_*.log): C3r 56.2 % -> 63.5 %, C5dev 60.1 % -> 65.7 %.
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
-    const int64_t g = std::min<int64_t>(g_tune.crc_grid > 0 ? g_tune.crc_grid : blocks, blocks);
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, e);
+    int64_t g = blocks;
+    EncCrcArgs ed = e;
+    if constexpr (DYN != 0) {
+      // persistent: one resident set of workgroups (occupancy x CUs), each building its tables once
+      static int resident = 0;  // per instantiation and process (one device type)
+      if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WPB * 64, 0) != hipSuccess)
+          return hipErrorInvalidValue;
+        resident = std::max(1, cus * std::max(1, per_cu));
+      }
+      if constexpr (DYN != 2) {
+        ed.work = work_slot(st);
+        if (ed.work == nullptr || units > (int64_t{1} << 30)) return hipErrorInvalidValue;
+      }
+      g = std::min<int64_t>(resident, blocks);
+    }
+    // non-persistent: one wave per (stripe, window) unit, no grid-stride: every workgroup builds its K*D*4 KiB of
+    // tables, and the dispatcher's refill of finished workgroups balances the CUs.  Measured on MI355X against a
+    // static persistent grid (profiles/r02/nb/ab_grid_*.log): C3r 56.2 % -> 63.5 %, C5dev 60.1 % -> 65.7 %.
+    if (g_tune.crc_grid > 0) g = std::min<int64_t>(g_tune.crc_grid, blocks);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, ed);
     return hipGetLastError();
   }
 }
@@ -494,6 +599,8 @@ template <int K, int R>
 hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
   constexpr int kD2 = K * 2 * 4096 + g26_words(2) * 4 <= 65536 ? 2 : 1;  // D = 2 where its tables fit
   constexpr int kNB = K % 2 == 0 && K > 2 ? K / 2 : K;                    // a deeper ring dividing the group
+  constexpr auto lds_of = [](int d) { return (g26_words(d) * 4 + 255) / 256 * 256 + K * d * 4096 + K * 128; };
+  constexpr int kDmax = lds_of(4) <= 160 * 1024 ? 4 : lds_of(2) <= 160 * 1024 ? 2 : 1;  // one workgroup per CU
   switch (v) {
     case 61: return launch_nb<K, R, 1, 2, 8, 4>(e, st);
     case 62: return launch_nb<K, R, 1, kNB, 8, 4>(e, st);
@@ -530,6 +637,21 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 93: return launch_nb<K, R, K == 10 ? 1 : kD2, K == 10 ? kNB : 2, K == 10 ? 8 : 12, 4, 0>(e, st);
     case 94: return launch_nb<K, R, K == 10 ? 1 : kD2, K == 10 ? kNB : 2, K == 10 ? 8 : 12, 4, 4>(e, st);
     case 95: return launch_nb<K, R, K == 10 ? 1 : kD2, 2, K == 10 ? 8 : 12, 4, 0>(e, st);
+    // persistent grid fed by the WorkQueue: the widest step groups whose tables fit one workgroup per CU (rs-10-x:
+    // D = 2, 95 KiB; rs-6-x / rs-3-x: D = 4, 117 / 69 KiB), and the round-2 geometries made persistent
+    case 100: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 1>(e, st);
+    case 101: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 1>(e, st);
+    case 102: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1>(e, st);
+    case 103: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 1>(e, st);
+    case 104: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1>(e, st);
+    case 105: return launch_nb<K, R, kDmax, 2, 12, 4, 2, true, 1>(e, st);
+    // the same geometry (round-2 rs-10-x default) with the static persistent order, guided claims, late claims
+    case 106: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 2>(e, st);
+    case 107: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 3>(e, st);
+    case 108: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 4>(e, st);
+    case 109: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 3>(e, st);
+    case 110: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 3>(e, st);
+    case 111: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 2>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);
@@ -552,7 +674,7 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // two-step groups in 12-wave workgroups (87: C5dev 66.9 %; encode_crc_lv 57.9 %); 56 / 59 pin the streamed-input
   // kernel's defaults
   if (v == 0) v = k == 10 ? 62 : 87;
-  if (v >= 60 && v < 100) {
+  if (v >= 60 && v < 120) {
     if (k == 6 && r == 3) return launch_nb_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_nb_kr<6, 2>(e, st, v);
     if (k == 3 && r == 2) return launch_nb_kr<3, 2>(e, st, v);

@@ -70,6 +70,7 @@ struct EncCrcArgs {
   int32_t verify;
   int32_t exp_units;
   int32_t in_unit[OZEC_MAX_K];
+  int32_t *work;  // WorkQueue counter slot of the persistent nibble kernel (set by its launcher)
 };
 
 // Device CRC "G5" table blob (uint32 entries), built on the host (crc_host.cpp), one per (CRC type, B) where

@@ -11,6 +11,7 @@
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <mutex>
@@ -94,12 +95,18 @@ int device_numa_node(int device) {
   }
 }
 
-int bind_to_node(void *p, size_t bytes, int node, bool move) {
+int bind_to_node(void *p, size_t bytes, int node, bool move, bool inner) {
   if (node < 0 || !p || bytes == 0) return 0;
   if (static_cast<size_t>(node) >= kMaxNodes) return -EINVAL;
+  // test hook (tests/test_gpu_e2e.py): placement fails as it does under a seccomp profile without CAP_SYS_NICE
+  static const bool fail = std::getenv("OZEC_TEST_FAIL_MBIND") != nullptr;
+  if (fail) return -EPERM;
   const size_t ps = page_size();
-  const uintptr_t lo = reinterpret_cast<uintptr_t>(p) / ps * ps;
-  const uintptr_t hi = (reinterpret_cast<uintptr_t>(p) + bytes + ps - 1) / ps * ps;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = a + bytes;
+  // inner: only the pages wholly inside [p, p + bytes) -- never the neighbours' data on a shared first/last page
+  const uintptr_t lo = inner ? (a + ps - 1) / ps * ps : a / ps * ps;
+  const uintptr_t hi = inner ? b / ps * ps : (b + ps - 1) / ps * ps;
+  if (hi <= lo) return 0;
   unsigned long mask[kMaxNodes / (8 * sizeof(unsigned long))] = {};
   mask[node / (8 * sizeof(unsigned long))] = 1ul << (node % (8 * sizeof(unsigned long)));
   long rc = syscall(SYS_mbind, lo, hi - lo, kMpolPreferred, mask, kMaxNodes, move ? kMpolMfMove : 0u);
@@ -120,7 +127,7 @@ int pinned_alloc(size_t bytes, int device, void **out) {
   if (p == MAP_FAILED) return -ENOMEM;
   (void)madvise(p, len, MADV_HUGEPAGE);  // fewer translations per DMA; best effort
   // placement first (pages are allocated on the first touch, which hipHostRegister does while pinning)
-  (void)bind_to_node(p, len, device >= 0 ? device_numa_node(device) : -1, false);
+  (void)bind_to_node(p, len, device >= 0 ? device_numa_node(device) : -1, false, false);
   if (hipHostRegister(p, len, hipHostRegisterPortable) != hipSuccess) {
     (void)hipGetLastError();
     munmap(p, len);

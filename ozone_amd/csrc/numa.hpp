@@ -9,9 +9,10 @@ namespace ozec {
 
 // host NUMA node closest to `device`, -1 when unknown or the host is not NUMA
 int device_numa_node(int device);
-// mbind [p, p+bytes) (page-aligned outward) to `node` with MPOL_PREFERRED (MOVE existing pages when move);
+// mbind [p, p+bytes) to `node` with MPOL_PREFERRED (MOVE existing pages when move): page-aligned outward, or with
+// inner only the pages wholly inside the range (caller memory whose first / last page it may share with others);
 // returns 0 or -errno.  node < 0 is a no-op.
-int bind_to_node(void *p, size_t bytes, int node, bool move);
+int bind_to_node(void *p, size_t bytes, int node, bool move, bool inner);
 // node of the page holding p (after it has been touched), -1 if unknown
 int page_node(const void *p);
 // pinned host allocation whose pages live on the device's node; free with pinned_free

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -31,6 +32,8 @@
 namespace {
 
 using ozec::set_error;
+
+std::atomic<uint64_t> g_place_failures{0};  // ozec_host_register calls whose NUMA placement was refused
 
 // batches in the ring: copies of the newest batches keep the link busy while the oldest one drains
 constexpr size_t kDefaultBatches = 3;
@@ -205,12 +208,16 @@ int ozec_host_register(void *p, size_t bytes, int device) {
   if (!p) return set_error(OZEC_EINVAL, "null pointer");
   if (bytes == 0) return OZEC_OK;
   const int node = device >= 0 ? ozec::device_numa_node(device) : -1;
-  // pages not touched yet are placed on the node as hipHostRegister faults them in; touched ones are moved
-  if (int e = ozec::bind_to_node(p, bytes, node, true))
-    return set_error(OZEC_EINVAL, "mbind to node " + std::to_string(node) + " failed: " + std::strerror(-e));
+  // placement is best effort, as for pinned_alloc: pages not touched yet are placed on the node as hipHostRegister
+  // faults them in, touched ones are moved -- only pages wholly inside the range.  Where mbind is refused (EPERM
+  // under a seccomp profile without CAP_SYS_NICE, ENOSYS without NUMA) the memory is still pinned where it lies;
+  // ozec_host_page_node shows the placement, and the failure is counted in g_place_failures.
+  if (ozec::bind_to_node(p, bytes, node, true, true) != 0) g_place_failures.fetch_add(1, std::memory_order_relaxed);
   SQ_HIP(hipHostRegister(p, bytes, hipHostRegisterPortable));
   return OZEC_OK;
 }
+
+uint64_t ozec_host_placement_failures(void) { return g_place_failures.load(std::memory_order_relaxed); }
 
 int ozec_host_unregister(void *p) {
   if (!p) return set_error(OZEC_EINVAL, "null pointer");
@@ -230,8 +237,12 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
       checksum_type != OZEC_CHECKSUM_CRC32C)
     return set_error(OZEC_EINVAL, "checksum type must be NONE, CRC32 or CRC32C");
   if (checksum_type != OZEC_CHECKSUM_NONE && bpc == 0) return set_error(OZEC_EINVAL, "bytesPerChecksum must be positive");
+  if (ozec_coder_is_closed(enc)) return set_error(OZEC_ECLOSED, "stripe queue: the encoder is closed");
   auto *q = new (std::nothrow) ozec_stripe_queue();
   if (!q) return set_error(OZEC_ENOMEM, "out of memory");
+  // the queue co-owns the encoder: it stays allocated until ozec_stripe_queue_free even if its creator releases and
+  // frees it first (the queue's launches then fail with OZEC_ECLOSED)
+  (void)ozec_coder_retain(enc);
   q->enc = enc;
   if (hipGetDevice(&q->device) != hipSuccess) {
     delete q;
@@ -280,6 +291,7 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
     if (!parity[r]) return set_error(OZEC_EINVAL, "Invalid buffer found, not allowing null");
   if (len == 0 || len > q->cell_len)
     return set_error(OZEC_EINVAL, "stripe length must be in [1, cell_len] (" + std::to_string(q->cell_len) + ")");
+  if (ozec_coder_is_closed(q->enc)) return set_error(OZEC_ECLOSED, "stripe queue submit failed: the encoder is closed");
   std::lock_guard<std::mutex> lk(q->mu);
   Batch *b = &q->batches[q->cur];
   // cur only ever points at a filling batch or, once the ring has wrapped, at the oldest in-flight one: that one
@@ -365,6 +377,18 @@ int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket) {
   }
 }
 
+int ozec_stripe_queue_info(const ozec_stripe_queue *q, int *num_data, int *num_parity, int *rows, size_t *cell_len,
+                           int *checksum_type, size_t *bytes_per_checksum) {
+  if (!q) return set_error(OZEC_EINVAL, "null queue");
+  if (num_data) *num_data = q->k;
+  if (num_parity) *num_parity = q->p;
+  if (rows) *rows = q->rows;
+  if (cell_len) *cell_len = q->cell_len;
+  if (checksum_type) *checksum_type = q->ctype;
+  if (bytes_per_checksum) *bytes_per_checksum = q->bpc;
+  return OZEC_OK;
+}
+
 int ozec_stripe_queue_state(ozec_stripe_queue *q, size_t *in_flight, uint64_t *oldest_in_flight_ticket,
                             size_t *filling) {
   if (!q) return set_error(OZEC_EINVAL, "null queue");
@@ -420,6 +444,7 @@ int ozec_stripe_queue_free(ozec_stripe_queue *q) {
     if (b.stream) (void)hipStreamDestroy(b.stream);
   }
   if (q->h2d) (void)hipStreamDestroy(q->h2d);
+  ozec_coder_free(q->enc);  // the queue's ownership (ozec_stripe_queue_create)
   delete q;
   return rc == OZEC_OK ? OZEC_OK : set_error(rc, "device error while draining the stripe queue");
 }

@@ -12,6 +12,9 @@ wl_name, key, vals = sys.argv[1], sys.argv[2].encode(), [int(v) for v in sys.arg
 rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 5
 torch.cuda.set_device(0)
 lib = L.lib()
+for kv in filter(None, os.environ.get("FIX", "").split(",")):  # knobs held fixed for every variant (FIX=k=v,k=v)
+    fk, fv = kv.split("=")
+    assert lib.ozec_set_tuning(fk.encode(), int(fv)) == 0, kv
 wl = bench.Workload(wl_name, 0, 1, None)
 if os.environ.get("ZERO"):  # all-zero data cells: separates data-dependent power/clock effects
     for name in ("units", "data", "blocks"):
@@ -46,5 +49,5 @@ for _ in range(rounds):
         times[v].append(a.elapsed_time(b) / 3)
 for v in sorted(vals, key=lambda v: np.median(times[v])):
     med = float(np.median(times[v]))
-    print(json.dumps({"wl": wl_name, key.decode(): v, "median_ms": round(med, 3),
+    print(json.dumps({"wl": wl_name, "fix": os.environ.get("FIX", ""), key.decode(): v, "median_ms": round(med, 3),
                       "frac": round(wl.alg_bytes / (med * 1e-3) / 8e12, 4)}), flush=True)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 3: parity of the persistent work-queue nibble variants (100-105), then same-process A/Bs on C3r / C5dev.
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
+export PYTHONPATH=$PWD:$PWD/tests/golden
+O=gpurun_out/r3dyn; mkdir -p $O
+if [ -z "$NOTEST" ]; then
+timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_next.py -k "${TESTK:-work_queue or 10[0-9] or 11[01]}" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+fi
+timeout -k 10 300 python -u scripts/ab.py c3r crc_variant ${C3R:-0,100,101,102,104} ${ROUNDS:-5} > $O/ab_c3r.log 2>&1 || { tail $O/ab_c3r.log; exit 1; }
+timeout -k 10 300 python -u scripts/ab.py c5dev crc_variant ${C5:-0,100,101,103,104,105} ${ROUNDS:-5} > $O/ab_c5dev.log 2>&1 || { tail $O/ab_c5dev.log; exit 1; }
+grep '"wl"' $O/ab_c3r.log $O/ab_c5dev.log

@@ -50,10 +50,12 @@ def _worker(rank, world, port, S, k, p, n, q):
     gathered = [None] * world
     dist.all_gather_object(gathered, digests)
     slowest = max_over_ranks(1.0 + rank, dist)
+    import bench
+    per_rank = bench.gather_per_rank({"elapsed_s": 1.0 + rank, "numa_node": rank % 2, "stripes": hi - lo}, dist)
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:
-        q.put((gathered, slowest))
+        q.put((gathered, slowest, per_rank))
 
 
 def test_two_rank_gloo_sharded_encode():
@@ -64,7 +66,7 @@ def test_two_rank_gloo_sharded_encode():
     procs = [ctx.Process(target=_worker, args=(r, world, port, S, k, p, n, q)) for r in range(world)]
     for pr in procs:
         pr.start()
-    gathered, slowest = q.get(timeout=120)
+    gathered, slowest, per_rank = q.get(timeout=120)
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
@@ -79,6 +81,26 @@ def test_two_rank_gloo_sharded_encode():
         par = oracle.rs_encode(k, p, cells(SEED, s * k, k, n))
         assert merged[s] == int(np.bitwise_xor.reduce(np.concatenate(par).view(np.uint64)))
     assert slowest == 2.0
+    # bench.py's per-rank arrays beside the max: rank order, one entry per rank
+    assert per_rank == {"elapsed_s": [1.0, 2.0], "numa_node": [0, 1],
+                        "stripes": [hi - lo for lo, hi in (stripe_range(S, r, world) for r in range(world))]}
+
+
+def test_launch_workers_environment_and_argv():
+    """bench.py --gpus N without torchrun: N children with the same argv, torchrun's variables for their rank, a
+    rendezvous on 127.0.0.1, only rank 0's stdout kept (the one JSON line)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    argv = ["--gpus", "4", "--steps", "5", "--workload", "c2"]
+    specs = bench.worker_specs(4, argv, {"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}, 29555)
+    assert len(specs) == 4
+    for r, (cmd, env, keep) in enumerate(specs):
+        assert cmd[0] == sys.executable and cmd[1] == "-u" and cmd[2].endswith("bench.py") and cmd[3:] == argv
+        assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"], env["LOCAL_WORLD_SIZE"]) == (str(r), str(r), "4", "4")
+        assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29555"
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["PATH"] == "/usr/bin"  # the caller's env is kept
+        assert keep == (r == 0)
 
 
 def test_bench_stdout_holds_only_the_json_line():

@@ -96,6 +96,60 @@ def test_host_batch_strided_units_and_big_endian():
     assert (v[:, :, n:] == 0xA5).all()  # the gaps are untouched
 
 
+def test_release_staging_between_host_batches():
+    """ozec_release_staging gives the host-batch ring (device chunk buffers, pinned staging) and the idle slots'
+    buffers back (they only ever grew); the next calls allocate again and stay bit-exact."""
+    from ozone_amd import _lib as L
+    k, p, n, S, bpc = 6, 3, 1 << 16, 9, 16384
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    for rep in range(3):
+        buf, v, us = _batch(S, k, p, n, 815000 + rep * 100)
+        crcs = np.zeros(S * (k + p) * (n // bpc), np.uint32)
+        base = v.ctypes.data
+        e.encode_crc_host_batch(base, (k + p) * us, us, base + k * us, (k + p) * us, us, S, n, ck.ChecksumType.CRC32C,
+                                bpc, crcs, False, 4)  # pageable: staged through the ring's pinned buffers
+        _check(v, crcs, "rs", k, p, n, S, ck.ChecksumType.CRC32C, bpc)
+        d = cells(SEED, 815500 + rep, k, 5000)
+        par = [np.zeros(5000, np.uint8) for _ in range(p)]
+        e.encode(d, par)  # a host-buffer call through a staging slot
+        assert all((a == b).all() for a, b in zip(par, oracle.rs_encode(k, p, d)))
+        assert L.lib().ozec_release_staging() == 0
+
+
+def test_host_register_pins_when_placement_is_refused(tmp_path):
+    """ozec_host_register places pages best effort (it used to fail outright when mbind was refused, as
+    under a seccomp profile without CAP_SYS_NICE): with mbind failing (test hook) the memory is still pinned, a host
+    batch over it is bit-exact, and the refusal is counted."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"""
+import sys; sys.path[:0] = [{root!r}, {os.path.join(root, 'tests')!r}, {os.path.join(root, 'tests', 'golden')!r}]
+import numpy as np, torch
+torch.cuda.set_device(0)
+from ozone_amd import _lib as L, checksum as ck, rawcoder as rc
+from ozone_amd.stripe_queue import host_register, host_unregister
+import test_gpu_e2e as t
+k, p, n, S, bpc = 6, 3, 1 << 15, 5, 8192
+buf, v, us = t._batch(S, k, p, n, 816000)
+crcs = np.zeros(S * (k + p) * (n // bpc), np.uint32)
+before = L.lib().ozec_host_placement_failures()
+host_register(buf.ctypes.data, buf.nbytes, 0)
+host_register(crcs.ctypes.data, crcs.nbytes, 0)
+assert L.lib().ozec_host_placement_failures() == before + 2
+e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+base = v.ctypes.data
+e.encode_crc_host_batch(base, (k + p) * us, us, base + k * us, (k + p) * us, us, S, n, ck.ChecksumType.CRC32C, bpc,
+                        crcs, False, 2)
+t._check(v, crcs, "rs", k, p, n, S, ck.ChecksumType.CRC32C, bpc)
+host_unregister(buf.ctypes.data); host_unregister(crcs.ctypes.data)
+print("ok")
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, OZEC_TEST_FAIL_MBIND="1"))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
 def test_host_batch_errors():
     e = rc.RawErasureEncoder(rc.ECReplicationConfig(6, 3))
     buf = np.zeros(9 * 4096, np.uint8)

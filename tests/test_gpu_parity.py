@@ -380,7 +380,7 @@ def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
             assert (crcs[s, u] == oracle.crc_windows(otype, units[u], bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [61, 63])
+@pytest.mark.parametrize("variant", [61, 63, 100, 101])
 @pytest.mark.parametrize("k,p,n,bpc,S", [(6, 3, 1 << 17, 16384, 3), (10, 4, 1 << 16, 4096, 2), (3, 2, 1 << 17, 8192, 3),
                                          (6, 2, 1 << 15, 32768, 2), (10, 1, 1 << 16, 16384, 2)])
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
@@ -406,8 +406,45 @@ def test_encode_crc_nibble_kernel_vs_oracle(variant, k, p, n, bpc, S, ctype, oty
             assert (crcs[s, u] == oracle.crc_windows(otype, cell, bpc)).all(), (s, u)
 
 
+@pytest.mark.parametrize("variant", [100, 101, 102, 106, 107, 108, 109])
+@pytest.mark.parametrize("grid", [1, 3, 0])
+def test_encode_crc_work_queue_any_grid_and_streams(variant, grid):
+    """The persistent nibble kernel's work queue (fused.hip WorkQueue): every (stripe, window) unit is done exactly
+    once for a grid of 1 workgroup (it drains all 8 ranges), 3 (ranges shared unevenly) and the resident set; the
+    counter slot is back at zero after each launch (five launches in a row on one stream give the same result), and
+    two streams have their own slots (concurrent launches of different batches, both vs the oracle)."""
+    lib = L.lib()
+    k, p, n, bpc, S = 6, 3, 1 << 17, 16384, 5
+    data = [np.stack([np.stack(cells(SEED, 57000 + b * 100 + s * k, k, n)) for s in range(S)]) for b in range(2)]
+    outs = [torch.full((S, p, n), 0xA5, dtype=torch.uint8, device=DEV) for _ in range(2)]
+    crcs = [torch.zeros((S, k + p, n // bpc), dtype=torch.int32, device=DEV) for _ in range(2)]
+    ins = [t(d) for d in data]
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    try:
+        assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+        assert lib.ozec_set_tuning(b"crc_grid", grid) == 0
+        for rep in range(5):
+            for b in range(2):
+                with torch.cuda.stream(streams[b]):
+                    crcs[b].zero_()
+                    e.encode_crc_batch(ins[b], k * n, n, outs[b], p * n, n, S, n, ck.ChecksumType.CRC32C, bpc, crcs[b])
+            torch.cuda.synchronize()
+            for b in range(2):
+                par, cr = h(outs[b]), h(crcs[b]).view(np.uint32)
+                for s in range(S):
+                    ref = oracle.rs_encode(k, p, list(data[b][s]))
+                    assert all((par[s, r] == ref[r]).all() for r in range(p)), (rep, b, s)
+                    for u, cell in enumerate(list(data[b][s]) + ref):
+                        assert (cr[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (rep, b, s, u)
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+        lib.ozec_set_tuning(b"crc_grid", 0)
+
+
 @pytest.mark.parametrize("variant", [11, 12, 13, 14, 15, 16, 17, 49, 51, 52, 53, 54, 55, 56, 57, 58,
-                                     61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 86, 87, 88, 89, 93, 94, 95])
+                                     61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 86, 87, 88, 89, 93, 94, 95,
+                                     100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, 111])
 @pytest.mark.parametrize("n,bpc,S", [(1 << 18, 16384, 3), (50000, 4096, 2), (1 << 17, 4096, 2), (1 << 17, 65536, 3)])
 def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
     """Every tuning variant of the rs-6-3 fused encode + CRC32C kernel (per-window kernel: D = 4, prefetch, table
@@ -435,7 +472,8 @@ def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
             assert (crcs[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [0, 11, 17, 49, 51, 54, 55, 57, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 86, 87, 88, 89, 93, 94, 95])
+@pytest.mark.parametrize("variant", [0, 11, 17, 49, 51, 54, 55, 57, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 86, 87, 88, 89, 93, 94, 95,
+                                     100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, 111])
 @pytest.mark.parametrize("k,p", [(10, 4), (6, 2), (3, 2), (10, 3), (10, 2), (10, 1)])
 def test_encode_crc_other_shapes_variants_vs_oracle(variant, k, p):
     """Fused encode + CRC32C variants of the other RS shapes (D = 2 default, D = 4, D = 4 with fenced halves)."""

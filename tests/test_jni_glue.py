@@ -51,9 +51,16 @@ def J():
         (P + "checksumWindowsArray", i32, [vp, vp, i32, vp, i32, i32, i32, vp]),
         (P + "allocatePinned", vp, [vp, vp, i32]), (P + "freePinned", None, [vp, vp, vp]),
         (P + "queueCreate", i64, [vp, vp, i64, i32, i32, i32, i32]),
-        (P + "queueSubmit", i64, [vp, vp, i64, vp, vp, vp, vp, i32, vp]),
+        (P + "queueSubmit", i64, [vp, vp, i64, vp, vp, vp, vp, i32, vp, i32]),
         (P + "queueWait", None, [vp, vp, i64, i64]), (P + "queueFree", None, [vp, vp, i64]),
-        (P + "reconstructHostBatch", None, [vp, vp, i64, vp, i64, i64, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp])]:
+        (P + "reconstructHostBatch", None, [vp, vp, i64, vp, i64, i64, vp, vp, vp, i32, i32, i32, i32, vp, vp, vp]),
+        (P + "crcMonomial", i32, [vp, vp, i32, i64]), (P + "crcCompose", i32, [vp, vp, i32, i32, i32, i64]),
+        (P + "composerCreate", i64, [vp, vp, i32, i64, i64]), (P + "composerUpdate", None, [vp, vp, i64, i32, i64]),
+        (P + "composerUpdateBytes", None, [vp, vp, i64, vp, i32, i32, i64]),
+        (P + "composerPending", i32, [vp, vp, i64]), (P + "composerDigest", i32, [vp, vp, i64, vp]),
+        (P + "composerFree", None, [vp, vp, i64]),
+        (P + "composeWindowsBatch", None, [vp, vp, i32, i64, i64, i64, i64, i64, i64, ctypes.c_uint8, i64,
+                                           ctypes.c_uint8, i64])]:
         fn = getattr(L, name)
         fn.restype, fn.argtypes = res, args
     L.env = L.mock_env()
@@ -172,6 +179,96 @@ def test_no_device_makes_the_factory_throw(J, java):
     assert cls == "java/io/IOException" and "no HIP device" in msg
 
 
+def _s32(v):
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
+@pytest.mark.parametrize("ctype", [2, 3])
+def test_crcutil_natives_vs_oracle(J, java, ctype):
+    """HipCrcUtil's natives (CrcUtil.getMonomial / compose, OC/CrcUtil.java:74-127) vs the oracle; a negative length
+    raises the reference's IllegalArgumentException, a non-CRC type its IOException."""
+    ot = oracle.CRC32 if ctype == 2 else oracle.CRC32C
+    r = np.random.default_rng(ctype)
+    for n in (0, 1, 16, 4096, 16384, 1 << 20, (1 << 40) + 7):
+        assert call(J, "crcMonomial", ctype, n) & 0xFFFFFFFF == oracle.crc_monomial(ot, n)
+    for _ in range(100):
+        a, b = (int(x) for x in r.integers(0, 1 << 32, 2, dtype=np.uint64))
+        n = int(r.integers(0, 1 << 33))
+        assert call(J, "crcCompose", ctype, _s32(a), _s32(b), n) & 0xFFFFFFFF == oracle.crc_compose(ot, a, b, n)
+    assert java.exception() is None
+    call(J, "crcMonomial", ctype, -1)
+    assert java.exception() == ("java/lang/IllegalArgumentException", "lengthBytes must be positive, got -1")
+    call(J, "crcCompose", ctype, 1, 2, -3)
+    assert java.exception()[0] == "java/lang/IllegalArgumentException"
+    call(J, "crcMonomial", 4, 16)  # SHA256
+    assert java.exception() == ("java/io/IOException", "No CRC polynomial could be associated with type: 4")
+
+
+@pytest.mark.parametrize("ctype", [2, 3])
+@pytest.mark.parametrize("hint,stripe", [(4096, (1 << 63) - 1), (4096, 16384), (512, 1536)])
+def test_crc_composer_natives_vs_oracle(J, java, ctype, hint, stripe):
+    """HipCrcComposer's natives (CrcComposer, OC/CrcComposer.java:44-215): update(int, long) and update(byte[], ...)
+    interleaved, digests of partial and whole stripes, vs the oracle's CrcComposer."""
+    ot = oracle.CRC32 if ctype == 2 else oracle.CRC32C
+    r = np.random.default_rng(hint + ctype)
+    c = call(J, "composerCreate", ctype, hint, stripe)
+    assert java.exception() is None and c
+    ref = oracle.Composer(ot, hint, stripe)
+    try:
+        for step in range(120):
+            crcs = r.integers(0, 1 << 32, int(r.integers(1, 5)), dtype=np.uint64)
+            crcs[0] = 0 if step % 17 == 0 else crcs[0]  # the cur == 0 shortcut
+            if step % 2:
+                for v in crcs:
+                    call(J, "composerUpdate", c, _s32(int(v)), hint)
+            else:
+                be = crcs.astype(">u4").view(np.uint8)
+                buf = np.concatenate([np.zeros(3, np.uint8), be])
+                call(J, "composerUpdateBytes", c, java.bytes(buf), 3, be.size, hint)
+            for v in crcs:
+                ref.update(int(v), hint)
+            assert java.exception() is None
+            if step % 25 == 0:
+                out = np.zeros(call(J, "composerPending", c), np.uint8)
+                assert call(J, "composerDigest", c, java.bytes(out)) == out.size
+                assert out.tobytes() == ref.digest()
+        out = np.zeros(call(J, "composerPending", c) + 8, np.uint8)
+        n = call(J, "composerDigest", c, java.bytes(out))
+        assert out[:n].tobytes() == ref.digest() and n > 0
+        assert call(J, "composerPending", c) == 0
+    finally:
+        call(J, "composerFree", c)
+
+
+def test_crc_composer_natives_raise_the_reference_exceptions(J, java):
+    c = call(J, "composerCreate", 3, 4, 10)
+    try:
+        call(J, "composerUpdate", c, 5, 4)
+        call(J, "composerUpdate", c, 6, 4)
+        assert java.exception() is None
+        call(J, "composerUpdate", c, 7, 4)  # position 12 passes the 10-byte stripe
+        ex = java.exception()
+        assert ex[0] == "java/io/IOException" and "without stripe alignment" in ex[1]
+        call(J, "composerUpdateBytes", c, java.bytes(np.zeros(8, np.uint8)), 0, 6, 4)
+        ex = java.exception()
+        assert ex == ("java/io/IOException", "Trying to update CRC from byte array with length '6' at offset '0' "
+                                             "which is not a multiple of 4!")
+        call(J, "composerUpdateBytes", c, java.bytes(np.zeros(8, np.uint8)), 6, 4, 4)
+        assert java.exception()[0] == "java/lang/ArrayIndexOutOfBoundsException"
+        call(J, "composerUpdate", c, 1, -4)
+        assert java.exception()[0] == "java/lang/IllegalArgumentException"
+        call(J, "composerDigest", c, java.bytes(np.zeros(0, np.uint8)))  # pending bytes do not fit
+        assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"
+    finally:
+        call(J, "composerFree", c)
+    assert call(J, "composerCreate", 5, 4, 0) == 0  # MD5
+    assert java.exception()[0] == "java/io/IOException"
+    assert call(J, "composerCreate", 3, -1, 0) == 0
+    assert java.exception()[0] == "java/lang/IllegalArgumentException"
+    call(J, "composerUpdate", 0, 1, 4)
+    assert java.exception() == ("java/io/IOException", "CrcComposer closed")
+
+
 # ------------------------------------------------------------------------------------------ GPU
 
 
@@ -239,6 +336,27 @@ def test_checksums_and_streaming_update_vs_oracle(J, java):
 
 
 @pytest.mark.gpu
+def test_compose_windows_batch_through_jni(J, java):
+    """composeWindowsBatch on device pointers (a GPU pipeline's window CRCs): the composite CRC of every cell equals
+    the CRC of the whole cell."""
+    import torch
+    n, bpc, C = 100_000, 4096, 5
+    nwin = (n + bpc - 1) // bpc
+    data = np.stack(cells(SEED, 747000, C, n))
+    win = np.stack([oracle.crc_windows(oracle.CRC32C, data[c], bpc) for c in range(C)]).astype(np.uint32)
+    d_win = torch.from_numpy(win.view(np.int32)).cuda()
+    d_out = torch.zeros(C, dtype=torch.int32, device="cuda")
+    call(J, "composeWindowsBatch", 3, d_win.data_ptr(), nwin, C, nwin, bpc, n - (nwin - 1) * bpc, 0, d_out.data_ptr(),
+         0, 0)
+    assert java.exception() is None
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(np.uint32)
+    assert [int(v) for v in got] == [oracle.crc_windows(oracle.CRC32C, data[c], n)[0] for c in range(C)]
+    call(J, "composeWindowsBatch", 3, d_win.data_ptr(), nwin, -1, nwin, bpc, 1, 0, d_out.data_ptr(), 0, 0)
+    assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"
+
+
+@pytest.mark.gpu
 def test_pinned_buffers_and_stripe_queue_through_jni(J, java):
     k, p, n, bpc = 6, 3, 1 << 15, 8192
     h = call(J, "coderCreate", 0, 0, k, p)
@@ -257,7 +375,7 @@ def test_pinned_buffers_and_stripe_queue_through_jni(J, java):
             cells_d = java.array([pb] * k)
             cells_p = java.array([pb] * p)
             t = call(J, "queueSubmit", q, cells_d, java.ints([j * n for j in range(k)]), cells_p,
-                     java.ints([(k + r) * n for r in range(p)]), n, java.direct(crcs.view(np.uint8)))
+                     java.ints([(k + r) * n for r in range(p)]), n, java.direct(crcs.view(np.uint8)), 0)
             assert java.exception() is None
             jobs.append((t, view, crcs))
         call(J, "queueWait", q, jobs[-1][0])
@@ -274,6 +392,60 @@ def test_pinned_buffers_and_stripe_queue_through_jni(J, java):
             call(J, "freePinned", pb)
             J.mock_free(pb)
         call(J, "coderRelease", h)
+    assert java.exception() is None
+
+
+@pytest.mark.gpu
+def test_stripe_queue_submit_checks_and_encoder_lifetime(J, java):
+    """queueSubmit checks the cell counts against the queue and the CRC buffer's room from its position (the
+    native side writes (k + p) * windows ints there); a queue keeps its encoder's native handle alive, so releasing
+    the encoder first makes submits fail with the reference's "closed" IOException and queueFree stays safe
+    (HipStripeQueue.java:32 / ozec_jni.c:372)."""
+    k, p, n, bpc = 6, 3, 1 << 14, 4096
+    nwin = n // bpc
+    cells_ = [np.asarray(x) for x in cells(SEED, 746000, k, n)]
+    par = [np.zeros(n, np.uint8) for _ in range(p)]
+    h = call(J, "coderCreate", 0, 0, k, p)
+    q = call(J, "queueCreate", h, n, 4, 3, bpc)
+    assert java.exception() is None and q
+
+    def submit(nd=k, np_=p, crc=None, crc_off=0, length=n):
+        return call(J, "queueSubmit", q, java.array([java.direct(x) for x in cells_[:nd]]), java.ints([0] * nd),
+                    java.array([java.direct(x) for x in par[:np_]] + [java.direct(par[0])] * (np_ - p)),
+                    java.ints([0] * np_), length, None if crc is None else java.direct(crc), crc_off)
+    try:
+        submit(nd=5)
+        ex = java.exception()
+        assert ex[0] == "org/apache/hadoop/HadoopIllegalArgumentException" and "Invalid inputs/outputs length" in ex[1]
+        submit(np_=4)
+        assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"
+        small = np.zeros((k + p) * nwin * 4 - 4, np.uint8)          # one CRC short
+        submit(crc=small)
+        ex = java.exception()
+        assert ex[0] == "org/apache/hadoop/HadoopIllegalArgumentException" and "too small" in ex[1]
+        roomy = np.zeros((k + p) * nwin * 4 + 64, np.uint8)
+        submit(crc=roomy, crc_off=68)                                # the position leaves 60 bytes short
+        assert "too small" in java.exception()[1]
+        submit(length=n + 1)
+        assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"
+        t = submit(crc=roomy, crc_off=64)
+        assert java.exception() is None
+        call(J, "queueWait", q, t)
+        assert java.exception() is None
+        crcs = roomy[64:].view(">u4")
+        ref = oracle.rs_encode(k, p, cells_)
+        assert all((par[r] == ref[r]).all() for r in range(p))
+        exp = np.concatenate([oracle.crc_windows(oracle.CRC32C, u, bpc) for u in cells_ + ref])
+        assert (crcs == exp).all() and not roomy[:64].any()
+        call(J, "coderRelease", h)                                   # encoder released while the queue lives
+        h = 0
+        submit(crc=roomy, crc_off=64)
+        ex = java.exception()
+        assert ex[0] == "java/io/IOException" and "closed" in ex[1]
+    finally:
+        call(J, "queueFree", q)
+        if h:
+            call(J, "coderRelease", h)
     assert java.exception() is None
 
 
@@ -330,6 +502,14 @@ def test_reconstruct_batch_through_jni(J, java):
         call(J, "reconstructHostBatch", h, sb, (k + p) * n, n, java.ints(present[:9]), java.ints(erased + [0]), ob, S,
              n, 3, bpc, eb, cb, mb)
         assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"  # 5 erased of 4 parity
+        for stride in (1 << 62, (1 << 63) - 1):  # strides whose layout size wraps int64: rejected, nothing read
+            call(J, "reconstructHostBatch", h, sb, stride, n, java.ints(present), java.ints(erased), ob, S, n, 3, bpc,
+                 eb, cb, mb)
+            ex = java.exception()
+            assert ex[0] == "org/apache/hadoop/HadoopIllegalArgumentException" and "overflows" in ex[1], stride
+        call(J, "reconstructHostBatch", h, sb, (k + p) * n, 1 << 61, java.ints(present), java.ints(erased), ob, S, n,
+             3, bpc, eb, cb, mb)
+        assert "overflows" in java.exception()[1]
         stripes[:, erased] = 0
         stripes[3, 12, 5] ^= 0x80                 # stripe 3: the last unit read is corrupted in window 0
         call(J, "reconstructHostBatch", h, sb, (k + p) * n, n, java.ints(present), java.ints(erased), ob, S, n, 3, bpc,

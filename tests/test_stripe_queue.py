@@ -264,3 +264,35 @@ def test_queue_rejects_buffers_it_cannot_dma():
         q.wait(q.submit(d, par, crcs=crcs))
     ref = oracle.rs_encode(k, p, d)
     assert all((a == b).all() for a, b in zip(par, ref))
+
+
+def test_queue_outlives_its_encoder_handle():
+    """The C ABI queue co-owns its encoder (ozec_coder_retain; ADVICE r2: the Java HipStripeQueue kept a raw handle
+    that AbstractHipRawEncoder.release() freed): with the encoder released and freed by its creator, a submit fails
+    with OZEC_ECLOSED and freeing the queue -- pending stripes included -- touches no freed memory."""
+    import ctypes
+    from ozone_amd import _lib as L
+    lib = L.lib()
+    k, p, n = 6, 3, 8192
+    h = ctypes.c_void_p()
+    assert lib.ozec_encoder_create(0, k, p, ctypes.byref(h)) == 0
+    q = ctypes.c_void_p()
+    assert lib.ozec_stripe_queue_create(h, n, 4, 3, 4096, 0, ctypes.byref(q)) == 0
+    kk, pp, rows, ct = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    cl, bpc = ctypes.c_size_t(), ctypes.c_size_t()
+    assert lib.ozec_stripe_queue_info(q, ctypes.byref(kk), ctypes.byref(pp), ctypes.byref(rows), ctypes.byref(cl),
+                                      ctypes.byref(ct), ctypes.byref(bpc)) == 0
+    assert (kk.value, pp.value, rows.value, cl.value, ct.value, bpc.value) == (k, p, p, n, 3, 4096)
+    d = cells(SEED, 93000, k, n)
+    par = [np.zeros(n, np.uint8) for _ in range(p)]
+    crcs = np.zeros((k + p) * 2, np.uint32)
+    dp = (ctypes.c_void_p * k)(*[x.ctypes.data for x in d])
+    pq = (ctypes.c_void_p * p)(*[x.ctypes.data for x in par])
+    t = ctypes.c_uint64()
+    assert lib.ozec_stripe_queue_submit(q, dp, pq, n, crcs.ctypes.data, ctypes.byref(t)) == 0  # pending in the queue
+    assert lib.ozec_coder_release(h) == 0
+    lib.ozec_coder_free(h)  # the creator's reference: the queue's keeps the memory
+    assert lib.ozec_stripe_queue_submit(q, dp, pq, n, crcs.ctypes.data, ctypes.byref(t)) == L.OZEC_ECLOSED
+    assert "closed" in L.last_error()
+    rc_ = lib.ozec_stripe_queue_free(q)  # drains: the pending batch cannot launch on a closed coder
+    assert rc_ in (0, L.OZEC_ECLOSED, L.OZEC_EDEVICE)

@@ -69,6 +69,7 @@ def parse(argv=None):
     ap.add_argument("--e2e-steps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0, help="C5: stripes per pipelined chunk (0 = library default)")
     ap.add_argument("--threads", type=int, default=1, help="host workload: caller threads sharing one coder")
+    ap.add_argument("--queue-batch", type=int, default=32, help="queue workloads: stripes per GPU batch")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="ozec_set_tuning knob (A/B and profiling runs only; defaults are the measured best)")
     return ap.parse_args(argv)
@@ -166,7 +167,7 @@ def host_info():
 class Workload:
     """Allocates device-resident inputs once; step() launches one batch on the current stream."""
 
-    def __init__(self, name, rank, world, stripes_override, threads=1, erased=(0, 1, 2, 3)):
+    def __init__(self, name, rank, world, stripes_override, threads=1, erased=(0, 1, 2, 3), queue_batch=32):
         from ozone_amd import checksum as ck
         from ozone_amd import rawcoder as rc
         from ozone_amd.shard import stripe_range
@@ -264,9 +265,10 @@ class Workload:
                 self._pool.append(pb)
                 return pb.array.view(dtype)
             rng = np.random.default_rng(rank)
-            # one buffer per stripe with its k data then p parity cells back to back (the layout a writer's
-            # pinned cell pool would use); the queue then moves a stripe in one H2D and one D2H copy
-            slabs = [buf((k + p) * n) for _ in range(pool)]
+            # a writer's cell pool: one allocation carved into per-stripe slabs of k data then p parity cells back to
+            # back; stripes submitted in pool order coalesce into one 2D copy per direction and run of 8 stripes
+            whole = buf(pool * (k + p) * n)
+            slabs = [whole[i * (k + p) * n:(i + 1) * (k + p) * n] for i in range(pool)]
             self.qd = [[sl[j * n:(j + 1) * n] for j in range(k)] for sl in slabs]
             for st in self.qd:
                 for a in st:
@@ -274,14 +276,14 @@ class Workload:
             self.qp = [[sl[(k + r) * n:(k + r + 1) * n] for r in range(p)] for sl in slabs]
             self.qc = [buf((k + p) * nwin * 4, np.uint32) for _ in range(pool)]
             enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
-            self.q = StripeQueue(enc, n, 64, self.crc_type, self.bpc)
+            self.q = StripeQueue(enc, n, queue_batch, self.crc_type, self.bpc)
             self.k, self.p, self.S = k, p, S
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + p) * n
-            self.kernel = "encode_crc_nb<6,3> via ozec_stripe_queue (+H2D/D2H per cell)"
+            self.kernel = "encode_crc_nb<6,3> via ozec_stripe_queue (+H2D/D2H 2D copies per run of stripes)"
             self.config = {"workload": f"rs-6-3-1024k + CRC32C/16 KiB through the stripe queue (SURVEY 8(f) row 3) "
                                        f"from {'pinned' if pinned else 'pageable'} host cells, {S} stripes, "
-                                       f"batches of 64", "stripes": S}
+                                       f"batches of {queue_batch}", "stripes": S, "stripes_per_batch": queue_batch}
 
             def step():
                 t = 0
@@ -975,7 +977,7 @@ def main():
                   "calls": stream_latency(args)})
         return 0
 
-    wl = Workload(args.workload, rank, world, args.stripes, args.threads, erased)
+    wl = Workload(args.workload, rank, world, args.stripes, args.threads, erased, args.queue_batch)
 
     def barrier():
         if dist is not None:

@@ -370,7 +370,8 @@ __device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t 
 // quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree;
 // DYN: 0 one wave per unit, no grid-stride; persistent grid (one resident set of workgroups, tables built once per
 // workgroup) fed by the WorkQueue with 1 a claim per unit, made one unit ahead, 3 guided claims of up to 8 units, 4 a
-// claim per unit made when it is needed; 2 persistent grid with the static grid-stride order
+// claim per unit made when it is needed; 2 persistent grid with the static grid-stride order, 5 the same with the
+// waves' starts staggered by up to one window (a probe: do waves in lockstep on the same step offsets contend?)
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
@@ -422,6 +423,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   constexpr bool kQueue = DYN == 1 || DYN == 3 || DYN == 4;
   WorkQueue wq{e.work, units, static_cast<int>(blockIdx.x & 7), 0, 0, 0, 0, static_cast<int32_t>(gridDim.x * WPB / 8)};
   int64_t u = kQueue ? wq.next(lane, DYN == 3) : bid * WPB + wave;
+  if constexpr (DYN == 5) {
+    const int n = static_cast<int>((blockIdx.x * WPB + wave) % 16) * 3;  // ~4 us per s_sleep 127 at 2 GHz
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   while (u < units) {
     // DYN 1 / 3: the next unit is claimed before this one is worked on, so the atomic's round trip overlaps the work
     const int64_t u_next = DYN == 1 || DYN == 3 ? wq.next(lane, DYN == 3) : u + static_cast<int64_t>(gridDim.x) * WPB;
@@ -652,6 +657,25 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 109: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 3>(e, st);
     case 110: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 3>(e, st);
     case 111: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 2>(e, st);
+    // deeper input rings: the loads of a whole step (K blocks) in flight ahead of the lookups
+    // probe: the round-2 rs-10-x default with one occupancy query of its kernel first (does the query change how the
+    // kernel runs?)
+    case 115: {
+      static bool asked = false;
+      if (!asked) {
+        int per_cu = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_crc_nb<K, R, 1, kNB, 8, 4>, 8 * 64, 0);
+        asked = true;
+      }
+      return launch_nb<K, R, 1, kNB, 8, 4>(e, st);
+    }
+    case 120: return launch_nb<K, R, 1, K, 8, 4>(e, st);
+    case 121: return launch_nb<K, R, kD2, K, 12, 4>(e, st);
+    case 122: return launch_nb<K, R, kD2, K, 8, 4>(e, st);
+    case 123: return launch_nb<K, R, 1, K, 8, 5>(e, st);
+    case 112: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 5>(e, st);
+    case 113: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 5>(e, st);
+    case 114: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 5>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);
@@ -674,7 +698,7 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // two-step groups in 12-wave workgroups (87: C5dev 66.9 %; encode_crc_lv 57.9 %); 56 / 59 pin the streamed-input
   // kernel's defaults
   if (v == 0) v = k == 10 ? 62 : 87;
-  if (v >= 60 && v < 120) {
+  if (v >= 60 && v < 130) {
     if (k == 6 && r == 3) return launch_nb_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_nb_kr<6, 2>(e, st, v);
     if (k == 3 && r == 2) return launch_nb_kr<3, 2>(e, st, v);

@@ -334,8 +334,9 @@ void ozec_stats_reset(void);
 
 /* ---- harness utilities ------------------------------------------------------------------------------- */
 /* process-wide tuning knobs for benchmarking: kernels ("grid", "gf_variant", "crc_variant", "crc_grid",
- * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_slots",
- * "copy_threads" = helper threads for pageable <-> pinned copies, 0 = copy on the calling thread) */
+ * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_chunk_shared"
+ * the same while other host-buffer calls are in flight (0: always host_chunk), "host_slots", "copy_threads" =
+ * helper threads for pageable <-> pinned copies, 0 = copy on the calling thread) */
 int ozec_set_tuning(const char *key, int64_t value);
 /* fill n bytes with splitmix64 stream `stream_id` of `seed` (tests/golden/synth.py is the CPU twin) */
 int ozec_fill_splitmix64(uint8_t *d_dst, size_t n, uint64_t seed, uint64_t stream_id, void *stream);

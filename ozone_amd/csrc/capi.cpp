@@ -133,6 +133,7 @@ struct DevCtx {
   std::condition_variable pool_cv;
   std::vector<std::unique_ptr<Slot>> slots;
   std::vector<Slot *> free_slots;
+  std::atomic<int> leased{0};       // slots leased to calls in flight
   uint32_t *crc_tables[2][3] = {};  // [type][B = 1, 2, 4]
   uint32_t *g26_tables[2][ozec::kG26Slots] = {};  // [type][kG26Cfg slot]
   uint32_t *nib_tables[2] = {};                   // [type]
@@ -150,6 +151,7 @@ struct DevCtx {
     }
     *out = free_slots.back();
     free_slots.pop_back();
+    ++leased;
     return OZEC_OK;
   }
 
@@ -157,6 +159,7 @@ struct DevCtx {
     {
       std::lock_guard<std::mutex> lk(pool_mu);
       free_slots.push_back(s);
+      --leased;
     }
     pool_cv.notify_one();
   }
@@ -348,16 +351,22 @@ template <class Launch, class OutBytes, class OutPos>
 int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, size_t gran, int nout,
                     uint8_t *const *out, OutBytes out_bytes, OutPos out_pos, Launch launch) {
   constexpr size_t kMaxChunks = 64;
-  size_t chunk = static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.host_chunk));
+  SlotLease lease(ctx);
+  if (int rc = ctx->acquire(&lease.slot)) return rc;
+  Slot *s = lease.slot;
+  // Chunk size: every chunk costs ~20 us of stream-operation latency, so a lone caller does best with few large
+  // chunks (host_chunk, 4 MiB per unit: one chunk for 1 MiB cells); with other calls in flight the link and the
+  // staging copies are shared, and overlapping the copies of one call's chunks pays (host_chunk_shared, 512 KiB:
+  // measured at T = 4 / 16 callers)
+  int64_t want = ozec::g_tune.host_chunk;
+  if (ctx->leased.load() > 1 && ozec::g_tune.host_chunk_shared > 0) want = std::min(want, ozec::g_tune.host_chunk_shared);
+  size_t chunk = static_cast<size_t>(std::max<int64_t>(1, want));
   chunk = std::max(chunk, (len + kMaxChunks - 1) / kMaxChunks);
   chunk = std::max(gran, chunk / gran * gran);
   if (chunk >= len) chunk = len;
   const size_t nch = (len + chunk - 1) / chunk;
   const size_t cp = round_up(chunk, kStageAlign), op = round_up(out_bytes(chunk), kStageAlign);
   const size_t per_chunk = nin * cp + nout * op;
-  SlotLease lease(ctx);
-  if (int rc = ctx->acquire(&lease.slot)) return rc;
-  Slot *s = lease.slot;
   // On an early error return, chunks already queued may still be copying into / out of the slot's buffers:
   // drain the slot's stream before the lease hands the slot to the next caller (declared after the lease, so
   // it runs first).
@@ -1536,6 +1545,7 @@ int ozec_set_tuning(const char *key, int64_t value) {
   else if (k == "crc_run") ozec::g_tune.crc_run = value;
   else if (k == "unit_map") ozec::g_tune.unit_map = static_cast<int>(value);
   else if (k == "host_chunk" && value > 0) ozec::g_tune.host_chunk = value;
+  else if (k == "host_chunk_shared" && value >= 0) ozec::g_tune.host_chunk_shared = value;
   else if (k == "host_slots" && value > 0) ozec::g_tune.host_slots = value;
   else if (k == "queue_batches" && value >= 0 && value <= 64) ozec::g_tune.queue_batches = value;
   else if (k == "copy_threads" && value >= 0) ozec::set_copy_threads(static_cast<int>(value));

@@ -371,16 +371,25 @@ __device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t 
 // DYN: 0 one wave per unit, no grid-stride; persistent grid (one resident set of workgroups, tables built once per
 // workgroup) fed by the WorkQueue with 1 a claim per unit, made one unit ahead, 3 guided claims of up to 8 units, 4 a
 // claim per unit made when it is needed; 2 persistent grid with the static grid-stride order, 5 the same with the
-// waves' starts staggered by up to one window (a probe: do waves in lockstep on the same step offsets contend?)
-template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0>
+// waves' starts staggered by up to one window (a probe: do waves in lockstep on the same step offsets contend?);
+// DO: steps per output-register group (a multiple of D): the R output registers are looked up with the G26 distance
+// sets of DO steps and shifted once per DO steps, the K input registers (whose distance sets live in the nibble
+// entries, K * 4 KiB per set) once per D steps
+// PADV / PADL: probes only (variants 140-147), PADV independent v_xor_b32 / PADL ds_read_b32 added per step: the
+// marginal cost of one more VALU or LDS instruction says which pipe sets the time
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
+          int PADV = 0, int PADL = 0>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
   static_assert(D <= kNibSets, "distance sets of the nibble blob");
-  static_assert((D * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
-  // one LDS block: G26 blob, then the (d, j, p) nibble tables, then the GF dwords of the setup.  Table regions
-  // past the 16-bit ds_read offset range are reached with bit 15 set in the index register (one v_or_b32)
-  constexpr uint32_t kTB = (g26_words(D) * 4 + 255) / 256 * 256;  // byte offset of the nibble tables
+  static_assert((DO * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
+  static_assert(DO % D == 0 && DO <= 4, "output groups of whole input groups; windows are multiples of 4 steps");
+  // one LDS block: G26 blob of DO sets (+ the D-step register shift when D < DO), then the (d, j, p) nibble tables,
+  // then the GF dwords of the setup.  Table regions past the 16-bit ds_read offset range are reached with bit 15 set
+  // in the index register (one v_or_b32)
+  constexpr uint32_t kShIn = DO == D ? g26_gshift(D) : g26_words(DO);  // word offset of the input-register shift
+  constexpr uint32_t kTB = ((g26_words(DO) + (DO == D ? 0 : 224)) * 4 + 255) / 256 * 256;  // nibble tables
   constexpr uint32_t kLds = kTB + K * D * 4096 + K * 32 * 4;
   static_assert(kLds <= 160 * 1024, "LDS per workgroup");
   __shared__ __attribute__((aligned(256))) uint8_t s_all[kLds];
@@ -396,7 +405,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     for (int r = 0; r < R; ++r) dw |= gf_mul_byte(a.coef[r * K + j], static_cast<uint32_t>(n) << (4 * h)) << (8 * r);
     s_gf[t] = dw;
   }
-  load_tables(s_t, cr.g26[g26_slot(1, D)], g26_words(D));
+  load_tables(s_t, cr.g26[g26_slot(1, DO)], g26_words(DO));
+  if constexpr (DO != D) load_tables(s_t + kShIn, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224);
   __syncthreads();
   for (int q = threadIdx.x; q < K * D * 512; q += blockDim.x) {
     const int t = q >> 4, n = q & 15, p = t & 31, dj = t >> 5, j = dj % K, d = dj / K;
@@ -410,7 +420,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   const int64_t nwin = cr.nwin;
   const int64_t units = a.nstripes * nwin;
   const int32_t T = static_cast<int32_t>(cr.bpc >> 10);  // steps per window
-  const int32_t G = T / D;                                // groups per window
+  const int32_t G = T / DO;                               // output groups per window
   const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
   uint32_t v4, vf0;  // index-op operands in VGPRs (VOP2/SDWA with no SGPR or literal operand issue fastest)
   asm volatile("v_mov_b32 %0, 4" : "=v"(v4));
@@ -449,9 +459,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     for (int i = 0; i + 1 < NB; ++i) ring[i] = load(vstep(i / K), i % K);
     for (int32_t g = 0; g < G; ++g) {
 #pragma unroll
-      for (int rr = 0; rr < D; ++rr) {
-        const int32_t t = g * D + rr;
-        const int d = D - 1 - rr;  // distance set of this step
+      for (int rr = 0; rr < DO; ++rr) {
+        const int32_t t = g * DO + rr;
+        const int d = D - 1 - rr % D;  // distance set of this step's inputs
+        const int dout = DO - 1 - rr;  // and outputs
         const uint32_t vcur = vstep(t), vnext = vstep(t + 1);
         uint32_t A[16];
 #pragma unroll
@@ -507,20 +518,33 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
           __attribute__((ext_vector_type(4))) unsigned int dv = {p.x, p.y, p.z, p.w};
           __builtin_amdgcn_raw_buffer_store_b128(dv, rout, vcur, static_cast<int>(a.out_off[r]), 2);
           store_data_hold(p);
-          S[K + r] ^= g26_block<true>(s_t + d * kG26Set, p);
+          S[K + r] ^= g26_block<true>(s_t + dout * kG26Set, p);
           __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (PADV > 0 || PADL > 0) {
+          uint32_t px[4] = {static_cast<uint32_t>(lane), vf0, v4, static_cast<uint32_t>(t)};
+#pragma unroll
+          for (int i = 0; i < PADV; ++i) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(px[i & 3]) : "v"(v4));
+#pragma unroll
+          for (int i = 0; i < PADL; ++i)
+            px[i & 3] ^= reinterpret_cast<volatile uint32_t *>(s_t)[(lane + 7 * i) & 31];
+          asm volatile("" ::"v"(px[0]), "v"(px[1]), "v"(px[2]), "v"(px[3]));
+        }
+        if (DO != D && rr % D == D - 1 && rr + 1 < DO) {  // input groups ending inside the output group
+#pragma unroll
+          for (int q = 0; q < K; ++q) S[q] = g5_shift(s_t + kShIn, S[q]);
         }
       }
       if (g + 1 < G) {
 #pragma unroll
-        for (int q = 0; q < K + R; ++q) S[q] = g5_shift(s_t + g26_gshift(D), S[q]);
+        for (int q = 0; q < K + R; ++q) S[q] = g5_shift(s_t + (q < K ? kShIn : g26_gshift(DO)), S[q]);
       }
     }
     const bool last = w == nwin - 1;
     const uint32_t init = last ? cr.init_last : cr.init_full;
     if constexpr (RS) {
       int q = 0;
-      const uint32_t v = g5_lane_tree_rs<K + R>(s_t + g26_tree(D) - kG5Tree, S, lane, q);
+      const uint32_t v = g5_lane_tree_rs<K + R>(s_t + g26_tree(DO) - kG5Tree, S, lane, q);
       if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
 #pragma unroll
         for (int qq = 0; qq < K + R; ++qq)
@@ -529,7 +553,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     } else {
 #pragma unroll
       for (int q = 0; q < K + R; ++q) {
-        const uint32_t v = g5_lane_tree(s_t + g26_tree(D) - kG5Tree, S[q], lane);
+        const uint32_t v = g5_lane_tree(s_t + g26_tree(DO) - kG5Tree, S[q], lane);
         if (lane == q) nb_emit<K, R>(e, s, w, q, v, init);
       }
     }
@@ -559,16 +583,17 @@ int32_t *work_slot(hipStream_t st) {
   return static_cast<int32_t *>(p);
 }
 
-template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0>
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
+          int PADV = 0, int PADL = 0>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
-  if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
+  if constexpr ((DO * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
-    constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
-    static_assert(kNB != NB && (D * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN>(e, st);
+    constexpr int kNB = (DO * K) % 2 == 0 ? 2 : (DO * K <= K + 1 ? DO * K : 1);
+    static_assert(kNB != NB && (DO * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
@@ -676,6 +701,22 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 112: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 5>(e, st);
     case 113: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 5>(e, st);
     case 114: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 5>(e, st);
+    // output registers shifted once per 2 / 4 steps (the input registers as before)
+    case 130: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 2>(e, st);
+    case 131: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 4>(e, st);
+    case 132: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, 4>(e, st);
+    case 133: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, 2>(e, st);
+    case 134: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 1, 4>(e, st);
+    case 135: return launch_nb<K, R, 1, 2, 8, 4, 2, true, 0, 4>(e, st);
+    // probes: the rs-10-x (62) and rs-6-x (87) defaults with 64 / 192 more VALU or 16 / 48 more LDS reads per step
+    case 140: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 64, 0>(e, st);
+    case 141: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 192, 0>(e, st);
+    case 142: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 16>(e, st);
+    case 143: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 48>(e, st);
+    case 144: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 64, 0>(e, st);
+    case 145: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 192, 0>(e, st);
+    case 146: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 16>(e, st);
+    case 147: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 48>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);
@@ -696,9 +737,12 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // default: the nibble-table kernel, one wave per window (same-process A/Bs on MI355X, profiles/r02/nb/): rs-10-x
   // with a ring of 5 input blocks and one-step groups (62: C3r 62.9 %; encode_crc_lv 52.5 %), rs-6-x / rs-3-x with
   // two-step groups in 12-wave workgroups (87: C5dev 66.9 %; encode_crc_lv 57.9 %); 56 / 59 pin the streamed-input
-  // kernel's defaults
-  if (v == 0) v = k == 10 ? 62 : 87;
-  if (v >= 60 && v < 130) {
+  // kernel's defaults.  Round 3: rs-10-x takes the same geometry as a persistent grid fed by the WorkQueue (102),
+  // 1-2 % faster than 62 in three same-process A/Bs on two boxes (profiles/r03/ab/); 62 where no counter slot can be had
+  if (v == 0 && k == 10)
+    v = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) && work_slot(st) != nullptr ? 102 : 62;
+  if (v == 0) v = 87;
+  if (v >= 60 && v < 150) {
     if (k == 6 && r == 3) return launch_nb_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_nb_kr<6, 2>(e, st, v);
     if (k == 3 && r == 2) return launch_nb_kr<3, 2>(e, st, v);

@@ -133,6 +133,7 @@ struct TuneKnobs {
   int unit_map = 0;       // CodeArgs::unit_map for the coding kernels
   int64_t host_chunk = 4 << 20;  // host-buffer calls: bytes per unit per pipelined chunk (per-chunk stream
                                  // latency ~20 us: 256 KiB chunks ran 16 MiB CRC updates at 2.7 GB/s, 4 MiB at 18)
+  int64_t host_chunk_shared = 512 << 10;  // the same while other host-buffer calls hold slots (0: host_chunk always)
   int64_t host_slots = 8;          // host-buffer calls: staging slots (concurrent calls) per GPU
   int64_t queue_batches = 0;       // stripe queue: batches in the ring (0 = default), read at queue creation
   int64_t e2e_chunk = 32;          // ozec_encode_crc_host_batch: stripes per pipelined chunk when the caller passes 0

@@ -30,15 +30,21 @@ def kernels(so_path):
             if r.returncode or not os.path.getsize(co):
                 continue
             notes = subprocess.run([f"{LLVM}/llvm-readobj", "--notes", co], capture_output=True, text=True).stdout
-            cur = None
+            # the metadata keys of a kernel are sorted: .group_segment_fixed_size comes before its .name (and the
+            # .args entries carry .name keys of their own), so values seen before a kernel's name are held for it
+            cur, pending = None, {}
             for ln in notes.splitlines():
                 m = re.search(r"\.(name|" + "|".join(KEYS) + r"):\s+(\S+)", ln)
                 if not m:
                     continue
                 k, v = m.groups()
                 if k == "name":
-                    cur = {"name": v}
-                    out.append(cur)
+                    if v.startswith("_Z"):
+                        cur = {"name": v, **pending}
+                        pending = {}
+                        out.append(cur)
+                elif k == "group_segment_fixed_size":
+                    pending[k] = int(v)
                 elif cur is not None:
                     cur[k] = int(v)
     return out

@@ -2,7 +2,12 @@
 
 #include "kernels.hpp"
 
+#include <utility>
+
 namespace ozec {
+
+int g26_bit(int g, int i);
+
 namespace {
 
 uint32_t mat_times(const uint32_t *mat, uint32_t v) {
@@ -14,6 +19,32 @@ uint32_t mat_times(const uint32_t *mat, uint32_t v) {
 
 void mat_square(const uint32_t *m, uint32_t *out) {
   for (int c = 0; c < 32; ++c) out[c] = mat_times(m, m[c]);
+}
+
+// inverse of the 32x32 GF(2) matrix given by its columns (Gauss-Jordan on [A | I]); the shift operators are
+// invertible because x is a unit mod P (P(0) = 1)
+void mat_invert(const uint32_t *cols, uint32_t *inv) {
+  uint32_t rows[32], id[32];  // row r of A as a bit mask over columns, and of the identity
+  for (int r = 0; r < 32; ++r) {
+    rows[r] = 0;
+    for (int c = 0; c < 32; ++c) rows[r] |= ((cols[c] >> r) & 1u) << c;
+    id[r] = 1u << r;
+  }
+  for (int c = 0; c < 32; ++c) {
+    int piv = c;
+    while (!((rows[piv] >> c) & 1u)) ++piv;  // exists: A is invertible
+    std::swap(rows[c], rows[piv]);
+    std::swap(id[c], id[piv]);
+    for (int r = 0; r < 32; ++r)
+      if (r != c && ((rows[r] >> c) & 1u)) {
+        rows[r] ^= rows[c];
+        id[r] ^= id[c];
+      }
+  }
+  for (int c = 0; c < 32; ++c) {  // column c of the inverse: bit r = id[r] bit c
+    inv[c] = 0;
+    for (int r = 0; r < 32; ++r) inv[c] |= ((id[r] >> c) & 1u) << r;
+  }
 }
 
 }  // namespace
@@ -53,6 +84,22 @@ CrcMath::CrcMath(uint32_t poly) : poly_(poly) {
           if ((n >> i) & 1) acc ^= bit[4 * p + i];
         nib_[(e * 32 + p) * 16 + n] = shift(acc, static_cast<uint64_t>(e) * 1024);
       }
+  // XO blob: the G26 block set advanced by kXoAdvance bytes, then the inverse of that advance
+  xo_.assign(kXoWords, 0);
+  for (int g = 0; g < 26; ++g)
+    for (uint32_t v = 0; v < 32; ++v) {
+      uint32_t acc = 0;
+      for (int i = 0; i < 5; ++i) {
+        const int p = g26_bit(g, i);
+        if (p >= 0 && ((v >> i) & 1)) acc ^= bit[p];
+      }
+      xo_[g * 32 + v] = shift(acc, kXoAdvance);
+    }
+  uint32_t adv[32], back[32];
+  shift_matrix(kXoAdvance, adv);
+  mat_invert(adv, back);
+  for (int g = 0; g < 7; ++g)
+    for (uint32_t v = 0; v < 32; ++v) xo_[kXoInv + g * 32 + v] = apply(back, static_cast<uint32_t>(uint64_t{v} << (5 * g)));
 }
 
 // Block bit (0..127; dword d bit k = 32d + k, i.e. byte p/8 bit p%8) that index bit i of G26 table g reads,

@@ -25,6 +25,8 @@ class CrcMath {
   const std::vector<uint32_t> &g26_tables(int slot) const { return g26_[slot]; }
   // the device nibble blob (kernels.hpp kNib*)
   const std::vector<uint32_t> &nib_tables() const { return nib_; }
+  // the device XO blob (kernels.hpp kXo*)
+  const std::vector<uint32_t> &xo_tables() const { return xo_; }
   uint32_t byte_table(int v) const { return t0_[v]; }
   uint32_t poly() const { return poly_; }
   // x^(8n) mod P in CrcUtil's reversed representation (CrcUtil.getMonomial)
@@ -49,6 +51,7 @@ class CrcMath {
   std::vector<uint32_t> blob_b1_, blob_b2_, blob_b4_;
   std::vector<uint32_t> g26_[kG26Slots];
   std::vector<uint32_t> nib_;
+  std::vector<uint32_t> xo_;
   std::vector<uint32_t> build_blob(int B) const;
   std::vector<uint32_t> build_g26(int B, int D) const;
 };

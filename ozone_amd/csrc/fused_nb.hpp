@@ -1,0 +1,515 @@
+// Nibble-table fused kernel (encode_crc_nb) and its launcher, instantiated per (K, R) shape in its own translation
+// unit (fused_nb_<K>_<R>.hip) so the variants of the seven shapes compile in parallel; fused.hip dispatches.
+#pragma once
+#include <algorithm>
+
+#include "device.hpp"
+
+namespace ozec {
+
+// Counter slot of the persistent kernel's WorkQueue for launches on `st` (fused.hip)
+int32_t *nb_work_slot(hipStream_t st);
+
+#define OZEC_NB_SHAPES(X) X(6, 3) X(6, 2) X(3, 2) X(10, 4) X(10, 3) X(10, 2) X(10, 1)
+#define OZEC_NB_DECL(K, R) hipError_t launch_nb_##K##_##R(const EncCrcArgs &e, hipStream_t st, int v);
+OZEC_NB_SHAPES(OZEC_NB_DECL)
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// Nibble-table fused kernel: the GF products and the CRC of every input share their LDS lookups.
+//
+// encode_crc_lv spends ~23 VALU per input dword on the GF part (5 selector ops + 3 v_perm + 1.5 XOR per output)
+// and ~12 per input dword on the CRC index math, and is VALU-issue bound.  Here every nibble n of
+// every input byte is looked up ONCE, with one ds_read_b64, in a table whose 8-B entry holds
+//   .x = the products c_rj * n (n shifted to its nibble half) for the R outputs, byte r = output r,
+//   .y = the raw-CRC contribution of n at its nibble position in the 16-B block (kNib* tables, distance set d).
+// Per input block: 32 index ops (one SDWA op each: (byte << 4) & 0xf0 and byte & 0xf0), 32 lookups, 16 XORs
+// into per-byte-position GF accumulators A[i] and 16 into the unit's CRC register -- 64 VALU against ~141 for
+// rs-10-4 in encode_crc_lv.  A[i] holds the R output bytes of byte position i; a 4x4 byte transpose (8 v_perm per
+// dword for R = 4) turns them into the R output dwords, whose CRCs use the G26 lookups as before.
+//
+// Tables: for each distance set d (D of them), input j and nibble position p, 16 entries of 8 B at a 16-B stride
+// with the tables of p and p ^ 1 interleaved (+0 / +8): under ds_read_b64 banking ((a/4) mod 64) the 16 entries
+// of a table cover 32 distinct banks, so random nibbles never conflict.  K*D*4 KiB of LDS (40 KiB for rs-10-4 at
+// D = 1), built once per workgroup; the grid is persistent (one resident set of workgroups).
+// Windows must be full and a whole number of D-step groups, as for encode_crc_lv.
+__device__ __forceinline__ uint32_t nib_lo_idx(uint32_t w, int q, uint32_t v4) {  // ((byte_q << 4) & 0xf0)
+  uint32_t d;
+  switch (q) {
+    case 0: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(d) : "v"(v4), "v"(w)); break;
+    case 1: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(d) : "v"(v4), "v"(w)); break;
+    case 2: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(d) : "v"(v4), "v"(w)); break;
+    default: asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(d) : "v"(v4), "v"(w)); break;
+  }
+  return d;
+}
+__device__ __forceinline__ uint32_t nib_hi_idx(uint32_t w, int q, uint32_t vf0) {  // (byte_q & 0xf0)
+  uint32_t d;
+  switch (q) {
+    case 0: asm("v_and_b32 %0, %1, %2" : "=v"(d) : "v"(vf0), "v"(w)); break;
+    case 1: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(d) : "v"(w), "v"(vf0)); break;
+    case 2: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "=v"(d) : "v"(w), "v"(vf0)); break;
+    default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(d) : "v"(w), "v"(vf0)); break;
+  }
+  return d;
+}
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32));
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+__device__ __forceinline__ uint2 lds64(const void *base, uint32_t byte_off) {
+  return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + byte_off);
+}
+
+// Dynamic work distribution of the persistent nibble kernel (DYN variants).  The (stripe, window) units are cut into
+// 8 contiguous ranges, one per XCD (the dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b starts
+// on range b % 8: each XCD streams one contiguous eighth of the batch), and a wave takes the next unit of its range
+// with one atomicAdd (a vector-memory atomic issued by lane 0 and broadcast with readfirstlane); a wave whose range is
+// used up moves on to the next range, so every unit is taken exactly once whatever the grid size or placement.  The
+// counters are a per-stream slot (launch_nb): launches on one stream run in order, and the last wave of a launch to
+// finish puts the slot back to zero for the next one.
+constexpr int kWqStride = 16;                 // ints between counters (64 B: one counter per cache line)
+constexpr int kWqDone = 8 * kWqStride;        // finished-wave counter
+constexpr int kWqInts = kWqDone + kWqStride;  // ints per slot
+struct WorkQueue {
+  int32_t *ctr;
+  int64_t units;
+  int q0, qi;
+  int64_t cur, end;  // claimed units [cur, end) not yet handed out (chunked claims)
+  int32_t seen;      // the own range's counter after this wave's last claim
+  int32_t per_range; // waves per range (chunk size of a guided claim: what is left / 2 per wave)
+  __device__ __forceinline__ int64_t next(int lane, bool guided) {
+    if (cur < end) return cur++;
+    while (qi < 8) {
+      const int q = (q0 + qi) & 7;
+      const int64_t lo = units * q / 8, hi = units * (q + 1) / 8;
+      int32_t c = 1;
+      if (guided && qi == 0) {
+        const int64_t left = hi - lo - seen;
+        c = static_cast<int32_t>(std::min<int64_t>(8, std::max<int64_t>(1, left / (2 * per_range))));
+      }
+      int32_t t = 0;
+      if (lane == 0) t = atomicAdd(ctr + q * kWqStride, c);
+      t = __builtin_amdgcn_readfirstlane(t);
+      seen = t + c;
+      if (lo + t < hi) {
+        cur = lo + t;
+        end = std::min<int64_t>(hi, cur + c);
+        return cur++;
+      }
+      ++qi;
+    }
+    return units;
+  }
+  // every wave calls this once after its last unit: the last of `waves` resets the slot
+  __device__ __forceinline__ void finish(int lane, int32_t waves) {
+    if (lane == 0 && atomicAdd(ctr + kWqDone, 1) == waves - 1) {
+      for (int q = 0; q < 8; ++q) atomicExch(ctr + q * kWqStride, 0);
+      atomicExch(ctr + kWqDone, 0);
+    }
+  }
+};
+
+// byte offset of the entry region of (distance set d, input j, byte i): lo-nibble table at +0, hi at +8
+template <int K>
+constexpr uint32_t nb_region(int d, int j, int i) {
+  return static_cast<uint32_t>(((d * K + j) * 16 + i) * 256);
+}
+
+// store (or, reconstructing, check) the finished window CRC of unit q (inputs 0..K-1, then the R outputs)
+template <int K, int R>
+__device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t w, int q, uint32_t v, uint32_t init) {
+  const CrcArgs &cr = e.crc;
+  const int64_t nwin = cr.nwin;
+  if (!e.verify) {
+    cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+  } else if (q >= K) {
+    cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+  } else if (cr.expected) {
+    const int64_t idx = (s * e.exp_units + e.in_unit[q]) * nwin + w;
+    const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
+    if (crc_finish(v, init, 0, 0) != ex) atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
+  }
+}
+
+// K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
+// FENCE: dwords of a block whose lookups go between scheduling fences (2: halves, at most 16 results live; 1:
+// quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree;
+// DYN: 0 one wave per unit, no grid-stride; persistent grid (one resident set of workgroups, tables built once per
+// workgroup) fed by the WorkQueue with 1 a claim per unit, made one unit ahead, 3 guided claims of up to 8 units, 4 a
+// claim per unit made when it is needed; 2 persistent grid with the static grid-stride order, 5 the same with the
+// waves' starts staggered by up to one window (a probe: do waves in lockstep on the same step offsets contend?);
+// DO: steps per output-register group (a multiple of D): the R output registers are looked up with the G26 distance
+// sets of DO steps and shifted once per DO steps, the K input registers (whose distance sets live in the nibble
+// entries, K * 4 KiB per set) once per D steps
+// PADV / PADL: probes only (variants 140-147), PADV independent v_xor_b32 / PADL ds_read_b32 added per step: the
+// marginal cost of one more VALU or LDS instruction says which pipe sets the time
+// XO: the output registers move by one step with no shift lookups (kernels.hpp kXo*): each is XORed into the first
+// dword of its next output block, whose G26 lookups use the set advanced by kXoAdvance bytes; the advance is undone
+// once per window.  Saves R x 7 lookups per step (the input registers keep their D-step shifts: their nibble lookups
+// also yield the GF products, which must see the unmodified data)
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
+          int PADV = 0, int PADL = 0, bool XO = false>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
+    const EncCrcArgs e) {
+  static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
+  static_assert(D <= kNibSets, "distance sets of the nibble blob");
+  static_assert((DO * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
+  static_assert(DO % D == 0 && DO <= 4, "output groups of whole input groups; windows are multiples of 4 steps");
+  static_assert(!XO || DO == D, "with XO the output registers are not grouped");
+  // one LDS block: G26 blob of DO sets (+ the D-step register shift when D < DO), then the (d, j, p) nibble tables,
+  // then the GF dwords of the setup.  Table regions past the 16-bit ds_read offset range are reached with bit 15 set
+  // in the index register (one v_or_b32).  XO: the input-register shift and the lane-tree shifts of the G26 blob,
+  // then the XO blob, instead of the G26 sets
+  constexpr uint32_t kXoOff = 224 + 1344;  // XO: word offset of the XO blob
+  constexpr uint32_t kShIn = XO ? 0 : DO == D ? g26_gshift(D) : g26_words(DO);  // word offset of the input-register shift
+  constexpr uint32_t kTree = XO ? 224 : g26_tree(DO);                           // and of the lane-tree shifts
+  constexpr uint32_t kTW = XO ? kXoOff + kXoWords : g26_words(DO) + (DO == D ? 0 : 224);
+  constexpr uint32_t kTB = (kTW * 4 + 255) / 256 * 256;  // nibble tables
+  constexpr uint32_t kLds = kTB + K * D * 4096 + K * 32 * 4;
+  static_assert(kLds <= 160 * 1024, "LDS per workgroup");
+  __shared__ __attribute__((aligned(256))) uint8_t s_all[kLds];
+  uint32_t *const s_t = reinterpret_cast<uint32_t *>(s_all);
+  uint2 *const s_c = reinterpret_cast<uint2 *>(s_all + kTB);
+  uint32_t *const s_gf = reinterpret_cast<uint32_t *>(s_all + kTB + K * D * 4096);
+  const CodeArgs &a = e.code;
+  const CrcArgs &cr = e.crc;
+  for (int t = threadIdx.x; t < K * 32; t += blockDim.x) {
+    const int j = t >> 5, h = (t >> 4) & 1, n = t & 15;
+    uint32_t dw = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) dw |= gf_mul_byte(a.coef[r * K + j], static_cast<uint32_t>(n) << (4 * h)) << (8 * r);
+    s_gf[t] = dw;
+  }
+  if constexpr (XO) {
+    load_tables(s_t, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224 + 1344);
+    load_tables(s_t + kXoOff, cr.xo, kXoWords);
+  } else {
+    load_tables(s_t, cr.g26[g26_slot(1, DO)], g26_words(DO));
+    if constexpr (DO != D) load_tables(s_t + kShIn, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224);
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < K * D * 512; q += blockDim.x) {
+    const int t = q >> 4, n = q & 15, p = t & 31, dj = t >> 5, j = dj % K, d = dj / K;
+    const uint32_t off = static_cast<uint32_t>((t >> 1) * 256 + n * 16 + (t & 1) * 8);
+    s_c[off >> 3] = make_uint2(s_gf[j * 32 + (p & 1) * 16 + n], cr.nib[(d * 32 + p) * 16 + n]);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwin = cr.nwin;
+  const int64_t units = a.nstripes * nwin;
+  const int32_t T = static_cast<int32_t>(cr.bpc >> 10);  // steps per window
+  const int32_t G = T / DO;                               // output groups per window
+  const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
+  uint32_t v4, vf0;  // index-op operands in VGPRs (VOP2/SDWA with no SGPR or literal operand issue fastest)
+  asm volatile("v_mov_b32 %0, 4" : "=v"(v4));
+  asm volatile("v_mov_b32 %0, 0xf0" : "=v"(vf0));
+  int64_t off_max = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
+  const uint32_t in_extent = static_cast<uint32_t>(off_max + cr.bpc);
+  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  constexpr bool kQueue = DYN == 1 || DYN == 3 || DYN == 4;
+  WorkQueue wq{e.work, units, static_cast<int>(blockIdx.x & 7), 0, 0, 0, 0, static_cast<int32_t>(gridDim.x * WPB / 8)};
+  int64_t u = kQueue ? wq.next(lane, DYN == 3) : bid * WPB + wave;
+  if constexpr (DYN == 5) {
+    const int n = static_cast<int>((blockIdx.x * WPB + wave) % 16) * 3;  // ~4 us per s_sleep 127 at 2 GHz
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  while (u < units) {
+    // DYN 1 / 3: the next unit is claimed before this one is worked on, so the atomic's round trip overlaps the work
+    const int64_t u_next = DYN == 1 || DYN == 3 ? wq.next(lane, DYN == 3) : u + static_cast<int64_t>(gridDim.x) * WPB;
+    // wave-uniform by construction; said explicitly so the descriptors below stay in SGPRs (the 64-bit division
+    // runs in the VALU, and without this the buffer accesses were wrapped in waterfall loops)
+    const int64_t s = uniform64(u / nwin);
+    const int64_t w = uniform64(u - s * nwin);
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
+    auto vstep = [&](int32_t t) { return voff + (t < T ? static_cast<uint32_t>(t) * 1024u : 0x80000000u); };
+    auto load = [&](uint32_t vo, int j) {
+      const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, vo, static_cast<int>(a.in_off[j]), 2);
+      return make_uint4(d[0], d[1], d[2], d[3]);
+    };
+    uint32_t S[K + R];
+#pragma unroll
+    for (int q = 0; q < K + R; ++q) S[q] = 0;
+    uint4 ring[NB];
+#pragma unroll
+    for (int i = 0; i + 1 < NB; ++i) ring[i] = load(vstep(i / K), i % K);
+    for (int32_t g = 0; g < G; ++g) {
+#pragma unroll
+      for (int rr = 0; rr < DO; ++rr) {
+        const int32_t t = g * DO + rr;
+        const int d = D - 1 - rr % D;  // distance set of this step's inputs
+        const int dout = DO - 1 - rr;  // and outputs
+        const uint32_t vcur = vstep(t), vnext = vstep(t + 1);
+        uint32_t A[16];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int ii = rr * K + j;
+          const int ahead = ii + NB - 1;
+          static_assert(NB - 1 <= K, "look-ahead of at most one step");
+          ring[ahead % NB] = load(ahead / K == rr ? vcur : vnext, ahead % K);
+          const uint4 x = ring[ii % NB];
+          const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+          XorChain ch;
+          ch.push(S[j]);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (FENCE > 0 && c > 0 && c % (FENCE > 0 ? FENCE : 1) == 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int i = 4 * c + q;
+              const uint32_t reg = kTB + nb_region<K>(d, j, i);
+              uint2 lo, hi;
+              if (reg + 256 <= 65536) {
+                lo = lds64(s_all, reg + nib_lo_idx(xw[c], q, v4));
+                hi = lds64(s_all, reg + 8 + nib_hi_idx(xw[c], q, vf0));
+              } else {
+                lo = lds64(s_all, (reg - 0x8000u) + (nib_lo_idx(xw[c], q, v4) | 0x8000u));
+                hi = lds64(s_all, (reg + 8 - 0x8000u) + (nib_hi_idx(xw[c], q, vf0) | 0x8000u));
+              }
+              A[i] = j == 0 ? (lo.x ^ hi.x) : xor3(A[i], lo.x, hi.x);
+              ch.push(lo.y);
+              ch.push(hi.y);
+            }
+          }
+          S[j] = ch.get();
+          if (FENCE > 0) __builtin_amdgcn_sched_barrier(0);
+        }
+        // 4x4 byte transposes: A[4c + q] byte r -> output r, dword c, byte q
+        uint32_t o[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t a0 = A[4 * c], a1 = A[4 * c + 1], a2 = A[4 * c + 2], a3 = A[4 * c + 3];
+          const uint32_t l01 = __builtin_amdgcn_perm(a1, a0, 0x05010400u), l23 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
+          o[0][c] = __builtin_amdgcn_perm(l23, l01, 0x05040100u);
+          if constexpr (R > 1) o[1][c] = __builtin_amdgcn_perm(l23, l01, 0x07060302u);
+          if constexpr (R > 2) {
+            const uint32_t h01 = __builtin_amdgcn_perm(a1, a0, 0x07030602u), h23 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+            o[2][c] = __builtin_amdgcn_perm(h23, h01, 0x05040100u);
+            if constexpr (R > 3) o[3][c] = __builtin_amdgcn_perm(h23, h01, 0x07060302u);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint4 p = make_uint4(o[r][0], o[r][1], o[r][2], o[r][3]);
+          __attribute__((ext_vector_type(4))) unsigned int dv = {p.x, p.y, p.z, p.w};
+          __builtin_amdgcn_raw_buffer_store_b128(dv, rout, vcur, static_cast<int>(a.out_off[r]), 2);
+          store_data_hold(p);
+          if constexpr (XO) {
+            uint4 px = p;
+            px.x ^= S[K + r];
+            S[K + r] = g26_block<true>(s_t + kXoOff, px);
+          } else {
+            S[K + r] ^= g26_block<true>(s_t + dout * kG26Set, p);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (PADV > 0 || PADL > 0) {
+          uint32_t px[4] = {static_cast<uint32_t>(lane), vf0, v4, static_cast<uint32_t>(t)};
+#pragma unroll
+          for (int i = 0; i < PADV; ++i) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(px[i & 3]) : "v"(v4));
+#pragma unroll
+          for (int i = 0; i < PADL; ++i)
+            px[i & 3] ^= reinterpret_cast<volatile uint32_t *>(s_t)[(lane + 7 * i) & 31];
+          asm volatile("" ::"v"(px[0]), "v"(px[1]), "v"(px[2]), "v"(px[3]));
+        }
+        if (DO != D && rr % D == D - 1 && rr + 1 < DO) {  // input groups ending inside the output group
+#pragma unroll
+          for (int q = 0; q < K; ++q) S[q] = g5_shift(s_t + kShIn, S[q]);
+        }
+      }
+      if (g + 1 < G) {
+#pragma unroll
+        for (int q = 0; q < (XO ? K : K + R); ++q) S[q] = g5_shift(s_t + (q < K ? kShIn : g26_gshift(DO)), S[q]);
+      }
+    }
+    const bool last = w == nwin - 1;
+    const uint32_t init = last ? cr.init_last : cr.init_full;
+    if constexpr (XO) {  // undo the advance of every output block
+#pragma unroll
+      for (int r = 0; r < R; ++r) S[K + r] = g5_shift(s_t + kXoOff + kXoInv, S[K + r]);
+    }
+    if constexpr (RS) {
+      int q = 0;
+      const uint32_t v = g5_lane_tree_rs<K + R>(s_t + kTree - kG5Tree, S, lane, q);
+      if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
+#pragma unroll
+        for (int qq = 0; qq < K + R; ++qq)
+          if (q == qq) nb_emit<K, R>(e, s, w, qq, v, init);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < K + R; ++q) {
+        const uint32_t v = g5_lane_tree(s_t + kTree - kG5Tree, S[q], lane);
+        if (lane == q) nb_emit<K, R>(e, s, w, q, v, init);
+      }
+    }
+    u = DYN == 4 ? wq.next(lane, false) : u_next;
+  }
+  if constexpr (kQueue) wq.finish(lane, static_cast<int32_t>(gridDim.x) * WPB);
+}
+
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
+          int PADV = 0, int PADL = 0, bool XO = false>
+hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
+  if constexpr ((DO * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
+    // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
+    // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
+    constexpr int kNB = (DO * K) % 2 == 0 ? 2 : (DO * K <= K + 1 ? DO * K : 1);
+    static_assert(kNB != NB && (DO * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO>(e, st);
+  } else {
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO>;
+    const int64_t units = e.code.nstripes * e.crc.nwin;
+    const int64_t blocks = (units + WPB - 1) / WPB;
+    int64_t g = blocks;
+    EncCrcArgs ed = e;
+    if constexpr (DYN != 0) {
+      // persistent: one resident set of workgroups (occupancy x CUs), each building its tables once
+      static int resident = 0;  // per instantiation and process (one device type)
+      if (resident == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WPB * 64, 0) != hipSuccess)
+          return hipErrorInvalidValue;
+        resident = std::max(1, cus * std::max(1, per_cu));
+      }
+      if constexpr (DYN != 2) {
+        ed.work = nb_work_slot(st);
+        if (ed.work == nullptr || units > (int64_t{1} << 30)) return hipErrorInvalidValue;
+      }
+      g = std::min<int64_t>(resident, blocks);
+    }
+    // non-persistent: one wave per (stripe, window) unit, no grid-stride: every workgroup builds its K*D*4 KiB of
+    // tables, and the dispatcher's refill of finished workgroups balances the CUs.  Measured on MI355X against a
+    // static persistent grid (profiles/r02/nb/ab_grid_*.log): C3r 56.2 % -> 63.5 %, C5dev 60.1 % -> 65.7 %.
+    if (g_tune.crc_grid > 0) g = std::min<int64_t>(g_tune.crc_grid, blocks);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, ed);
+    return hipGetLastError();
+  }
+}
+
+// variant (g_tune.crc_variant): 60-69 nibble-table kernel step groups / ring / occupancy A/B
+template <int K, int R>
+hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
+  constexpr int kD2 = K * 2 * 4096 + g26_words(2) * 4 <= 65536 ? 2 : 1;  // D = 2 where its tables fit
+  constexpr int kNB = K % 2 == 0 && K > 2 ? K / 2 : K;                    // a deeper ring dividing the group
+  constexpr auto lds_of = [](int d) { return (g26_words(d) * 4 + 255) / 256 * 256 + K * d * 4096 + K * 128; };
+  constexpr int kDmax = lds_of(4) <= 160 * 1024 ? 4 : lds_of(2) <= 160 * 1024 ? 2 : 1;  // one workgroup per CU
+  switch (v) {
+    case 61: return launch_nb<K, R, 1, 2, 8, 4>(e, st);
+    case 62: return launch_nb<K, R, 1, kNB, 8, 4>(e, st);
+    case 63: return launch_nb<K, R, kD2, 2, 8, 4>(e, st);
+    case 64: return launch_nb<K, R, kD2, kNB, 8, 4>(e, st);
+    case 65: return launch_nb<K, R, 1, 2, 8, 5>(e, st);
+    case 66: return launch_nb<K, R, 1, 2, 8, 4, 4>(e, st);
+    case 67: return launch_nb<K, R, 1, 2, 4, 4>(e, st);
+    case 68: return launch_nb<K, R, kD2, 2, 16, 4>(e, st);
+    case 69: return launch_nb<K, R, kD2, 2, 12, 4>(e, st);
+    case 70: return launch_nb<K, R, 1, 2, 8, 6>(e, st);
+    case 71: return launch_nb<K, R, 1, 2, 8, 8>(e, st);
+    case 72: return launch_nb<K, R, kD2, 2, 16, 8>(e, st);
+    case 73: return launch_nb<K, R, 1, kNB, 8, 5>(e, st);
+    case 74: return launch_nb<K, R, 1, 2, 8, 4, 2, false>(e, st);
+    case 75: return launch_nb<K, R, 1, kNB, 8, 4, 2, false>(e, st);
+    case 76: return launch_nb<K, R, kD2, 2, 16, 4, 2, false>(e, st);
+    // two-step groups for every K (tables past the 64 KiB offset range), four-step groups where they fit
+    case 77: return launch_nb<K, R, 2, kNB, 16, 4>(e, st);
+    case 78: return launch_nb<K, R, 2, 2, 16, 4>(e, st);
+    case 79: return launch_nb<K, R, K <= 6 ? 4 : 2, 2, 16, 4>(e, st);
+    // lookups fenced per dword (8 results live) for occupancy
+    case 80: return launch_nb<K, R, 1, kNB, 8, 4, 1>(e, st);
+    case 81: return launch_nb<K, R, 1, kNB, 8, 6, 1>(e, st);
+    case 82: return launch_nb<K, R, kD2, 2, 16, 4, 1>(e, st);
+    case 83: return launch_nb<K, R, kD2, 2, 16, 8, 1>(e, st);
+    case 84: return launch_nb<K, R, 1, 2, 8, 6, 1>(e, st);
+    // workgroup sizes that fill the VGPR-limited wave slots (occupancy is per workgroup)
+    case 85: return launch_nb<K, R, 1, kNB, 10, 4>(e, st);
+    case 86: return launch_nb<K, R, kD2, 2, 14, 4>(e, st);
+    case 87: return launch_nb<K, R, kD2, 2, 12, 4>(e, st);
+    case 88: return launch_nb<K, R, 1, kNB, 10, 5>(e, st);
+    case 89: return launch_nb<K, R, 1, kNB, 12, 4>(e, st);
+    case 93: return launch_nb<K, R, K == 10 ? 1 : kD2, K == 10 ? kNB : 2, K == 10 ? 8 : 12, 4, 0>(e, st);
+    case 94: return launch_nb<K, R, K == 10 ? 1 : kD2, K == 10 ? kNB : 2, K == 10 ? 8 : 12, 4, 4>(e, st);
+    case 95: return launch_nb<K, R, K == 10 ? 1 : kD2, 2, K == 10 ? 8 : 12, 4, 0>(e, st);
+    // persistent grid fed by the WorkQueue: the widest step groups whose tables fit one workgroup per CU (rs-10-x:
+    // D = 2, 95 KiB; rs-6-x / rs-3-x: D = 4, 117 / 69 KiB), and the round-2 geometries made persistent
+    case 100: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 1>(e, st);
+    case 101: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 1>(e, st);
+    case 102: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1>(e, st);
+    case 103: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 1>(e, st);
+    case 104: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1>(e, st);
+    case 105: return launch_nb<K, R, kDmax, 2, 12, 4, 2, true, 1>(e, st);
+    // the same geometry (round-2 rs-10-x default) with the static persistent order, guided claims, late claims
+    case 106: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 2>(e, st);
+    case 107: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 3>(e, st);
+    case 108: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 4>(e, st);
+    case 109: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 3>(e, st);
+    case 110: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 3>(e, st);
+    case 111: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 2>(e, st);
+    // deeper input rings: the loads of a whole step (K blocks) in flight ahead of the lookups
+    // probe: the round-2 rs-10-x default with one occupancy query of its kernel first (does the query change how the
+    // kernel runs?)
+    case 115: {
+      static bool asked = false;
+      if (!asked) {
+        int per_cu = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_crc_nb<K, R, 1, kNB, 8, 4>, 8 * 64, 0);
+        asked = true;
+      }
+      return launch_nb<K, R, 1, kNB, 8, 4>(e, st);
+    }
+    case 120: return launch_nb<K, R, 1, K, 8, 4>(e, st);
+    case 121: return launch_nb<K, R, kD2, K, 12, 4>(e, st);
+    case 122: return launch_nb<K, R, kD2, K, 8, 4>(e, st);
+    case 123: return launch_nb<K, R, 1, K, 8, 5>(e, st);
+    case 112: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 5>(e, st);
+    case 113: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 5>(e, st);
+    case 114: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 5>(e, st);
+    // output registers shifted once per 2 / 4 steps (the input registers as before)
+    case 130: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 2>(e, st);
+    case 131: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 4>(e, st);
+    case 132: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, 4>(e, st);
+    case 133: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, 2>(e, st);
+    case 134: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 1, 4>(e, st);
+    case 135: return launch_nb<K, R, 1, 2, 8, 4, 2, true, 0, 4>(e, st);
+    // probes: the rs-10-x (62) and rs-6-x (87) defaults with 64 / 192 more VALU or 16 / 48 more LDS reads per step
+    case 140: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 64, 0>(e, st);
+    case 141: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 192, 0>(e, st);
+    case 142: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 16>(e, st);
+    case 143: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 48>(e, st);
+    case 144: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 64, 0>(e, st);
+    case 145: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 192, 0>(e, st);
+    case 146: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 16>(e, st);
+    case 147: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 48>(e, st);
+    // round 3: free output-register shifts (XO) on the rs-10-x default (102 / 62) and rs-6-x default (87)
+    // geometries, and the geometries the saved LDS work may favour
+    case 150: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, 1, 0, 0, true>(e, st);
+    case 151: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 0, true>(e, st);
+    case 152: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 0, true>(e, st);
+    case 153: return launch_nb<K, R, 1, 2, 8, 4, 2, true, 0, 1, 0, 0, true>(e, st);
+    case 154: return launch_nb<K, R, 1, kNB, 8, 5, 2, true, 0, 1, 0, 0, true>(e, st);
+    case 155: return launch_nb<K, R, kD2, 2, 16, 4, 2, true, 0, kD2, 0, 0, true>(e, st);
+    case 156: return launch_nb<K, R, 1, 2, 12, 4, 2, true, 0, 1, 0, 0, true>(e, st);
+    case 157: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 1, kD2, 0, 0, true>(e, st);
+    case 158: return launch_nb<K, R, 1, kNB, 10, 4, 2, true, 0, 1, 0, 0, true>(e, st);
+    // XO with the widest input step groups whose tables fit one workgroup per CU (rs-10-x: D = 2; rs-6-x: D = 4),
+    // persistent (WorkQueue) and not, and the rs-6-x default geometry in 8-wave workgroups
+    case 159: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 1, kDmax, 0, 0, true>(e, st);
+    case 160: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 0, kDmax, 0, 0, true>(e, st);
+    case 161: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 1, kDmax, 0, 0, true>(e, st);
+    case 162: return launch_nb<K, R, kD2, 2, 8, 4, 2, true, 0, kD2, 0, 0, true>(e, st);
+    case 163: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true>(e, st);
+    default: break;
+  }
+  return launch_nb<K, R, 1, 2, 8, 4>(e, st);
+}
+}  // namespace
+}  // namespace ozec

@@ -1,0 +1,6 @@
+// encode_crc_nb variants of the rs-10-4 shape (fused_nb.hpp)
+#include "fused_nb.hpp"
+
+namespace ozec {
+hipError_t launch_nb_10_4(const EncCrcArgs &e, hipStream_t st, int v) { return launch_nb_kr<10, 4>(e, st, v); }
+}  // namespace ozec

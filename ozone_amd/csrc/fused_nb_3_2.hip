@@ -1,0 +1,6 @@
+// encode_crc_nb variants of the rs-3-2 shape (fused_nb.hpp)
+#include "fused_nb.hpp"
+
+namespace ozec {
+hipError_t launch_nb_3_2(const EncCrcArgs &e, hipStream_t st, int v) { return launch_nb_kr<3, 2>(e, st, v); }
+}  // namespace ozec

@@ -46,6 +46,7 @@ struct CrcArgs {
   const uint32_t *tables[3];  // device G5 table blobs for this CRC type, B = 1, 2, 4 blocks per lane per step
   const uint32_t *g26[6];     // device G26 table blobs for this CRC type, one per kG26Cfg entry
   const uint32_t *nib;        // device nibble table blob for this CRC type (kNib* layout)
+  const uint32_t *xo;         // device XO table blob for this CRC type (kXo* layout)
   uint32_t init_full;      // shift(0xFFFFFFFF, bpc bytes)
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
@@ -121,6 +122,18 @@ constexpr int g26_slot(int B, int D) {
 // steps of a 64-lane wave before the end of its step group).  Same map as the G26 set e of (B = 1, D > e).
 constexpr int kNibSets = 4;
 constexpr int kNibWords = kNibSets * 32 * 16;
+
+// Device CRC "XO" blob of the nibble kernel's free register shift (fused_nb.hpp, XO variants).  A lane's output
+// register U is XORed into the first dword of its next 16-B block before that block's lookups: the raw CRC of
+// (block ^ U) is crc(block) advanced by 0 bytes plus U advanced by 16 bytes (the CRC register identity
+// raw(U; B) = raw(0; B ^ U)).  With the block tables advanced by kXoAdvance = 1008 bytes, U therefore moves by
+// 1008 + 16 = 1024 bytes -- one step of the wave, the shift the register needs -- at the cost of one XOR, and every
+// block lands kXoAdvance bytes too far; the register is brought back once per window by the inverse shift.
+//   [0, kG26Set)            G26 set: block -> raw CRC advanced by kXoAdvance zero bytes (g26_block extraction)
+//   [kXoInv, +224)          register shift by -kXoAdvance bytes (inverse of the advance), 7 tables of 5-bit groups
+constexpr int kXoAdvance = 1024 - 16;
+constexpr int kXoInv = kG26Set;
+constexpr int kXoWords = kG26Set + 224;
 
 // Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.
 struct TuneKnobs {

@@ -11,6 +11,6 @@ CXX=/opt/rocm/lib/llvm/bin/clang++
 $CXX -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer -c "$R/tests/native/gpu_host_asan.cpp" \
   -o "$R/build/asan/gpu_host_asan.o"
 $CXX -fsanitize=address,undefined -o "$R/tests/native/bin/gpu_host_asan" "$R/build/asan/gpu_host_asan.o" \
-  "$R"/build/asan/{gf256,crc_host,capi,stripe_queue,copy_pool,numa}.o "$R/build/obj/kernels.o" "$R/build/obj/fused.o" \
+  "$R"/build/asan/{gf256,crc_host,capi,stripe_queue,copy_pool,numa}.o "$R/build/obj/kernels.o" "$R"/build/obj/fused*.o \
   "$R/build/asan/oracle.o" -L/opt/rocm/lib -lamdhip64 -lpthread -Wl,-rpath,/opt/rocm/lib
 echo built "$R/tests/native/bin/gpu_host_asan"

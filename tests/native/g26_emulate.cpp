@@ -108,6 +108,48 @@ int main() {
         ++nib_checked;
       }
   }
-  printf("g26 emulation: %d windows bit-exact; nibble tables: %d blocks bit-exact\n", checked, nib_checked);
+  // XO scheme of the nibble kernel's output registers (fused_nb.hpp, XO variants): per step every lane XORs its
+  // register into the first dword of its next block and looks the block up in the XO set (advanced by kXoAdvance
+  // bytes), so the register moves by one 1 KiB step with no shift lookups; the inverse table undoes the advance
+  int xo_checked = 0;
+  for (int ty = 0; ty < 2; ++ty) {
+    const CrcMath &cm = CrcMath::get(static_cast<CrcType>(ty));
+    const std::vector<uint32_t> &X = cm.xo_tables();
+    if (static_cast<int>(X.size()) != kXoWords) {
+      printf("XO blob size mismatch\n");
+      return 1;
+    }
+    for (int it = 0; it < 200; ++it) {  // the inverse really inverts the advance
+      const uint32_t v = static_cast<uint32_t>(rand()) * 2654435761u + static_cast<uint32_t>(it);
+      if (shift7(X.data() + kXoInv, cm.shift(v, kXoAdvance)) != v) {
+        printf("FAIL XO inverse crc type %d\n", ty);
+        return 1;
+      }
+    }
+    for (int T : {1, 2, 3, 4, 16}) {  // steps per window (bpc = T KiB)
+      std::vector<uint8_t> buf(static_cast<size_t>(T) * 1024);
+      for (auto &x : buf) x = static_cast<uint8_t>(rand());
+      uint32_t ref = 0;
+      for (uint8_t x : buf) ref = (ref >> 8) ^ cm.byte_table((ref ^ x) & 0xff);
+      uint32_t total = 0;
+      for (int l = 0; l < 64; ++l) {
+        uint32_t U = 0;
+        for (int t = 0; t < T; ++t) {
+          uint32_t w[4];
+          memcpy(w, &buf[static_cast<size_t>(t) * 1024 + 16 * l], 16);
+          w[0] ^= U;
+          U = g26_block(X.data(), w);
+        }
+        total = cm.shift(total, 16) ^ shift7(X.data() + kXoInv, U);
+      }
+      if (total != ref) {
+        printf("FAIL XO window crc type %d T=%d: %08x vs %08x\n", ty, T, total, ref);
+        return 1;
+      }
+      ++xo_checked;
+    }
+  }
+  printf("g26 emulation: %d windows bit-exact; nibble tables: %d blocks bit-exact; XO: %d windows bit-exact\n", checked,
+         nib_checked, xo_checked);
   return 0;
 }

@@ -32,7 +32,8 @@ void mat_invert(const uint32_t *cols, uint32_t *inv) {
   }
   for (int c = 0; c < 32; ++c) {
     int piv = c;
-    while (!((rows[piv] >> c) & 1u)) ++piv;  // exists: A is invertible
+    while (piv < 32 && !((rows[piv] >> c) & 1u)) ++piv;
+    if (piv == 32) continue;  // singular (not for a shift: P(0) = 1); the CPU test checks inverse o advance = identity
     std::swap(rows[c], rows[piv]);
     std::swap(id[c], id[piv]);
     for (int r = 0; r < 32; ++r)

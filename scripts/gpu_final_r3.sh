@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round-3 evidence on one MI355X, in two calls (each under gpurun's 20-minute limit):
+# Round-3 evidence on one MI355X, in three calls (each under gpurun's 20-minute limit):
 #   PHASE=a  the whole GPU suite, smoke(), the default bench line, a 2-rank rehearsal with per-rank arrays;
-#   PHASE=b  every workload's line (live PMC traffic and rocprof clocks where bench.py takes them), rocprofv3 kernel
-#            stats of the main kernels with the bench's own warmup/steps, SQ counter passes of the fused defaults.
+#   PHASE=b  every workload's line (live PMC traffic and rocprof clocks where bench.py takes them);
+#   PHASE=c  the mixed erasure sets, the per-call host encode at T threads, rocprofv3 kernel stats of the main kernels
+#            with the bench's own warmup/steps, SQ counter passes of the fused defaults.
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=$R/gpurun_out/${OUT:-r3final}; mkdir -p $O
@@ -19,10 +20,17 @@ if [ "${PHASE:-a}" = a ]; then
   echo "2-rank ok"
   exit 0
 fi
+if [ "${PHASE}" = b ]; then
 for w in ${WORKLOADS:-c1 c3 c3r c3r_host c4 c5dev crc verify queue queue_pageable host stream}; do
   timeout -k 10 300 python bench.py --workload $w > $O/bench_$w.json 2> $O/bench_$w.err || { echo "bench $w failed"; tail $O/bench_$w.err; exit 1; }
   echo "bench $w ok"
 done
+echo workloads done
+exit 0
+fi
+timeout -k 10 300 python -u scripts/ab.py c3r crc_variant 0,102,62,151 6 > $O/ab_c3r_defaults.log 2>&1 || { tail $O/ab_c3r_defaults.log; exit 1; }
+timeout -k 10 300 python -u scripts/ab.py c5dev crc_variant 0,87,152,157 6 > $O/ab_c5dev_defaults.log 2>&1 || { tail $O/ab_c5dev_defaults.log; exit 1; }
+grep -h '"wl"' $O/ab_c3r_defaults.log $O/ab_c5dev_defaults.log
 timeout -k 10 300 python bench.py --workload c3 --erased 1,4,10,13 > $O/bench_c3_mixed.json 2> $O/bench_c3_mixed.err || { echo "c3 mixed failed"; exit 1; }
 timeout -k 10 300 python bench.py --workload c3r --erased 1,4,10,13 > $O/bench_c3r_mixed.json 2> $O/bench_c3r_mixed.err || { echo "c3r mixed failed"; exit 1; }
 for t in 4 8 16; do

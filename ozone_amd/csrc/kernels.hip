@@ -406,11 +406,20 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26(const CrcArgs a) {
 // unrolled step (NS divides D), so no register copy or branch sits between a load and its use -- either makes
 // the compiler wait for every load in flight (vmcnt(0)) at every step.  For the same reason verify mode reads
 // the stored CRC with a scalar load (lgkmcnt), not a vector one.
-template <int D, int NS>
+// XO: the register moves by one step with no shift lookups (kernels.hpp kXo*): it is XORed into the first dword of
+// its lane's next block, which is looked up in the XO set; the advance is undone once per window.  D then only sets
+// the unroll (the load ring NS divides it); the LDS holds the lane-tree shifts and the XO blob instead of D sets.
+template <int D, int NS, bool XO = false>
 __global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int64_t nfull, int64_t per_wave) {
   static_assert(NS >= 2 && D % NS == 0, "the register ring must divide the unrolled group");
-  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(D)];
-  load_tables(s_t, a.g26[g26_slot(1, D)], g26_words(D));
+  constexpr int kTree = XO ? 0 : g26_tree(D), kXoOff = 1344;
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[XO ? 1344 + kXoWords : g26_words(D)];
+  if constexpr (XO) {
+    load_tables(s_t, a.g26[g26_slot(1, D)] + g26_tree(D), 1344);
+    load_tables(s_t + kXoOff, a.xo, kXoWords);
+  } else {
+    load_tables(s_t, a.g26[g26_slot(1, D)], g26_words(D));
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -455,11 +464,18 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int6
 #pragma unroll
       for (int rr = 0; rr < D; ++rr) {
         load_next(x[(rr + NS - 1) % NS]);
-        S ^= g26_block(s_t + (D - 1 - rr) * kG26Set, x[rr % NS]);
+        if constexpr (XO) {
+          uint4 xs = x[rr % NS];
+          xs.x ^= S;
+          S = g26_block(s_t + kXoOff, xs);
+        } else {
+          S ^= g26_block(s_t + (D - 1 - rr) * kG26Set, x[rr % NS]);
+        }
       }
-      if (g + 1 < G) S = g5_shift(s_t + g26_gshift(D), S);
+      if (!XO && g + 1 < G) S = g5_shift(s_t + g26_gshift(D), S);
     } while (++g < G);
-    S = g5_lane_tree(s_t + g26_tree(D) - kG5Tree, S, lane);
+    S = g5_lane_tree(s_t + kTree - kG5Tree, S, lane);
+    if constexpr (XO) S = g5_shift(s_t + kXoOff + kXoInv, S);
     if (lane == 0) {
       if (a.expected) {
         if (crc_finish(S, a.init_full, 0, 0) != (a.expected_be ? __builtin_bswap32(ex) : ex))
@@ -1151,13 +1167,13 @@ int64_t stream_grid(int64_t total, int64_t per_wave) {
 
 // Full windows of every cell through the streaming kernel, the short last window of each cell (len % bpc)
 // through the per-window kernel.
-template <int D, int NS>
+template <int D, int NS, bool XO = false>
 hipError_t launch_crc_stream(const CrcArgs &a, hipStream_t st) {
   const int64_t nfull = a.len / a.bpc;
   const int64_t total = a.ncells * nfull;
   if (total > 0) {
     const int64_t per_wave = stream_per_wave(total, a.bpc);
-    hipLaunchKernelGGL((crc_windows_g26s<D, NS>), dim3(static_cast<unsigned>(stream_grid(total, per_wave))),
+    hipLaunchKernelGGL((crc_windows_g26s<D, NS, XO>), dim3(static_cast<unsigned>(stream_grid(total, per_wave))),
                        dim3(kBlock), 0, st, a, nfull, per_wave);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
@@ -1187,15 +1203,22 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
                    aligned16(a.bpc);
   if (vec) {
     const int v = g_tune.crc_variant;
-    // streaming kernel (D, ring) = (4, 4) for windows of whole 4 KiB groups; variants 20-24 for A/B
-    // (scripts/tune_crc.py): (4, 2), (8, 4), (4, 4), (8, 8), (2, 2)
-    if ((v == 0 || v >= 20) && a.bpc % (v == 21 || v == 23 ? 8192 : v == 24 ? 2048 : 4096) == 0) {
+    // streaming kernel for windows of whole 4 KiB groups, (D, ring) = (4, 2) with free register shifts (XO); variants
+    // 20-24 for A/B (scripts/tune_crc.py): (4, 2), (8, 4), (4, 4), (8, 8), (2, 2) with D-step groups; 25-27 with XO:
+    // (4, 4), (4, 2), (8, 4)
+    if ((v == 0 || v >= 20) && a.bpc % (v == 21 || v == 23 || v == 27 ? 8192 : v == 24 ? 2048 : 4096) == 0) {
       switch (v) {
+        case 25: return launch_crc_stream<4, 4, true>(a, st);
+        case 26: return launch_crc_stream<4, 2, true>(a, st);
+        case 27: return launch_crc_stream<8, 4, true>(a, st);
         case 20: return launch_crc_stream<4, 2>(a, st);
         case 21: return launch_crc_stream<8, 4>(a, st);
         case 23: return launch_crc_stream<8, 8>(a, st);
         case 24: return launch_crc_stream<2, 2>(a, st);
-        default: return launch_crc_stream<4, 4>(a, st);
+        case 22: return launch_crc_stream<4, 4>(a, st);  // the round-2 default
+        // default (round 3): free register shifts, ring of 2 (CRC32C 78.5 -> 80.3 %, verify 77.8 -> 80.3 % in
+        // same-process A/Bs, profiles/r03/ab/crcxo_*.log)
+        default: return launch_crc_stream<4, 2, true>(a, st);
       }
     }
     // per-window kernel: G26 tables, B = 1 block per lane per step, groups of D = 4 steps, two steps of loads in

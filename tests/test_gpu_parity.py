@@ -212,8 +212,9 @@ def test_checksum_batch_vs_oracle(ctype, otype, bpc):
         assert (got[c] == oracle.crc_windows(otype, data[c], bpc)).all(), c
 
 
-@pytest.mark.parametrize("variant", [0, 1, 11, 13, 20, 21, 23, 24])
-def test_checksum_stream_runs_cross_cells(variant):
+@pytest.mark.parametrize("variant", [0, 1, 11, 13, 20, 21, 22, 23, 24, 25, 26, 27])
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
+def test_checksum_stream_runs_cross_cells(variant, ctype, otype):
     """crc_windows_g26s (the streaming kernel): per-wave runs of full windows that cross cell boundaries
     (cell_stride > len, crc_grid forced small), the short last window of every cell (the per-window kernel's
     launch), compute and verify modes -- every CRC kernel variant bit-exact vs the oracle."""
@@ -226,12 +227,12 @@ def test_checksum_stream_runs_cross_cells(variant):
     for c in range(C):
         buf[c * stride:c * stride + n] = data[c]
     nwin = (n + bpc - 1) // bpc
-    ref = np.stack([oracle.crc_windows(oracle.CRC32C, data[c], bpc) for c in range(C)]).astype(np.uint32)
+    ref = np.stack([oracle.crc_windows(otype, data[c], bpc) for c in range(C)]).astype(np.uint32)
     try:
         assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
         assert lib.ozec_set_tuning(b"crc_grid", 3) == 0  # 12 waves for 35 full windows: runs of 3 cross cells
         out = torch.zeros((C, nwin), dtype=torch.int32, device=DEV)
-        ck.checksum_windows_batch(ck.ChecksumType.CRC32C, t(buf), stride, C, n, bpc, out)
+        ck.checksum_windows_batch(ctype, t(buf), stride, C, n, bpc, out)
         assert (h(out).view(np.uint32) == ref).all()
         bad = buf.copy()
         bad[3 * stride + 4 * bpc + 9] ^= 0x10  # window 4 of cell 3
@@ -239,7 +240,7 @@ def test_checksum_stream_runs_cross_cells(variant):
         bad[6 * stride + n - 1] ^= 1           # short last window of cell 6
         bad[0] ^= 0x80                         # window 0 of cell 0
         mism = torch.zeros(C, dtype=torch.int32, device=DEV)
-        ck.checksum_verify_batch(ck.ChecksumType.CRC32C, t(bad), stride, C, n, bpc, t(ref.view(np.int32)), mism)
+        ck.checksum_verify_batch(ctype, t(bad), stride, C, n, bpc, t(ref.view(np.int32)), mism)
         assert h(mism).tolist() == [0, -1, -1, 2, -1, -1, nwin - 1]
     finally:
         lib.ozec_set_tuning(b"crc_variant", 0)

@@ -680,18 +680,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 // LDS too (ds_read_b32 broadcast).
 // PAD > 0 (diagnostic variants only): PAD extra independent VALU ops per step, to measure what one more VALU
 // instruction costs the kernel (scripts/gpu_valu_pad.sh; DESIGN §2.3 "what bounds it").
+// XO (XOR codec only): the input registers move by one step with no shift lookups (kernels.hpp kXo*; as
+// crc_windows_g26s), the parity's register is still the XOR of theirs, and the advance is undone once per window.
 template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false, bool HV = false, int PAD = 0,
-          int PADK = 0, bool VMASK = false>
+          int PADK = 0, bool VMASK = false, bool XO = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_g26(const EncCrcArgs e, const TabArgs<K * R> tabs) {
   constexpr int E = D;
   static_assert(D >= 1, "group of at least one step");
-  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(E)];
+  static_assert(!XO || XORC, "XO only where every CRC register belongs to an input (the XOR codec)");
+  constexpr int kXoOff = g26_words(E);  // XO: the XO blob after the G26 blob
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(E) + (XO ? kXoWords : 0)];
   __shared__ __attribute__((aligned(16))) uint4 s_q[K * R];
   __shared__ __attribute__((aligned(16))) uint2 s_d[K * R];
   __shared__ uint32_t s_top[K * R];
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
   load_tables(s_t, cr.g26[g26_slot(1, D)], g26_words(E));
+  if constexpr (XO) load_tables(s_t + kXoOff, cr.xo, kXoWords);
   for (int t = threadIdx.x; t < K * R; t += blockDim.x) {
     s_q[t] = make_uint4(tabs.w[t][0], tabs.w[t][1], tabs.w[t][2], tabs.w[t][3]);
     s_d[t] = make_uint2(tabs.w[t][0], tabs.w[t][2]);
@@ -805,7 +810,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
         if constexpr (XORC) store_data_hold(acc[0]);
 #pragma unroll
         for (int j = 0; j < (XORC ? K : K + R); ++j) {
-          S[j] ^= g26_block<HV, VMASK>(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K], vmask);
+          if constexpr (XO) {
+            uint4 xs = x[j];
+            xs.x ^= S[j];
+            S[j] = g26_block<HV, VMASK>(s_t + kXoOff, xs, vmask);
+          } else {
+            S[j] ^= g26_block<HV, VMASK>(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K], vmask);
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (PAD > 0) {  // PADK: 0 v_xor_b32 (fast class), 1 v_perm_b32 (slow class), 2 ds_read_b32
@@ -828,7 +839,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
           }
         }
       }
-      if (g + 1 < G) {
+      if (!XO && g + 1 < G) {
 #pragma unroll
         for (int j = 0; j < (XORC ? K : K + R); ++j) S[j] = g5_shift(s_t + g26_gshift(E), S[j]);
       }
@@ -837,6 +848,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
       S[K] = 0;
 #pragma unroll
       for (int j = 0; j < K; ++j) S[K] ^= S[j];
+    }
+    if constexpr (XO) {  // undo the advance (the parity register is linear in the inputs': the same once)
+#pragma unroll
+      for (int q = 0; q <= K; ++q) S[q] = g5_shift(s_t + kXoOff + kXoInv, S[q]);
     }
     if constexpr (PAD > 0) S[0] ^= (pad[0] ^ pad[1] ^ pad[2] ^ pad[3]) & 0u;  // keeps the pad live, changes nothing
     const uint32_t init = last ? cr.init_last : cr.init_full;
@@ -1284,6 +1299,10 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
     if (e.code.all_ones && v != 2) {
       // XOR codec: D = 4 with the next step's loads in flight (C4 77.9 % vs 75.8 % for D = 2, ab_c4.log)
       if (v == 3) hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1>), grid, block, 0, st, e, tabs);
+      else if (v == 4)  // free register shifts (XO)
+        hipLaunchKernelGGL((encode_crc_g26<K, R, 4, true, 1, 4, true, false, 0, 0, false, true>), grid, block, 0, st, e, tabs);
+      else if (v == 5)
+        hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1, 4, true, false, 0, 0, false, true>), grid, block, 0, st, e, tabs);
       else hipLaunchKernelGGL((encode_crc_g26<K, R, 4, true, 1, 4, true>), grid, block, 0, st, e, tabs);
       return hipGetLastError();
     }

@@ -381,6 +381,32 @@ def test_encode_crc_fused_vs_oracle(k, p, codec, n, bpc, S, ctype, otype):
             assert (crcs[s, u] == oracle.crc_windows(otype, units[u], bpc)).all(), (s, u)
 
 
+@pytest.mark.parametrize("variant", [4, 5])
+@pytest.mark.parametrize("k,n,bpc,S", [(2, 1 << 18, 16384, 3), (3, 50000, 16384, 2), (6, 65536 + 4096, 4096, 2),
+                                       (2, 1040 * 16, 1040, 2), (10, 3 * 16384 - 16, 16384, 2)])
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
+def test_encode_crc_xor_free_shift_vs_oracle(variant, k, n, bpc, S, ctype, otype):
+    """The XOR codec's per-window fused kernel with free register shifts (XO, variants 4 / 5: groups of 4 / 2 steps),
+    short last windows (leading virtual blocks), windows that are not a multiple of 1 KiB, both CRC types."""
+    lib = L.lib()
+    data = np.stack([np.stack(cells(SEED, 50500 + s * k, k, n)) for s in range(S)])
+    nwin = (n + bpc - 1) // bpc
+    d_out = torch.full((S, 1, n), 0xA5, dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, k + 1, nwin), dtype=torch.int32, device=DEV)
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, 1, "xor"))
+    try:
+        assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+        e.encode_crc_batch(t(data), k * n, n, d_out, n, n, S, n, ctype, bpc, d_crc)
+        par, crcs = h(d_out), h(d_crc).view(np.uint32)
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+    for s in range(S):
+        ref = oracle.xor_encode(list(data[s]))
+        assert (par[s, 0] == ref).all(), s
+        for u, cell in enumerate(list(data[s]) + [ref]):
+            assert (crcs[s, u] == oracle.crc_windows(otype, cell, bpc)).all(), (s, u)
+
+
 @pytest.mark.parametrize("variant", [61, 63, 100, 101, 150, 151, 152])
 @pytest.mark.parametrize("k,p,n,bpc,S", [(6, 3, 1 << 17, 16384, 3), (10, 4, 1 << 16, 4096, 2), (3, 2, 1 << 17, 8192, 3),
                                          (6, 2, 1 << 15, 32768, 2), (10, 1, 1 << 16, 16384, 2)])
@@ -500,7 +526,7 @@ def test_encode_crc_other_shapes_variants_vs_oracle(variant, k, p):
             assert (crcs[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [0, 13, 20, 21])
+@pytest.mark.parametrize("variant", [0, 4, 5, 13, 20, 21])
 @pytest.mark.parametrize("k,n,bpc,S", [(2, 1 << 18, 16384, 5), (3, 65536, 4096, 7), (6, 1 << 17, 8192, 3)])
 def test_encode_xor_crc_stream_runs_cross_stripes(variant, k, n, bpc, S):
     """encode_xor_crc_g26s (XOR codec, all windows full): per-wave runs of (stripe, window) units that cross

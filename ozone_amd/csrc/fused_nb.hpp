@@ -507,6 +507,14 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 161: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 1, kDmax, 0, 0, true>(e, st);
     case 162: return launch_nb<K, R, kD2, 2, 8, 4, 2, true, 0, kD2, 0, 0, true>(e, st);
     case 163: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true>(e, st);
+    // the XO defaults (150: rs-10-x, 163: rs-6-x / rs-3-x) without lookup fences, with one fence per input block,
+    // with a deeper ring, a full-step ring, 14-wave workgroups
+    case 164: return launch_nb<K, R, 1, kNB, 8, 4, 0, true, 1, 1, 0, 0, true>(e, st);
+    case 165: return launch_nb<K, R, 1, kNB, 8, 4, 4, true, 1, 1, 0, 0, true>(e, st);
+    case 166: return launch_nb<K, R, 2, 2, 16, 4, 0, true, 1, 2, 0, 0, true>(e, st);
+    case 167: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true>(e, st);
+    case 168: return launch_nb<K, R, 2, 2, 14, 4, 2, true, 1, 2, 0, 0, true>(e, st);
+    case 169: return launch_nb<K, R, 1, K, 8, 4, 2, true, 1, 1, 0, 0, true>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);

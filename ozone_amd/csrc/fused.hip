@@ -285,11 +285,12 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // of 5 input blocks and one-step groups (62: C3r 62.9 %; encode_crc_lv 52.5 %), rs-6-x / rs-3-x with two-step
   // groups in 12-wave workgroups (87: C5dev 66.9 %; encode_crc_lv 57.9 %); 56 / 59 pin the streamed-input kernel's
   // defaults.  Round 3 (profiles/r03/ab/): the output registers shift for free (XO), and the grid is persistent, fed
-  // by the WorkQueue -- rs-10-x 150 (62's geometry; C3r 64.8 % vs 63.7 % for 102, 62.5 % for 62), rs-6-x / rs-3-x
-  // 163 (two-step groups in 16-wave workgroups; C5dev 68.4 % vs 67.2 % for 87); without a counter slot the same
-  // kernels on a one-wave-per-window grid (151 / 152)
+  // by the WorkQueue -- rs-10-x 150 (62's geometry; C3r 64.8 % vs 63.7 % for 102, 62.5 % for 62), rs-3-x 163
+  // (two-step groups in 16-wave workgroups), rs-6-x 167 (163 with a ring of 3 input blocks; C5dev 68.4 % for 163 vs
+  // 67.2 % for 87 on one box, 66.9 % for 167 vs 66.2 % for 163 on another); without a counter slot the same kernels
+  // on a one-wave-per-window grid (151 / 152)
   const bool queue = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) && nb_work_slot(st) != nullptr;
-  if (v == 0) v = k == 10 ? (queue ? 150 : 151) : (queue ? 163 : 152);
+  if (v == 0) v = k == 10 ? (queue ? 150 : 151) : !queue ? 152 : k == 6 ? 167 : 163;
   if (v >= 60 && v < 170) {
     if (k == 6 && r == 3) return launch_nb_6_3(e, st, v);
     if (k == 6 && r == 2) return launch_nb_6_2(e, st, v);

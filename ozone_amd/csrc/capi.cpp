@@ -1554,6 +1554,7 @@ int ozec_set_tuning(const char *key, int64_t value) {
   else if (k == "host_slots" && value > 0) ozec::g_tune.host_slots = value;
   else if (k == "queue_batches" && value >= 0 && value <= 64) ozec::g_tune.queue_batches = value;
   else if (k == "copy_threads" && value >= 0) ozec::set_copy_threads(static_cast<int>(value));
+  else if (k == "copy_stream") ozec::set_copy_stream(static_cast<int>(value));
   else if (k == "e2e_chunk" && value > 0) ozec::g_tune.e2e_chunk = value;
   else if (k == "e2e_rect") ozec::g_tune.e2e_rect = static_cast<int>(value);
   else return fail(OZEC_EINVAL, "unknown tuning key " + k);

@@ -19,5 +19,8 @@ void parallel_copy(const std::vector<CopyTask> &tasks);
 void set_copy_threads(int n);
 // bind the pool's workers to the CPUs of a NUMA node (-1: no binding)
 void set_copy_node(int node);
+// pieces copied with streaming (non-temporal) stores: 1 on, 0 plain memcpy, -1 auto (on where AVX2 exists);
+// set by ozec_set_tuning("copy_stream", n)
+void set_copy_stream(int mode);
 
 }  // namespace ozec

@@ -39,6 +39,11 @@ timeout -k 10 300 python bench.py --workload c3r --erased 1,4,10,13 > $O/bench_c
 for t in 4 8 16; do
   timeout -k 10 300 python bench.py --workload host --threads $t --no-cpu > $O/bench_host_t$t.json 2> $O/bench_host_t$t.err || { echo "host T=$t failed"; exit 1; }
 done
+# staging copies with plain memcpy (copy_stream=0) beside the default streaming stores
+for t in 1 16; do
+  timeout -k 10 300 python bench.py --workload host --threads $t --no-cpu --tune copy_stream=0 > $O/bench_host_t${t}_memcpy.json 2> $O/bench_host_t${t}_memcpy.err || { echo "host memcpy T=$t failed"; exit 1; }
+done
+timeout -k 10 300 python bench.py --workload queue_pageable --no-cpu --tune copy_stream=0 > $O/bench_queue_pageable_memcpy.json 2> $O/bench_queue_pageable_memcpy.err || { echo "queue_pageable memcpy failed"; exit 1; }
 echo "mixed + host T ok"
 export TMPDIR=/tmp
 cd /tmp

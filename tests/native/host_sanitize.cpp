@@ -134,25 +134,36 @@ static void check_copy() {
       std::vector<ozec::CopyTask> tasks;
       std::vector<std::vector<uint8_t>> src, dst;
       const int ntask = 1 + static_cast<int>(rng() % 5);
+      std::vector<size_t> so, dof;  // misaligned starts: the streaming copy's head / body / tail split
       for (int i = 0; i < ntask; ++i) {
         const size_t n = 1 + rng() % (3u << 20);
-        src.emplace_back(n);
-        dst.emplace_back(n, 0);
-        for (size_t j = 0; j < n; j += 4096) src.back()[j] = static_cast<uint8_t>(rng());
-        src.back()[n - 1] = static_cast<uint8_t>(id + it);
+        so.push_back(rng() % 64);
+        dof.push_back(rng() % 64);
+        src.emplace_back(n + so.back());
+        dst.emplace_back(n + dof.back() + 64, 0);
+        for (size_t j = 0; j < src.back().size(); j += 97) src.back()[j] = static_cast<uint8_t>(rng());
+        src.back()[so.back() + n - 1] = static_cast<uint8_t>(id + it);
       }
-      for (int i = 0; i < ntask; ++i) tasks.push_back({dst[i].data(), src[i].data(), src[i].size()});
-      ozec::parallel_copy(tasks);
       for (int i = 0; i < ntask; ++i)
-        if (dst[i] != src[i]) ++bad;
+        tasks.push_back({dst[i].data() + dof[i], src[i].data() + so[i], src[i].size() - so[i]});
+      ozec::parallel_copy(tasks);
+      for (int i = 0; i < ntask; ++i) {
+        const size_t n = src[i].size() - so[i];
+        if (std::memcmp(dst[i].data() + dof[i], src[i].data() + so[i], n) != 0) ++bad;
+        for (size_t j = 0; j < dof[i]; ++j) bad += dst[i][j] != 0;                   // nothing written before
+        for (size_t j = dof[i] + n; j < dst[i].size(); ++j) bad += dst[i][j] != 0;  // or after the range
+      }
     }
   };
-  for (int threads : {4, 0, 2}) {
-    ozec::set_copy_threads(threads);  // resize the pool between rounds of concurrent callers
-    std::vector<std::thread> ts;
-    for (int c = 0; c < 4; ++c) ts.emplace_back(caller, c);
-    for (auto &t : ts) t.join();
-  }
+  for (int stream : {1, 0})  // streaming stores (where AVX2 exists) and plain memcpy
+    for (int threads : {4, 0, 2}) {
+      ozec::set_copy_stream(stream);
+      ozec::set_copy_threads(threads);  // resize the pool between rounds of concurrent callers
+      std::vector<std::thread> ts;
+      for (int c = 0; c < 4; ++c) ts.emplace_back(caller, c);
+      for (auto &t : ts) t.join();
+    }
+  ozec::set_copy_stream(-1);
   CHECK(bad.load() == 0, "%d parallel copies differ", bad.load());
 }
 
@@ -167,7 +178,7 @@ int main(int argc, char **argv) {
                 g_fail ? "FAILED" : "ok");
   } else {
     check_copy();
-    std::printf("copy: 3 pool sizes x 4 concurrent callers -- %s\n", g_fail ? "FAILED" : "ok");
+    std::printf("copy: 2 store kinds x 3 pool sizes x 4 concurrent callers, misaligned -- %s\n", g_fail ? "FAILED" : "ok");
   }
   return g_fail ? 1 : 0;
 }

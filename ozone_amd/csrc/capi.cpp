@@ -385,7 +385,7 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     const uint8_t *src = s->pinned + c * per_chunk + nin * cp;
     std::vector<ozec::CopyTask> tasks;
     for (int r = 0; r < nout; ++r) tasks.push_back({out[r] + out_pos(off), src + r * op, out_bytes(cl)});
-    ozec::parallel_copy(tasks);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging);
     return OZEC_OK;
   };
   for (size_t c = 0; c < nch; ++c) {
@@ -393,7 +393,7 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     uint8_t *h = s->pinned + c * per_chunk, *d = s->dbuf + c * per_chunk;
     std::vector<ozec::CopyTask> tasks;
     for (int j = 0; j < nin; ++j) tasks.push_back({h + j * cp, in[j] + off, cl});
-    ozec::parallel_copy(tasks);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging);
     OZEC_HIP(hipMemcpyAsync(d, h, nin * cp, hipMemcpyHostToDevice, s->stream));
     OZEC_HIP(launch(d, static_cast<int64_t>(cp), d + nin * cp, static_cast<int64_t>(op), off, cl, s->stream));
     OZEC_HIP(hipMemcpyAsync(h + nin * cp, d + nin * cp, nout * op, hipMemcpyDeviceToHost, s->stream));
@@ -1052,7 +1052,7 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
                            P.hstage[b] + i * dstripe + static_cast<size_t>(k + r) * len, len});
     if (with_crc && !crc_pinned)
       tasks.push_back({h_crcs + s0 * ncrc, P.hstage[b] + dcrc_off, cs * ncrc * sizeof(uint32_t)});
-    ozec::parallel_copy(tasks);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging);
     return OZEC_OK;
   };
   for (size_t c = 0; c < nch; ++c) {
@@ -1068,7 +1068,7 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
           for (int j = 0; j < k; ++j)
             tasks.push_back({P.hstage[b] + i * dstripe + static_cast<size_t>(j) * len,
                              h_in + (s0 + i) * in_stripe_stride + j * in_unit_stride, len});
-        ozec::parallel_copy(tasks);
+        ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging);
       }
     }
     // H2D after the chunk that used this buffer NB chunks ago has left the device.  The host waits for it too
@@ -1390,7 +1390,7 @@ int ozec_reconstruct_crc_host_batch(ozec_coder *dec, const uint8_t *h_in, int64_
     if (!ocrc_pinned)
       tasks.push_back({h_out_crcs + s0 * e * nwin, P.hstage[b] + docrc_off, cs * e * nwin * sizeof(uint32_t)});
     if (!mis_pinned) tasks.push_back({h_mismatch + s0, P.hstage[b] + dmis_off, cs * sizeof(int32_t)});
-    ozec::parallel_copy(tasks);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging);
     return OZEC_OK;
   };
   for (size_t c = 0; c < nch; ++c) {
@@ -1409,7 +1409,7 @@ int ozec_reconstruct_crc_host_batch(ozec_coder *dec, const uint8_t *h_in, int64_
                              h_in + (s0 + i) * in_stripe_stride + u * in_unit_stride, len});
       if (!exp_pinned)
         tasks.push_back({hs + dexp_off, h_expected + s0 * n_all * nwin, cs * n_all * nwin * sizeof(uint32_t)});
-      ozec::parallel_copy(tasks);
+      ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging);
     }
     if (c >= static_cast<size_t>(E2E::NB)) {
       if (!staged) OZEC_HIP(hipEventSynchronize(P.d2h_done[b]));

@@ -19,6 +19,7 @@ namespace ozec {
 namespace {
 
 constexpr size_t kPiece = 256 << 10;
+constexpr int kStreamAuto = 1;  // the default where AVX2 exists
 
 // Streaming copy: every destination line is written whole with non-temporal stores, so the copy costs one read of
 // the source and one write of the destination in DRAM -- a cached store first reads the line it writes (read for
@@ -48,24 +49,24 @@ __attribute__((target("avx2"))) void copy_stream_avx2(void *dst, const void *src
   _mm_sfence();
 }
 
-std::atomic<int> g_stream_mode{-1};  // -1 auto (streaming where AVX2 exists), 0 memcpy, 1 streaming
+// -1 auto, 0 memcpy, 1 streaming stores both ways, 2 streaming stores into staging buffers only (the copies whose
+// destination only the DMA engine reads); auto = the measured default where AVX2 exists (copy_pool.hpp)
+std::atomic<int> g_stream_mode{-1};
 
-bool use_stream() {
+bool use_stream(CopyDir dir) {
   int m = g_stream_mode.load(std::memory_order_relaxed);
-  if (m < 0) {
-    m = __builtin_cpu_supports("avx2") ? 1 : 0;
-    g_stream_mode.store(m, std::memory_order_relaxed);
-  }
-  return m == 1;
+  if (m < 0) m = __builtin_cpu_supports("avx2") ? kStreamAuto : 0;
+  return m == 1 || (m == 2 && dir == CopyDir::kToStaging);
 }
 
-void copy_bytes(void *dst, const void *src, size_t n) {
-  if (n >= 4096 && use_stream()) copy_stream_avx2(dst, src, n);
+void copy_bytes(void *dst, const void *src, size_t n, bool stream) {
+  if (stream && n >= 4096) copy_stream_avx2(dst, src, n);
   else std::memcpy(dst, src, n);
 }
 
 struct Job {
   std::vector<CopyTask> pieces;
+  bool stream = false;
   std::atomic<size_t> next{0};
   std::atomic<size_t> done{0};
   std::mutex mu;
@@ -74,7 +75,7 @@ struct Job {
   // copy pieces until none are left; returns after contributing
   void work() {
     for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
-      copy_bytes(pieces[i].dst, pieces[i].src, pieces[i].n);
+      copy_bytes(pieces[i].dst, pieces[i].src, pieces[i].n, stream);
       if (done.fetch_add(1) + 1 == pieces.size()) {
         std::lock_guard<std::mutex> lk(mu);
         cv.notify_all();
@@ -183,15 +184,17 @@ void set_copy_node(int node) { Pool::get().set_node(node); }
 
 void set_copy_stream(int mode) { g_stream_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0); }
 
-void parallel_copy(const std::vector<CopyTask> &tasks) {
+void parallel_copy(const std::vector<CopyTask> &tasks, CopyDir dir) {
   size_t total = 0;
   for (const CopyTask &t : tasks) total += t.n;
+  const bool stream = use_stream(dir);
   Pool &pool = Pool::get();
   if (pool.size() == 0 || total < 2 * kPiece) {
-    for (const CopyTask &t : tasks) copy_bytes(t.dst, t.src, t.n);
+    for (const CopyTask &t : tasks) copy_bytes(t.dst, t.src, t.n, stream);
     return;
   }
   auto job = std::make_shared<Job>();
+  job->stream = stream;
   for (const CopyTask &t : tasks)
     for (size_t off = 0; off < t.n; off += kPiece)
       job->pieces.push_back({static_cast<char *>(t.dst) + off, static_cast<const char *>(t.src) + off,

@@ -13,14 +13,16 @@ struct CopyTask {
   size_t n;
 };
 
+// kToStaging: into pinned staging memory that only a DMA engine reads next; kFromStaging: into caller memory
+enum class CopyDir { kToStaging, kFromStaging };
 // run every task (in any order) and return when all are done
-void parallel_copy(const std::vector<CopyTask> &tasks);
+void parallel_copy(const std::vector<CopyTask> &tasks, CopyDir dir);
 // threads used besides the caller (0 = copy inline); set by ozec_set_tuning("copy_threads", n)
 void set_copy_threads(int n);
 // bind the pool's workers to the CPUs of a NUMA node (-1: no binding)
 void set_copy_node(int node);
-// pieces copied with streaming (non-temporal) stores: 1 on, 0 plain memcpy, -1 auto (on where AVX2 exists);
-// set by ozec_set_tuning("copy_stream", n)
+// pieces copied with streaming (non-temporal) stores: 1 both directions, 2 into staging only, 0 plain memcpy, -1
+// auto (the measured default where AVX2 exists); set by ozec_set_tuning("copy_stream", n)
 void set_copy_stream(int mode);
 
 }  // namespace ozec

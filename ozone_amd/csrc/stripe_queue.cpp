@@ -216,7 +216,7 @@ struct ozec_stripe_queue {
       if (pd.crcs && ctype != OZEC_CHECKSUM_NONE)
         tasks.push_back({pd.crcs, b.h_crcs + i * units() * nw, units() * nw * sizeof(uint32_t)});
     }
-    ozec::parallel_copy(tasks);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging);
     b.in_flight = false;
     b.n = 0;
     return OZEC_OK;
@@ -398,7 +398,7 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
     tasks.push_back({st, src[j], len});
     src[j] = st;
   }
-  ozec::parallel_copy(tasks);
+  ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging);
   for (int j = 0; j < q->k;) {
     const size_t off = i * q->stripe_bytes() + static_cast<size_t>(j) * q->cell_len;
     int run = 1;

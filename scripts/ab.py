@@ -15,7 +15,8 @@ lib = L.lib()
 for kv in filter(None, os.environ.get("FIX", "").split(",")):  # knobs held fixed for every variant (FIX=k=v,k=v)
     fk, fv = kv.split("=")
     assert lib.ozec_set_tuning(fk.encode(), int(fv)) == 0, kv
-wl = bench.Workload(wl_name, 0, 1, None)
+wl = bench.Workload(wl_name, 0, 1, int(os.environ["STRIPES"]) if os.environ.get("STRIPES") else None,
+                   int(os.environ.get("THREADS", "1")))
 if os.environ.get("ZERO"):  # all-zero data cells: separates data-dependent power/clock effects
     for name in ("units", "data", "blocks"):
         if hasattr(wl, name):

@@ -28,6 +28,10 @@ done
 echo workloads done
 exit 0
 fi
+if [ -n "$CTESTS" ]; then  # the GPU tests of the host-buffer paths (staging copies), before the lines
+  timeout -k 10 600 python -u -m pytest $CTESTS -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_host_paths.log 2>&1 || { echo "host-path tests failed"; tail -30 $O/pytest_host_paths.log; exit 1; }
+  tail -1 $O/pytest_host_paths.log
+fi
 for w in ${CWORKLOADS:-crc verify}; do
   timeout -k 10 300 python bench.py --workload $w > $O/bench_$w.json 2> $O/bench_$w.err || { echo "bench $w failed"; tail $O/bench_$w.err; exit 1; }
 done

@@ -146,7 +146,7 @@ static void check_copy() {
       }
       for (int i = 0; i < ntask; ++i)
         tasks.push_back({dst[i].data() + dof[i], src[i].data() + so[i], src[i].size() - so[i]});
-      ozec::parallel_copy(tasks);
+      ozec::parallel_copy(tasks, (it & 1) ? ozec::CopyDir::kToStaging : ozec::CopyDir::kFromStaging);
       for (int i = 0; i < ntask; ++i) {
         const size_t n = src[i].size() - so[i];
         if (std::memcmp(dst[i].data() + dof[i], src[i].data() + so[i], n) != 0) ++bad;
@@ -155,7 +155,7 @@ static void check_copy() {
       }
     }
   };
-  for (int stream : {1, 0})  // streaming stores (where AVX2 exists) and plain memcpy
+  for (int stream : {1, 2, 0})  // streaming stores both ways / into staging only (where AVX2 exists), plain memcpy
     for (int threads : {4, 0, 2}) {
       ozec::set_copy_stream(stream);
       ozec::set_copy_threads(threads);  // resize the pool between rounds of concurrent callers
@@ -178,7 +178,7 @@ int main(int argc, char **argv) {
                 g_fail ? "FAILED" : "ok");
   } else {
     check_copy();
-    std::printf("copy: 2 store kinds x 3 pool sizes x 4 concurrent callers, misaligned -- %s\n", g_fail ? "FAILED" : "ok");
+    std::printf("copy: 3 store modes x 3 pool sizes x 4 concurrent callers, misaligned -- %s\n", g_fail ? "FAILED" : "ok");
   }
   return g_fail ? 1 : 0;
 }

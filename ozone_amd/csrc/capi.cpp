@@ -379,13 +379,15 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     ~DrainOnExit() { (void)hipStreamSynchronize(st); }
   } drain{s->stream};
   if (int rc = s->reserve(per_chunk * nch, nch)) return rc;
+  // other calls in flight: their copies and DMA share host DRAM with this call's staging copies (copy_pool.hpp)
+  const bool shared = ctx->leased.load() > 1 || nch > 1;
   auto unstage = [&](size_t c) -> int {
     OZEC_HIP(hipEventSynchronize(s->events[c]));
     const size_t off = c * chunk, cl = std::min(chunk, len - off);
     const uint8_t *src = s->pinned + c * per_chunk + nin * cp;
     std::vector<ozec::CopyTask> tasks;
     for (int r = 0; r < nout; ++r) tasks.push_back({out[r] + out_pos(off), src + r * op, out_bytes(cl)});
-    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, shared);
     return OZEC_OK;
   };
   for (size_t c = 0; c < nch; ++c) {
@@ -393,7 +395,7 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     uint8_t *h = s->pinned + c * per_chunk, *d = s->dbuf + c * per_chunk;
     std::vector<ozec::CopyTask> tasks;
     for (int j = 0; j < nin; ++j) tasks.push_back({h + j * cp, in[j] + off, cl});
-    ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, shared);
     OZEC_HIP(hipMemcpyAsync(d, h, nin * cp, hipMemcpyHostToDevice, s->stream));
     OZEC_HIP(launch(d, static_cast<int64_t>(cp), d + nin * cp, static_cast<int64_t>(op), off, cl, s->stream));
     OZEC_HIP(hipMemcpyAsync(h + nin * cp, d + nin * cp, nout * op, hipMemcpyDeviceToHost, s->stream));

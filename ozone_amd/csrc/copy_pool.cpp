@@ -19,7 +19,6 @@ namespace ozec {
 namespace {
 
 constexpr size_t kPiece = 256 << 10;
-constexpr int kStreamAuto = 1;  // the default where AVX2 exists
 
 // Streaming copy: every destination line is written whole with non-temporal stores, so the copy costs one read of
 // the source and one write of the destination in DRAM -- a cached store first reads the line it writes (read for
@@ -50,12 +49,15 @@ __attribute__((target("avx2"))) void copy_stream_avx2(void *dst, const void *src
 }
 
 // -1 auto, 0 memcpy, 1 streaming stores both ways, 2 streaming stores into staging buffers only (the copies whose
-// destination only the DMA engine reads); auto = the measured default where AVX2 exists (copy_pool.hpp)
+// destination only the DMA engine reads).  Auto: streaming stores where AVX2 exists and the copy shares DRAM with
+// other transfers (DMA of other chunks or batches, other callers' copies); a lone caller's copy, with nothing else
+// in flight, runs faster through the cache (same-process A/Bs, profiles/r03/ab/copy_*.log: 1 caller 3.7 % slower
+// with streaming stores, 16 callers 6 % faster, the pageable stripe queue 11 % faster).
 std::atomic<int> g_stream_mode{-1};
 
-bool use_stream(CopyDir dir) {
+bool use_stream(CopyDir dir, bool shared) {
   int m = g_stream_mode.load(std::memory_order_relaxed);
-  if (m < 0) m = __builtin_cpu_supports("avx2") ? kStreamAuto : 0;
+  if (m < 0) m = shared && __builtin_cpu_supports("avx2") ? 1 : 0;
   return m == 1 || (m == 2 && dir == CopyDir::kToStaging);
 }
 
@@ -184,10 +186,10 @@ void set_copy_node(int node) { Pool::get().set_node(node); }
 
 void set_copy_stream(int mode) { g_stream_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0); }
 
-void parallel_copy(const std::vector<CopyTask> &tasks, CopyDir dir) {
+void parallel_copy(const std::vector<CopyTask> &tasks, CopyDir dir, bool shared) {
   size_t total = 0;
   for (const CopyTask &t : tasks) total += t.n;
-  const bool stream = use_stream(dir);
+  const bool stream = use_stream(dir, shared);
   Pool &pool = Pool::get();
   if (pool.size() == 0 || total < 2 * kPiece) {
     for (const CopyTask &t : tasks) copy_bytes(t.dst, t.src, t.n, stream);

@@ -48,16 +48,17 @@ __attribute__((target("avx2"))) void copy_stream_avx2(void *dst, const void *src
   _mm_sfence();
 }
 
-// -1 auto, 0 memcpy, 1 streaming stores both ways, 2 streaming stores into staging buffers only (the copies whose
-// destination only the DMA engine reads).  Auto: streaming stores where AVX2 exists and the copy shares DRAM with
-// other transfers (DMA of other chunks or batches, other callers' copies); a lone caller's copy, with nothing else
-// in flight, runs faster through the cache (same-process A/Bs, profiles/r03/ab/copy_*.log: 1 caller 3.7 % slower
-// with streaming stores, 16 callers 6 % faster, the pageable stripe queue 11 % faster).
+// -1 auto (= 1 where AVX2 exists), 0 memcpy, 1 streaming stores both ways, 2 streaming stores into staging buffers
+// only (the copies whose destination only the DMA engine reads).  Same-process A/Bs on two boxes
+// (profiles/r03/ab/copy*_*.log): 16 callers 6 % / 27 % faster with streaming stores, the pageable stripe queue 11 % /
+// 25 %, one caller 3.7 % slower on one box and 3.6 % faster on the other.  `shared` (a copy that shares DRAM with
+// other transfers) is kept for A/Bs of a policy that streams only then (mode 3).
 std::atomic<int> g_stream_mode{-1};
 
 bool use_stream(CopyDir dir, bool shared) {
   int m = g_stream_mode.load(std::memory_order_relaxed);
-  if (m < 0) m = shared && __builtin_cpu_supports("avx2") ? 1 : 0;
+  if (m < 0) m = __builtin_cpu_supports("avx2") ? 1 : 0;
+  if (m == 3) return shared && __builtin_cpu_supports("avx2");
   return m == 1 || (m == 2 && dir == CopyDir::kToStaging);
 }
 

@@ -155,7 +155,7 @@ static void check_copy() {
       }
     }
   };
-  for (int stream : {1, 2, 0})  // streaming stores both ways / into staging only (where AVX2 exists), plain memcpy
+  for (int stream : {1, 2, 3, 0})  // streaming stores both ways / into staging only / when shared, plain memcpy
     for (int threads : {4, 0, 2}) {
       ozec::set_copy_stream(stream);
       ozec::set_copy_threads(threads);  // resize the pool between rounds of concurrent callers
@@ -178,7 +178,7 @@ int main(int argc, char **argv) {
                 g_fail ? "FAILED" : "ok");
   } else {
     check_copy();
-    std::printf("copy: 3 store modes x 3 pool sizes x 4 concurrent callers, misaligned -- %s\n", g_fail ? "FAILED" : "ok");
+    std::printf("copy: 4 store modes x 3 pool sizes x 4 concurrent callers, misaligned -- %s\n", g_fail ? "FAILED" : "ok");
   }
   return g_fail ? 1 : 0;
 }

@@ -150,8 +150,11 @@ __device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t 
 // dword of its next output block, whose G26 lookups use the set advanced by kXoAdvance bytes; the advance is undone
 // once per window.  Saves R x 7 lookups per step (the input registers keep their D-step shifts: their nibble lookups
 // also yield the GF products, which must see the unmodified data)
+// NF: probe only (wrong results): table regions past the 16-bit offset range are read from the region 32 KiB below
+// instead, with no index OR -- the same LDS traffic without the far-addressing VALU, an upper bound for what
+// removing that VALU could give wide step groups
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
-          int PADV = 0, int PADL = 0, bool XO = false>
+          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -266,9 +269,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
               const int i = 4 * c + q;
               const uint32_t reg = kTB + nb_region<K>(d, j, i);
               uint2 lo, hi;
-              if (reg + 256 <= 65536) {
-                lo = lds64(s_all, reg + nib_lo_idx(xw[c], q, v4));
-                hi = lds64(s_all, reg + 8 + nib_hi_idx(xw[c], q, vf0));
+              if (reg + 256 <= 65536 || NF) {
+                const uint32_t rg = reg + 256 <= 65536 ? reg : reg - 0x8000u;
+                lo = lds64(s_all, rg + nib_lo_idx(xw[c], q, v4));
+                hi = lds64(s_all, rg + 8 + nib_hi_idx(xw[c], q, vf0));
               } else {
                 lo = lds64(s_all, (reg - 0x8000u) + (nib_lo_idx(xw[c], q, v4) | 0x8000u));
                 hi = lds64(s_all, (reg + 8 - 0x8000u) + (nib_hi_idx(xw[c], q, vf0) | 0x8000u));
@@ -356,16 +360,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
-          int PADV = 0, int PADL = 0, bool XO = false>
+          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((DO * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
     constexpr int kNB = (DO * K) % 2 == 0 ? 2 : (DO * K <= K + 1 ? DO * K : 1);
     static_assert(kNB != NB && (DO * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO>(e, st);
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
@@ -515,6 +519,9 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 167: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true>(e, st);
     case 168: return launch_nb<K, R, 2, 2, 14, 4, 2, true, 1, 2, 0, 0, true>(e, st);
     case 169: return launch_nb<K, R, 1, K, 8, 4, 2, true, 1, 1, 0, 0, true>(e, st);
+    // probes (wrong results, NF): the XO D = 2 geometries (rs-10-x: 163 / 161) without the far-addressing VALU
+    case 148: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true, true>(e, st);
+    case 149: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, true>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);

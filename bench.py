@@ -816,6 +816,18 @@ def stream_latency(args):
         enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
         rows[f"encode_stripe_{cell >> 10}KiB_cells"] = {"gpu_us": round(per_call(lambda: enc.encode(d, o)), 1),
                                                        "cpu_us": round(cpu("percall_encode", cell), 1)}
+        # the same call with every cell in pinned memory (ozec_host_alloc; Java: allocatePinned): DMA in place,
+        # no staging copy
+        from ozone_amd.stripe_queue import host_alloc
+        pool = host_alloc((k + p) * cell)
+        dp = [pool.array[i * cell:(i + 1) * cell] for i in range(k + p)]
+        for i in range(k):
+            dp[i][:] = d[i]
+        us = per_call(lambda: enc.encode(dp[:k], dp[k:]))
+        rows[f"encode_stripe_{cell >> 10}KiB_cells_pinned"] = {"gpu_us": round(us, 1),
+                                                              "GBps": round(k * cell / us / 1e3, 2)}
+        del dp
+        pool.free()
     buf = rng.integers(0, 256, 16 << 20, dtype=np.uint8)
     st = ctypes.c_uint32(0xFFFFFFFF)
     cross = None

@@ -62,6 +62,19 @@ struct Slot {
   size_t dbuf_cap = 0;
   std::vector<hipEvent_t> events;
 
+  // device buffer only (calls whose caller buffers are pinned need no staging)
+  int reserve_device(size_t bytes) {
+    if (bytes > dbuf_cap) {
+      if (dbuf) (void)hipFree(dbuf);
+      dbuf = nullptr;
+      dbuf_cap = 0;
+      size_t cap = std::max<size_t>(bytes, 1 << 20);
+      OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&dbuf), cap));
+      dbuf_cap = cap;
+    }
+    return OZEC_OK;
+  }
+
   int reserve(size_t bytes, size_t nevents) {
     if (bytes > pinned_cap) {
       if (pinned) (void)ozec::pinned_free(pinned);
@@ -346,6 +359,20 @@ void encode_rows(const ozec_coder *enc, std::vector<uint8_t> &rows) {
 int out_rows(const ozec_coder *enc) { return enc->codec == OZEC_CODEC_XOR ? 1 : enc->p; }
 
 
+bool host_pinned(const void *p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+// the whole [p, p+n) must be registered / pinned: check its two ends
+bool range_pinned(const void *p, size_t n) {
+  return n == 0 || (host_pinned(p) && host_pinned(static_cast<const uint8_t *>(p) + n - 1));
+}
+
 // Host-buffer job through one staging slot, pipelined in chunks: while the GPU copies / codes / copies back
 // chunk c, this thread stages chunk c+1 (pageable -> pinned) and unstages chunk c-1 (pinned -> pageable).
 // Chunk-major staging layout, chunk c at c * per_chunk: [nin inputs x Cp][nout outputs x Op].
@@ -378,6 +405,23 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     hipStream_t st;
     ~DrainOnExit() { (void)hipStreamSynchronize(st); }
   } drain{s->stream};
+  // Caller buffers that are all pinned (ozec_host_alloc / ozec_host_register; Java: OzecNative.allocatePinned) are
+  // DMA'd in place: no staging copy and no chunking, one H2D per input, one kernel, one D2H per output
+  bool direct = true;
+  for (int j = 0; j < nin && direct; ++j) direct = range_pinned(in[j], len);
+  for (int r = 0; r < nout && direct; ++r) direct = range_pinned(out[r] + out_pos(0), out_bytes(len));
+  if (direct) {
+    const size_t dcp = round_up(len, kStageAlign), dop = round_up(out_bytes(len), kStageAlign);
+    if (int rc = s->reserve_device(nin * dcp + nout * dop)) return rc;
+    uint8_t *d = s->dbuf;
+    for (int j = 0; j < nin; ++j) OZEC_HIP(hipMemcpyAsync(d + j * dcp, in[j], len, hipMemcpyHostToDevice, s->stream));
+    OZEC_HIP(launch(d, static_cast<int64_t>(dcp), d + nin * dcp, static_cast<int64_t>(dop), 0, len, s->stream));
+    for (int r = 0; r < nout; ++r)
+      OZEC_HIP(hipMemcpyAsync(out[r] + out_pos(0), d + nin * dcp + r * dop, out_bytes(len), hipMemcpyDeviceToHost,
+                              s->stream));
+    OZEC_HIP(hipStreamSynchronize(s->stream));
+    return OZEC_OK;
+  }
   if (int rc = s->reserve(per_chunk * nch, nch)) return rc;
   // other calls in flight: their copies and DMA share host DRAM with this call's staging copies (copy_pool.hpp)
   const bool shared = ctx->leased.load() > 1 || nch > 1;
@@ -946,24 +990,6 @@ int ozec_encode_crc_block_groups(ozec_coder *enc, uint8_t *d_base, int64_t group
 }
 
 // ---- end-to-end batch from host memory ----------------------------------------
-
-namespace {
-
-bool host_pinned(const void *p) {
-  hipPointerAttribute_t at;
-  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return at.type == hipMemoryTypeHost;
-}
-
-// the whole [p, p+n) must be registered / pinned: check its two ends
-bool range_pinned(const void *p, size_t n) {
-  return n == 0 || (host_pinned(p) && host_pinned(static_cast<const uint8_t *>(p) + n - 1));
-}
-
-}  // namespace
 
 int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_stripe_stride,
                                int64_t in_unit_stride, uint8_t *h_out, int64_t out_stripe_stride,

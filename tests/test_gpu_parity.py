@@ -797,6 +797,48 @@ def test_host_path_chunked_pipeline(chunk, copy_threads):
         L.lib().ozec_set_tuning(b"copy_threads", 3)
 
 
+@pytest.mark.parametrize("codec,k,p,n", [("rs", 6, 3, 1 << 20), ("rs", 10, 4, 300_001), ("xor", 2, 1, 65536 + 7)])
+def test_host_path_pinned_buffers_dma_in_place(codec, k, p, n):
+    """Caller buffers that are all pinned (ozec_host_alloc) are DMA'd in place with no staging copy; one pageable
+    buffer among them sends the call through the staging pipeline.  Encode, decode and per-window CRCs, both ways,
+    at misaligned offsets inside the pinned allocations -- vs the oracle."""
+    from ozone_amd.stripe_queue import host_alloc
+    rows = p if codec == "rs" else 1
+    data = cells(SEED, 96000 + k, k, n)
+    ref = oracle.rs_encode(k, p, data) if codec == "rs" else [oracle.xor_encode(data)]
+    pool = host_alloc((k + 2 * rows + 2) * (n + 64))
+    views = [pool.array[i * (n + 64) + 3 + i: i * (n + 64) + 3 + i + n] for i in range(k + 2 * rows + 2)]
+    ins = views[:k]
+    for a, b in zip(ins, data):
+        a[:] = b
+    for mixed in (False, True):
+        par = [v for v in views[k:k + rows]]
+        for v in par:
+            v[:] = 0xA5
+        if mixed:
+            par[0] = np.full(n, 0xA5, np.uint8)  # pageable
+        e = enc(codec, k, p)
+        e.encode(ins, par + [np.zeros(n, np.uint8) for _ in range(p - rows)])
+        assert all((a == b).all() for a, b in zip(par, ref)), mixed
+        # decode two units (one for XOR) from pinned survivors into pinned outputs
+        erased = [0, k] if codec == "rs" else [1]
+        units = list(ins) + list(views[k:k + rows])
+        for i, r in enumerate(ref):
+            units[k + i][:] = r
+        dins = [None if u in erased else units[u] for u in range(k + rows)] + [None] * (p - rows)
+        outs = [views[k + rows + i] for i in range(len(erased))]
+        if mixed:
+            outs[0] = np.zeros(n, np.uint8)
+        dec(codec, k, p).decode(dins, erased, outs)
+        truth = list(data) + ref
+        assert all((o == truth[u]).all() for o, u in zip(outs, erased)), mixed
+    bpc = 16384
+    cd = ck.Checksum(ck.ChecksumType.CRC32C, bpc).compute_checksum(ins[1])
+    got = [int.from_bytes(b, "big") for b in cd.get_checksums()]
+    assert got == [int(x) for x in oracle.crc_windows(oracle.CRC32C, data[1], bpc)]
+    pool.free()
+
+
 def test_encode_crc_batch_xor_p2_zero_fills_extra_parity():
     """the fused batch path resets XOR outputs past the first, like ozec_encode_batch and
     XORRawEncoder (XORRawEncoder.java:67-85)."""

@@ -406,19 +406,47 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     ~DrainOnExit() { (void)hipStreamSynchronize(st); }
   } drain{s->stream};
   // Caller buffers that are all pinned (ozec_host_alloc / ozec_host_register; Java: OzecNative.allocatePinned) are
-  // DMA'd in place: no staging copy and no chunking, one H2D per input, one kernel, one D2H per output
-  bool direct = true;
-  for (int j = 0; j < nin && direct; ++j) direct = range_pinned(in[j], len);
-  for (int r = 0; r < nout && direct; ++r) direct = range_pinned(out[r] + out_pos(0), out_bytes(len));
+  // DMA'd in place: no staging copy and no chunking.  Units at one constant stride (a buffer pool's cells) go up and
+  // come back as one rectangular copy each way; otherwise one copy per unit, which pays only for large cells (each
+  // copy is a stream operation of ~10 us; the staging path moves all units in one)
+  auto stride_of = [](const uint8_t *const *b, int n, size_t w, int64_t *st) {
+    *st = n > 1 ? b[1] - b[0] : static_cast<int64_t>(w);
+    if (*st < static_cast<int64_t>(w)) return false;
+    for (int i = 2; i < n; ++i)
+      if (b[i] - b[i - 1] != *st) return false;
+    return true;
+  };
+  int64_t sin = 0, sout = 0;
+  const size_t obytes = out_bytes(len);
+  std::vector<const uint8_t *> obase(nout);
+  for (int r = 0; r < nout; ++r) obase[r] = out[r] + out_pos(0);
+  const bool rect = stride_of(in, nin, len, &sin) && stride_of(obase.data(), nout, obytes, &sout);
+  bool direct = rect || len >= (256u << 10);
+  if (rect && direct) {
+    direct = range_pinned(in[0], static_cast<size_t>(sin) * (nin - 1) + len) &&
+             range_pinned(obase[0], static_cast<size_t>(sout) * (nout - 1) + obytes);
+  } else {
+    for (int j = 0; j < nin && direct; ++j) direct = range_pinned(in[j], len);
+    for (int r = 0; r < nout && direct; ++r) direct = range_pinned(obase[r], obytes);
+  }
   if (direct) {
-    const size_t dcp = round_up(len, kStageAlign), dop = round_up(out_bytes(len), kStageAlign);
+    const size_t dcp = round_up(len, kStageAlign), dop = round_up(obytes, kStageAlign);
     if (int rc = s->reserve_device(nin * dcp + nout * dop)) return rc;
     uint8_t *d = s->dbuf;
-    for (int j = 0; j < nin; ++j) OZEC_HIP(hipMemcpyAsync(d + j * dcp, in[j], len, hipMemcpyHostToDevice, s->stream));
+    if (rect) {
+      OZEC_HIP(hipMemcpy2DAsync(d, dcp, in[0], static_cast<size_t>(sin), len, nin, hipMemcpyHostToDevice, s->stream));
+    } else {
+      for (int j = 0; j < nin; ++j) OZEC_HIP(hipMemcpyAsync(d + j * dcp, in[j], len, hipMemcpyHostToDevice, s->stream));
+    }
     OZEC_HIP(launch(d, static_cast<int64_t>(dcp), d + nin * dcp, static_cast<int64_t>(dop), 0, len, s->stream));
-    for (int r = 0; r < nout; ++r)
-      OZEC_HIP(hipMemcpyAsync(out[r] + out_pos(0), d + nin * dcp + r * dop, out_bytes(len), hipMemcpyDeviceToHost,
-                              s->stream));
+    if (rect) {
+      OZEC_HIP(hipMemcpy2DAsync(const_cast<uint8_t *>(obase[0]), static_cast<size_t>(sout), d + nin * dcp, dop, obytes,
+                                nout, hipMemcpyDeviceToHost, s->stream));
+    } else {
+      for (int r = 0; r < nout; ++r)
+        OZEC_HIP(hipMemcpyAsync(const_cast<uint8_t *>(obase[r]), d + nin * dcp + r * dop, obytes, hipMemcpyDeviceToHost,
+                                s->stream));
+    }
     OZEC_HIP(hipStreamSynchronize(s->stream));
     return OZEC_OK;
   }

@@ -69,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--e2e-steps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0, help="C5: stripes per pipelined chunk (0 = library default)")
     ap.add_argument("--threads", type=int, default=1, help="host workload: caller threads sharing one coder")
+    ap.add_argument("--host-pinned", action="store_true",
+                    help="host workload: every caller's cells in pinned memory (ozec_host_alloc): DMA in place")
     ap.add_argument("--queue-batch", type=int, default=32, help="queue workloads: stripes per GPU batch")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="ozec_set_tuning knob (A/B and profiling runs only; defaults are the measured best)")
@@ -180,16 +182,28 @@ class Workload:
             k, p, S = 6, 3, stripes_override or 64
             T = max(1, threads)
             rng = np.random.default_rng(rank)
-            self.hd = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for _ in range(T)]
-            self.hp = [[np.empty(n, np.uint8) for _ in range(p)] for _ in range(T)]
+            if HOST_PINNED:  # one pinned pool per caller, its cells at one stride (a writer's buffer pool)
+                from ozone_amd.stripe_queue import host_alloc
+                self._pools = [host_alloc((k + p) * n) for _ in range(T)]
+                cellv = [[pl.array[i * n:(i + 1) * n] for i in range(k + p)] for pl in self._pools]
+                for t in range(T):
+                    for i in range(k):
+                        cellv[t][i][:] = rng.integers(0, 256, n, dtype=np.uint8)
+                self.hd = [cv[:k] for cv in cellv]
+                self.hp = [cv[k:] for cv in cellv]
+            else:
+                self.hd = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for _ in range(T)]
+                self.hp = [[np.empty(n, np.uint8) for _ in range(p)] for _ in range(T)]
             self.k, self.p, self.S = k, p, S
             enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
             self.data_bytes = S * k * n
             self.alg_bytes = S * (k + p) * n
             self.kernel = "gf_code_vec<6,3> (+pageable->pinned staging, H2D, D2H, per stripe)"
             self.config = {"workload": f"rs-6-3-1024k encode through the host-pointer ABI (ozec_encode: the JNI "
-                                       f"drop-in path), {S} single-stripe calls from {T} threads sharing one coder",
-                           "stripes": S, "threads": T}
+                                       f"drop-in path), {S} single-stripe calls from {T} threads sharing one coder"
+                                       + (", cells in pinned memory (DMA in place)" if HOST_PINNED else
+                                          ", cells in pageable memory (staged)"),
+                           "stripes": S, "threads": T, "pinned": HOST_PINNED}
 
             def run(t):
                 for _ in range(t, S, T):
@@ -701,6 +715,8 @@ def cpu_baseline(workload, budget_s):
 
 # ------------------------------------------------------------------------------------------ live PMC traffic
 
+HOST_PINNED = False  # --host-pinned (host workload)
+
 KERNEL_PAT = {"c1": "gf_code_vec<3, 2", "c2": "gf_code_vec<6, 3", "c3": "gf_code_vec<10, 4",
               "c3r": ("encode_crc_nb<10, 4", "encode_crc_lv<10, 4", "encode_crc_g26<10, 4"), "c4": "encode_crc_g26<2, 1",
               "c4s": "encode_crc_g26<2, 1", "c5dev": ("encode_crc_nb<6, 3", "encode_crc_lv<6, 3", "encode_crc_g26<6, 3"),
@@ -989,6 +1005,8 @@ def main():
                   "calls": stream_latency(args)})
         return 0
 
+    global HOST_PINNED
+    HOST_PINNED = bool(args.host_pinned)
     wl = Workload(args.workload, rank, world, args.stripes, args.threads, erased, args.queue_batch)
 
     def barrier():

@@ -288,10 +288,13 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // by the WorkQueue -- rs-10-x 150 (62's geometry; C3r 64.8 % vs 63.7 % for 102, 62.5 % for 62), rs-3-x 163
   // (two-step groups in 16-wave workgroups), rs-6-x 167 (163 with a ring of 3 input blocks; C5dev 68.4 % for 163 vs
   // 67.2 % for 87 on one box, 66.9 % for 167 vs 66.2 % for 163 on another); without a counter slot the same kernels
-  // on a one-wave-per-window grid (151 / 152)
+  // on a one-wave-per-window grid (151 / 152).  Since the last round-3 build the window CRCs leave through one
+  // lane-parallel store / compare (EM: 170 = 150, 171 = 167, 172 = 163, 173 = 151, 174 = 152 with it; K + R fewer
+  // divergent blocks per window, SGPR spills 104 -> 12 for rs-10-4): C3r 5.711 -> 5.582 ms, C5dev 6.956 -> 6.911 ms,
+  // every fallback faster too (profiles/r03/em/ab_*.log, 7 rounds)
   const bool queue = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) && nb_work_slot(st) != nullptr;
-  if (v == 0) v = k == 10 ? (queue ? 150 : 151) : !queue ? 152 : k == 6 ? 167 : 163;
-  if (v >= 60 && v < 170) {
+  if (v == 0) v = k == 10 ? (queue ? 170 : 173) : !queue ? 174 : k == 6 ? 171 : 172;
+  if (v >= 60 && v < 180) {
     if (k == 6 && r == 3) return launch_nb_6_3(e, st, v);
     if (k == 6 && r == 2) return launch_nb_6_2(e, st, v);
     if (k == 3 && r == 2) return launch_nb_3_2(e, st, v);

@@ -134,6 +134,29 @@ __device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t 
   }
 }
 
+// The same from every emitting lane at once (EM variants): `q` is the lane's unit (a VGPR), the address is computed
+// in the VALU and one store (or one compare) serves all units, instead of K + R divergent blocks with scalar
+// address math, one per unit.  The lane's input unit comes from a select chain over the kernarg array (static
+// indices only, so the array stays in SGPRs).
+template <int K, int R>
+__device__ __forceinline__ void nb_emit_lane(const EncCrcArgs &e, int64_t s, int64_t w, int q, uint32_t v,
+                                             uint32_t init) {
+  const CrcArgs &cr = e.crc;
+  const int64_t nwin = cr.nwin;
+  if (!e.verify) {
+    cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+  } else if (q >= K) {
+    cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
+  } else if (cr.expected) {
+    int32_t unit = e.in_unit[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) unit = q == j ? e.in_unit[j] : unit;
+    const int64_t idx = (s * e.exp_units + unit) * nwin + w;
+    const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
+    if (crc_finish(v, init, 0, 0) != ex) atomicMin(cr.mismatch + s, static_cast<int32_t>(unit * nwin + w));
+  }
+}
+
 // K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
 // FENCE: dwords of a block whose lookups go between scheduling fences (2: halves, at most 16 results live; 1:
 // quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree;
@@ -153,8 +176,9 @@ __device__ __forceinline__ void nb_emit(const EncCrcArgs &e, int64_t s, int64_t 
 // NF: probe only (wrong results): table regions past the 16-bit offset range are read from the region 32 KiB below
 // instead, with no index OR -- the same LDS traffic without the far-addressing VALU, an upper bound for what
 // removing that VALU could give wide step groups
+// EM: the window CRCs leave through nb_emit_lane (one lane-parallel store / compare) instead of K + R unit blocks
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
-          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false>
+          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false, bool EM = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -342,7 +366,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     if constexpr (RS) {
       int q = 0;
       const uint32_t v = g5_lane_tree_rs<K + R>(s_t + kTree - kG5Tree, S, lane, q);
-      if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
+      if constexpr (EM) {
+        if (lane < tree_np(K + R) && q < K + R) nb_emit_lane<K, R>(e, s, w, q, v, init);
+      } else if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
 #pragma unroll
         for (int qq = 0; qq < K + R; ++qq)
           if (q == qq) nb_emit<K, R>(e, s, w, qq, v, init);
@@ -360,16 +386,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
-          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false>
+          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false, bool EM = false>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((DO * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
     constexpr int kNB = (DO * K) % 2 == 0 ? 2 : (DO * K <= K + 1 ? DO * K : 1);
     static_assert(kNB != NB && (DO * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF>(e, st);
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF, EM>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF, EM>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
@@ -522,6 +548,12 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     // probes (wrong results, NF): the XO D = 2 geometries (rs-10-x: 163 / 161) without the far-addressing VALU
     case 148: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true, true>(e, st);
     case 149: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, true>(e, st);
+    // the XO defaults (150 / 167 / 163) and their non-persistent fallbacks (151 / 152) with the lane-parallel emit
+    case 170: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, 1, 0, 0, true, false, true>(e, st);
+    case 171: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true>(e, st);
+    case 172: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true, false, true>(e, st);
+    case 173: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 0, true, false, true>(e, st);
+    case 174: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 0, true, false, true>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);

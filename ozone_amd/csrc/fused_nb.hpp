@@ -177,8 +177,13 @@ __device__ __forceinline__ void nb_emit_lane(const EncCrcArgs &e, int64_t s, int
 // instead, with no index OR -- the same LDS traffic without the far-addressing VALU, an upper bound for what
 // removing that VALU could give wide step groups
 // EM: the window CRCs leave through nb_emit_lane (one lane-parallel store / compare) instead of K + R unit blocks
+// H (< K, XO with D = 2 only): only inputs 0..H-1 get the second distance set (K + H instead of 2K tables of 4 KiB, so
+// rs-10-x two-step groups fit two workgroups per CU); inputs H..K-1 are looked up in set 0 and shifted by one step
+// after every step (table at kSh1), inputs 0..H-1 by two at the group end
+// LT (with H < K): the lane-tree shifts (used once per window) move behind the nibble tables, so that 5.3 KiB more of
+// the tables stay inside the 16-bit ds_read offset range (fewer index ORs)
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
-          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false, bool EM = false>
+          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false, bool EM = false, int H = K, bool LT = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -186,21 +191,27 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   static_assert((DO * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
   static_assert(DO % D == 0 && DO <= 4, "output groups of whole input groups; windows are multiples of 4 steps");
   static_assert(!XO || DO == D, "with XO the output registers are not grouped");
+  static_assert(H == K || (XO && D == 2 && H >= 0 && H < K), "partial second distance set: XO, two-step groups");
+  constexpr int kSets = K + (D - 1) * H;  // (d, j) nibble tables of 4 KiB: all K inputs in set 0, inputs < H in sets >= 1
   // one LDS block: G26 blob of DO sets (+ the D-step register shift when D < DO), then the (d, j, p) nibble tables,
   // then the GF dwords of the setup.  Table regions past the 16-bit ds_read offset range are reached with bit 15 set
   // in the index register (one v_or_b32).  XO: the input-register shift and the lane-tree shifts of the G26 blob,
   // then the XO blob, instead of the G26 sets
-  constexpr uint32_t kXoOff = 224 + 1344;  // XO: word offset of the XO blob
+  static_assert(!LT || (XO && H < K), "late lane-tree tables only with a partial second distance set");
+  constexpr uint32_t kXoOff = LT ? 224 + 224 : 224 + 1344;  // XO: word offset of the XO blob
   constexpr uint32_t kShIn = XO ? 0 : DO == D ? g26_gshift(D) : g26_words(DO);  // word offset of the input-register shift
-  constexpr uint32_t kTree = XO ? 224 : g26_tree(DO);                           // and of the lane-tree shifts
-  constexpr uint32_t kTW = XO ? kXoOff + kXoWords : g26_words(DO) + (DO == D ? 0 : 224);
+  constexpr uint32_t kTree = XO ? 224 : g26_tree(DO);  // and of the lane-tree shifts (LT: behind the tables)
+  constexpr uint32_t kSh1 = LT ? 224 : kXoOff + kXoWords;  // H < K: one-step register shift (inputs H..K-1)
+  constexpr uint32_t kTW = LT ? kXoOff + kXoWords
+                              : XO ? kXoOff + kXoWords + (H < K ? 224 : 0) : g26_words(DO) + (DO == D ? 0 : 224);
   constexpr uint32_t kTB = (kTW * 4 + 255) / 256 * 256;  // nibble tables
-  constexpr uint32_t kLds = kTB + K * D * 4096 + K * 32 * 4;
+  constexpr uint32_t kLds = kTB + kSets * 4096 + K * 32 * 4 + (LT ? 1344 * 4 : 0);
   static_assert(kLds <= 160 * 1024, "LDS per workgroup");
   __shared__ __attribute__((aligned(256))) uint8_t s_all[kLds];
   uint32_t *const s_t = reinterpret_cast<uint32_t *>(s_all);
   uint2 *const s_c = reinterpret_cast<uint2 *>(s_all + kTB);
-  uint32_t *const s_gf = reinterpret_cast<uint32_t *>(s_all + kTB + K * D * 4096);
+  uint32_t *const s_gf = reinterpret_cast<uint32_t *>(s_all + kTB + kSets * 4096);
+  uint32_t *const s_tree = LT ? s_gf + K * 32 : s_t + kTree;  // lane-tree shifts
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
   for (int t = threadIdx.x; t < K * 32; t += blockDim.x) {
@@ -210,15 +221,21 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     for (int r = 0; r < R; ++r) dw |= gf_mul_byte(a.coef[r * K + j], static_cast<uint32_t>(n) << (4 * h)) << (8 * r);
     s_gf[t] = dw;
   }
-  if constexpr (XO) {
+  if constexpr (LT) {
+    load_tables(s_t, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224);
+    load_tables(s_tree, cr.g26[g26_slot(1, D)] + g26_tree(D), 1344);
+    load_tables(s_t + kXoOff, cr.xo, kXoWords);
+    load_tables(s_t + kSh1, cr.g26[g26_slot(1, 1)] + g26_gshift(1), 224);
+  } else if constexpr (XO) {
     load_tables(s_t, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224 + 1344);
     load_tables(s_t + kXoOff, cr.xo, kXoWords);
+    if constexpr (H < K) load_tables(s_t + kSh1, cr.g26[g26_slot(1, 1)] + g26_gshift(1), 224);
   } else {
     load_tables(s_t, cr.g26[g26_slot(1, DO)], g26_words(DO));
     if constexpr (DO != D) load_tables(s_t + kShIn, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224);
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < K * D * 512; q += blockDim.x) {
+  for (int q = threadIdx.x; q < kSets * 512; q += blockDim.x) {
     const int t = q >> 4, n = q & 15, p = t & 31, dj = t >> 5, j = dj % K, d = dj / K;
     const uint32_t off = static_cast<uint32_t>((t >> 1) * 256 + n * 16 + (t & 1) * 8);
     s_c[off >> 3] = make_uint2(s_gf[j * 32 + (p & 1) * 16 + n], cr.nib[(d * 32 + p) * 16 + n]);
@@ -291,7 +308,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int i = 4 * c + q;
-              const uint32_t reg = kTB + nb_region<K>(d, j, i);
+              const uint32_t reg = kTB + nb_region<K>(j < H ? d : 0, j, i);
               uint2 lo, hi;
               if (reg + 256 <= 65536 || NF) {
                 const uint32_t rg = reg + 256 <= 65536 ? reg : reg - 0x8000u;
@@ -347,6 +364,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             px[i & 3] ^= reinterpret_cast<volatile uint32_t *>(s_t)[(lane + 7 * i) & 31];
           asm volatile("" ::"v"(px[0]), "v"(px[1]), "v"(px[2]), "v"(px[3]));
         }
+        if constexpr (H < K) {
+          if (rr + 1 < D) {
+#pragma unroll
+            for (int q = H; q < K; ++q) S[q] = g5_shift(s_t + kSh1, S[q]);
+          }
+        }
         if (DO != D && rr % D == D - 1 && rr + 1 < DO) {  // input groups ending inside the output group
 #pragma unroll
           for (int q = 0; q < K; ++q) S[q] = g5_shift(s_t + kShIn, S[q]);
@@ -354,7 +377,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
       }
       if (g + 1 < G) {
 #pragma unroll
-        for (int q = 0; q < (XO ? K : K + R); ++q) S[q] = g5_shift(s_t + (q < K ? kShIn : g26_gshift(DO)), S[q]);
+        for (int q = 0; q < (XO ? K : K + R); ++q)
+          S[q] = g5_shift(s_t + (q < H ? kShIn : q < K ? kSh1 : g26_gshift(DO)), S[q]);
       }
     }
     const bool last = w == nwin - 1;
@@ -365,7 +389,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     }
     if constexpr (RS) {
       int q = 0;
-      const uint32_t v = g5_lane_tree_rs<K + R>(s_t + kTree - kG5Tree, S, lane, q);
+      const uint32_t v = g5_lane_tree_rs<K + R>(s_tree - kG5Tree, S, lane, q);
       if constexpr (EM) {
         if (lane < tree_np(K + R) && q < K + R) nb_emit_lane<K, R>(e, s, w, q, v, init);
       } else if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
@@ -376,7 +400,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     } else {
 #pragma unroll
       for (int q = 0; q < K + R; ++q) {
-        const uint32_t v = g5_lane_tree(s_t + kTree - kG5Tree, S[q], lane);
+        const uint32_t v = g5_lane_tree(s_tree - kG5Tree, S[q], lane);
         if (lane == q) nb_emit<K, R>(e, s, w, q, v, init);
       }
     }
@@ -386,16 +410,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
-          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false, bool EM = false>
+          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false, bool EM = false, int H = K, bool LT = false>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((DO * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
     constexpr int kNB = (DO * K) % 2 == 0 ? 2 : (DO * K <= K + 1 ? DO * K : 1);
     static_assert(kNB != NB && (DO * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF, EM>(e, st);
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF, EM, H, LT>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF, EM>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF, EM, H, LT>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
@@ -433,6 +457,10 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
   constexpr int kNB = K % 2 == 0 && K > 2 ? K / 2 : K;                    // a deeper ring dividing the group
   constexpr auto lds_of = [](int d) { return (g26_words(d) * 4 + 255) / 256 * 256 + K * d * 4096 + K * 128; };
   constexpr int kDmax = lds_of(4) <= 160 * 1024 ? 4 : lds_of(2) <= 160 * 1024 ? 2 : 1;  // one workgroup per CU
+  // partial second distance sets (XO, D = 2): the XO blob ahead of the tables is (224 + 1344 + 1056 + 224) words
+  constexpr int kXoTB = ((224 + 1344 + kXoWords + 224) * 4 + 255) / 256 * 256;
+  constexpr int kHp = std::max(0, std::min(K - 1, (65536 - kXoTB) / 4096 - K));
+  constexpr int kHh = K / 2;
   switch (v) {
     case 61: return launch_nb<K, R, 1, 2, 8, 4>(e, st);
     case 62: return launch_nb<K, R, 1, kNB, 8, 4>(e, st);
@@ -554,6 +582,22 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 172: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true, false, true>(e, st);
     case 173: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 0, true, false, true>(e, st);
     case 174: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 0, true, false, true>(e, st);
+    // two-step groups with the second distance set for the first H inputs only (kHp: the most whose tables stay in
+    // the 16-bit ds_read offset range; kHh: half the inputs), the rest shifted every step; 8-wave workgroups (two per
+    // CU by LDS) on the 170 geometry, and 16-wave workgroups
+    case 175: return launch_nb<K, R, 2, kNB, 8, 4, 2, true, 1, 2, 0, 0, true, false, true, kHp>(e, st);
+    case 176: return launch_nb<K, R, 2, kNB, 8, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh>(e, st);
+    case 177: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh>(e, st);
+    case 178: return launch_nb<K, R, 2, 2, 8, 4, 2, true, 1, 2, 0, 0, true, false, true, kHp>(e, st);
+    // 16-wave workgroups (measured faster than 8 for two-step groups) over H = kHp, kHh with a ring of 2, K - 3
+    case 179: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, kHp>(e, st);
+    case 180: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh>(e, st);
+    case 181: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, std::max(1, K - 3)>(e, st);
+    case 182: return launch_nb<K, R, 2, kNB, 12, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh>(e, st);
+    // the same with the lane-tree tables behind the nibble tables (LT): 177, 181, and H = kHh + 1
+    case 183: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh, true>(e, st);
+    case 184: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, std::max(1, K - 3), true>(e, st);
+    case 185: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, std::min(K - 1, kHh + 1), true>(e, st);
     default: break;
   }
   return launch_nb<K, R, 1, 2, 8, 4>(e, st);

@@ -5,7 +5,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=$R/gpurun_out/${OUT:-r3em}; mkdir -p $O
 export PYTHONPATH=$R:$R/tests/golden
 if [ -z "$SKIP_TESTS" ]; then
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu -k "17" \
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu -k "${KSEL:-17}" \
   tests/test_gpu_parity.py::test_encode_crc_nibble_kernel_vs_oracle tests/test_gpu_parity.py::test_encode_crc_rs63_variants_vs_oracle \
   tests/test_gpu_parity.py::test_encode_crc_other_shapes_variants_vs_oracle tests/test_gpu_next.py::test_reconstruct_crc_batch \
   > $O/pytest_em.log 2>&1 || { tail -30 $O/pytest_em.log; exit 1; }

@@ -9,7 +9,7 @@ for w in c3r c5dev; do
 done
 timeout -k 10 300 python bench.py --workload c3r --erased 1,4,10,13 > $O/bench_c3r_mixed.json 2> $O/bench_c3r_mixed.err || { echo "c3r mixed failed"; exit 1; }
 echo lines ok
-timeout -k 10 300 python -u scripts/ab.py c3r crc_variant 0,150,102,62,173 6 > $O/ab_c3r_defaults.log 2>&1 || { tail $O/ab_c3r_defaults.log; exit 1; }
+timeout -k 10 300 python -u scripts/ab.py c3r crc_variant 0,170,150,102,173 6 > $O/ab_c3r_defaults.log 2>&1 || { tail $O/ab_c3r_defaults.log; exit 1; }
 timeout -k 10 300 python -u scripts/ab.py c5dev crc_variant 0,167,163,87,174 6 > $O/ab_c5dev_defaults.log 2>&1 || { tail $O/ab_c5dev_defaults.log; exit 1; }
 grep -h '"wl"' $O/ab_c3r_defaults.log $O/ab_c5dev_defaults.log
 export TMPDIR=/tmp

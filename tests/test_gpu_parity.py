@@ -407,7 +407,7 @@ def test_encode_crc_xor_free_shift_vs_oracle(variant, k, n, bpc, S, ctype, otype
             assert (crcs[s, u] == oracle.crc_windows(otype, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [61, 63, 100, 101, 150, 151, 152, 170, 171, 172, 173, 174])
+@pytest.mark.parametrize("variant", [61, 63, 100, 101, 150, 151, 152, 170, 171, 172, 173, 174, 175, 176, 177, 178, 179, 180, 181, 182, 183, 184, 185])
 @pytest.mark.parametrize("k,p,n,bpc,S", [(6, 3, 1 << 17, 16384, 3), (10, 4, 1 << 16, 4096, 2), (3, 2, 1 << 17, 8192, 3),
                                          (6, 2, 1 << 15, 32768, 2), (10, 1, 1 << 16, 16384, 2)])
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
@@ -473,7 +473,7 @@ def test_encode_crc_work_queue_any_grid_and_streams(variant, grid):
                                      61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 86, 87, 88, 89, 93, 94, 95,
                                      100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, 111, 112, 113, 114, 120, 121, 122, 123, 130, 131, 132, 133, 134, 135,
                                      150, 151, 152, 153, 154, 155, 156, 157, 158, 159, 160, 161, 162, 163, 164, 165, 166, 167, 168, 169,
-                                     170, 171, 172, 173, 174])
+                                     170, 171, 172, 173, 174, 175, 176, 177, 178, 179, 180, 181, 182, 183, 184, 185])
 @pytest.mark.parametrize("n,bpc,S", [(1 << 18, 16384, 3), (50000, 4096, 2), (1 << 17, 4096, 2), (1 << 17, 65536, 3)])
 def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
     """Every tuning variant of the rs-6-3 fused encode + CRC32C kernel (per-window kernel: D = 4, prefetch, table
@@ -504,7 +504,7 @@ def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
 @pytest.mark.parametrize("variant", [0, 11, 17, 49, 51, 54, 55, 57, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 86, 87, 88, 89, 93, 94, 95,
                                      100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, 111, 112, 113, 114, 120, 121, 122, 123, 130, 131, 132, 133, 134, 135,
                                      150, 151, 152, 153, 154, 155, 156, 157, 158, 159, 160, 161, 162, 163, 164, 165, 166, 167, 168, 169,
-                                     170, 171, 172, 173, 174])
+                                     170, 171, 172, 173, 174, 175, 176, 177, 178, 179, 180, 181, 182, 183, 184, 185])
 @pytest.mark.parametrize("k,p", [(10, 4), (6, 2), (3, 2), (10, 3), (10, 2), (10, 1)])
 def test_encode_crc_other_shapes_variants_vs_oracle(variant, k, p):
     """Fused encode + CRC32C variants of the other RS shapes (D = 2 default, D = 4, D = 4 with fenced halves)."""

@@ -333,11 +333,16 @@ int ozec_stats(int op, ozec_op_stats *out);
 void ozec_stats_reset(void);
 
 /* ---- harness utilities ------------------------------------------------------------------------------- */
-/* process-wide tuning knobs for benchmarking: kernels ("grid", "gf_variant", "crc_variant", "crc_grid",
- * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_chunk_shared"
- * the same while other host-buffer calls are in flight (0: always host_chunk), "host_slots", "copy_threads" =
- * helper threads for pageable <-> pinned copies, 0 = copy on the calling thread) */
+/* process-wide tuning knobs for A/B and profiling runs (a production process leaves them at their defaults; a set
+ * knob applies to every caller's next call): kernels ("grid", "gf_variant", "crc_variant", "crc_grid", "crc_run",
+ * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_chunk_shared" the
+ * same while other host-buffer calls are in flight (0: always host_chunk), "host_slots", "copy_threads" = helper
+ * threads for pageable <-> pinned copies, 0 = copy on the calling thread, "copy_stream" -1..3, "queue_batches",
+ * "e2e_chunk", "e2e_rect").  OZEC_EINVAL for an unknown key, a value out of range, or a kernel variant the library
+ * does not hold. */
 int ozec_set_tuning(const char *key, int64_t value);
+/* the kernel variants "gf_variant" / "crc_variant" accept besides 0: writes up to cap ids, returns how many exist */
+int ozec_tuning_variants(const char *key, int *ids, int cap);
 /* fill n bytes with splitmix64 stream `stream_id` of `seed` (tests/golden/synth.py is the CPU twin) */
 int ozec_fill_splitmix64(uint8_t *d_dst, size_t n, uint64_t seed, uint64_t stream_id, void *stream);
 /* same, many cells: cell c (stream first_stream + c) at d_base + c*cell_stride */

@@ -15,8 +15,9 @@ import org.apache.ratis.thirdparty.com.google.protobuf.UnsafeByteOperations;
  * window loop builds -- 4-byte big-endian int2ByteString((int) getValue()) per window, last window short
  * (Checksum.java:59-70).
  *
- * <p>The hook (java/patches/hdds-common-checksum-hook.patch) takes this path only when {@link #useGpu} says so:
- * CRC32/CRC32C, one contiguous buffer, libozec usable, and at least {@code ozone.checksum.hip.batch.min.bytes} bytes.
+ * <p>{@link HipChecksumAccelerator} (the provider of hdds-common's ChecksumAccelerator seam,
+ * java/patches/hdds-common-checksum-hook.patch) takes this path only when {@link #useGpu} says so: CRC32/CRC32C, a
+ * single-buffer ChunkBuffer, libozec usable, and at least {@code ozone.checksum.hip.batch.min.bytes} bytes.
  * That threshold defaults to never: a host buffer crosses PCIe twice (staging copy, H2D, kernel, D2H) and on MI355X
  * that lost to one core's JDK-class CRC32C at every size measured, 16 KiB to 64 MiB, from 1 and from 16 threads
  * (bench.py --workload stream, checksum_windows_* rows, profiles/r03/).  Every other call runs the reference's own
@@ -36,7 +37,12 @@ public final class HipChecksum {
     return OzecNative.isAvailable();
   }
 
-  /** Whether Checksum.computeChecksum(ChunkBuffer) should take the GPU batch path for this call. */
+  /**
+   * Whether Checksum.computeChecksum(ChunkBuffer) should take the GPU batch path for this call: only the single-buffer
+   * ChunkBuffer (ChunkBufferImplWithByteBuffer, CM/ChunkBufferImplWithByteBuffer.java:78-98), whose iterate() the
+   * batch reproduces including the position it leaves; the buffer-list and incremental forms (whose iterate copies
+   * across buffers, or rejects a bytesPerChecksum other than its increment) keep the reference's loop.
+   */
   public static boolean useGpu(ChecksumType type, ChunkBuffer data) {
     if (MIN_GPU_BYTES == Long.MAX_VALUE || data.remaining() < MIN_GPU_BYTES) {
       return false;
@@ -44,15 +50,18 @@ public final class HipChecksum {
     if (type != ChecksumType.CRC32 && type != ChecksumType.CRC32C) {
       return false;
     }
-    final List<ByteBuffer> buffers = data.asByteBufferList();
-    return buffers.size() == 1 && isAvailable();
+    return data instanceof ChunkBufferImplWithByteBuffer && isAvailable();
   }
 
-  /** The ChecksumData of {@code data} (one contiguous buffer, see {@link #useGpu}); positions are not moved. */
+  /**
+   * The ChecksumData of {@code data} (a single-buffer ChunkBuffer, see {@link #useGpu}).  Like the reference's
+   * {@code data.iterate(bytesPerChecksum)} loop, it consumes the buffer: its position ends at its limit.
+   */
   public static ChecksumData computeChecksum(ChecksumType type, ChunkBuffer data, int bytesPerChecksum) {
     final ByteBuffer b = data.asByteBufferList().get(0);
     final byte[] crcs = computeChecksumBytes(type == ChecksumType.CRC32 ? OzecNative.CHECKSUM_CRC32
         : OzecNative.CHECKSUM_CRC32C, b, bytesPerChecksum);
+    b.position(b.limit());
     final List<ByteString> list = new ArrayList<>(crcs.length / 4);
     for (int i = 0; i < crcs.length; i += 4) {
       list.add(UnsafeByteOperations.unsafeWrap(crcs, i, 4));

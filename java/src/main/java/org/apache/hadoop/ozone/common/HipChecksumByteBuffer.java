@@ -33,8 +33,8 @@ public final class HipChecksumByteBuffer implements ChecksumByteBuffer {
   private long hostLen;       // bytes the host CRC has seen since its last reset
   private boolean split;      // a GPU update happened since reset()
 
-  /** True when the GPU threshold is set and libozec_jni is usable; ChecksumByteBufferFactory installs this class
-   * only then (java/patches/hdds-common-checksum-hook.patch). */
+  /** True when the GPU threshold is set and libozec_jni is usable; HipChecksumAccelerator.wrap (the provider of the
+   * hdds-common ChecksumAccelerator seam, java/patches/hdds-common-checksum-hook.patch) installs this class only then. */
   public static boolean enabled() {
     return MIN_GPU_BYTES != Integer.MAX_VALUE && OzecNative.isAvailable();
   }

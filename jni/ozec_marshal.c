@@ -273,13 +273,19 @@ int ozm_composer_update_bytes(ozec_crc_composer *c, const uint8_t *buf, int64_t 
     return fail_as(OZEC_EINVAL, "java/io/IOException", msg, st);
   }
   if (length <= 0) return ok(st);
-  if (!buf || offset < 0 || offset + length > cap) {
-    snprintf(msg, sizeof(msg), "Index %lld out of bounds for length %lld",
-             (long long)(offset < 0 ? offset : offset + length - 1), (long long)cap);
-    return fail_as(OZEC_EINVAL, "java/lang/ArrayIndexOutOfBoundsException", msg, st);
-  }
-  for (int64_t i = 0; i < length; i += 4) { /* one CRC at a time, so a stripe overrun stops where the reference does */
-    const uint8_t *b = buf + offset + i;
+  if (!buf) return fail_as(OZEC_EINVAL, "java/lang/NullPointerException", "crcBuffer is null", st);
+  /* CrcComposer.update(byte[], int, int, long) (OC/CrcComposer.java:124-139): one CrcUtil.readInt (OC/CrcUtil.java:
+   * 181-193) and one update per CRC, so the CRCs before a failing read are composed, as in the reference */
+  for (int64_t o = offset; o < offset + length; o += 4) {
+    if (o + 4 > cap) { /* readInt's bounds check */
+      snprintf(msg, sizeof(msg), "readInt out of bounds: buf.length=%lld, offset=%lld", (long long)cap, (long long)o);
+      return fail_as(OZEC_EINVAL, "java/io/IOException", msg, st);
+    }
+    if (o < 0) { /* buf[offset + 0] of a negative offset: the JVM's array bounds check */
+      snprintf(msg, sizeof(msg), "Index %lld out of bounds for length %lld", (long long)o, (long long)cap);
+      return fail_as(OZEC_EINVAL, "java/lang/ArrayIndexOutOfBoundsException", msg, st);
+    }
+    const uint8_t *b = buf + o;
     const uint32_t v = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
     if (ozm_composer_update(c, v, bytes_per_crc, st)) return st ? st->code : OZEC_EINVAL;
   }

@@ -94,8 +94,9 @@ int ozm_queue_submit(ozec_stripe_queue *q, const ozm_buf *data, int nd, const oz
  * hadoop-ozone/common/src/main/java/org/apache/hadoop/ozone/client/checksum/) with the reference's exceptions:
  * a negative length -> java.lang.IllegalArgumentException (CrcUtil.getMonomial), an unsupported type or a composer
  * position past its stripe -> java.io.IOException (CrcUtil.getCrcPolynomialForType, CrcComposer.update), a CRC
- * byte run whose length is not a multiple of 4 -> java.io.IOException, one past the array ->
- * java.lang.ArrayIndexOutOfBoundsException (CrcUtil.readInt). */
+ * byte run whose length is not a multiple of 4 -> java.io.IOException, a CRC read past the array -> java.io.IOException
+ * "readInt out of bounds: ..." after the CRCs before it were composed (CrcUtil.readInt, OC/CrcUtil.java:181-193), a
+ * negative offset -> java.lang.ArrayIndexOutOfBoundsException (the array access). */
 int ozm_crc_monomial(int checksum_type, int64_t len_bytes, uint32_t *out, ozm_status *st);
 int ozm_crc_compose(int checksum_type, uint32_t crc_a, uint32_t crc_b, int64_t len_b, uint32_t *out, ozm_status *st);
 int ozm_composer_create(int checksum_type, int64_t bytes_per_crc_hint, int64_t stripe_length,

@@ -145,6 +145,7 @@ _SIGS = {
     "ozec_stats": (ctypes.c_int, [ctypes.c_int, c_voidp]),
     "ozec_stats_reset": (None, []),
     "ozec_set_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
+    "ozec_tuning_variants": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "ozec_fill_splitmix64": (ctypes.c_int, [c_voidp, c_size, ctypes.c_uint64, ctypes.c_uint64, c_voidp]),
     "ozec_fill_splitmix64_cells": (ctypes.c_int, [c_voidp, c_i64, c_size, c_size, ctypes.c_uint64, ctypes.c_uint64,
                                                   c_voidp]),

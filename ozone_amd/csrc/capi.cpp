@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <iterator>
 #include <memory>
 #include <mutex>
 #include <regex>
@@ -154,7 +155,7 @@ struct DevCtx {
 
   int acquire(Slot **out) {
     std::unique_lock<std::mutex> lk(pool_mu);
-    const size_t max_slots = static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.host_slots));
+    const size_t max_slots = static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.host_slots.load()));
     pool_cv.wait(lk, [&] { return !free_slots.empty() || slots.size() < max_slots; });
     if (free_slots.empty()) {
       auto s = std::make_unique<Slot>();
@@ -368,9 +369,15 @@ bool host_pinned(const void *p) {
   return at.type == hipMemoryTypeHost;
 }
 
-// the whole [p, p+n) must be registered / pinned: check its two ends
+// the whole [p, p+n) must lie in ONE registered / pinned allocation: both ends pinned, and in the same allocation (two
+// separately pinned buffers that happen to be adjacent, or evenly spaced cells of different allocations, are not one
+// DMA source: HIP resolves a copy's host range through the allocation of its start)
 bool range_pinned(const void *p, size_t n) {
-  return n == 0 || (host_pinned(p) && host_pinned(static_cast<const uint8_t *>(p) + n - 1));
+  if (n == 0) return true;
+  const uint8_t *last = static_cast<const uint8_t *>(p) + n - 1;
+  if (!host_pinned(p) || !host_pinned(last)) return false;
+  const void *b = ozec::pinned_alloc_base(p);
+  return b != nullptr && b == ozec::pinned_alloc_base(last);
 }
 
 // Host-buffer job through one staging slot, pipelined in chunks: while the GPU copies / codes / copies back
@@ -389,8 +396,9 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
   // chunks (host_chunk, 4 MiB per unit: one chunk for 1 MiB cells); with other calls in flight the link and the
   // staging copies are shared, and overlapping the copies of one call's chunks pays (host_chunk_shared, 512 KiB:
   // measured at T = 4 / 16 callers)
-  int64_t want = ozec::g_tune.host_chunk;
-  if (ctx->leased.load() > 1 && ozec::g_tune.host_chunk_shared > 0) want = std::min(want, ozec::g_tune.host_chunk_shared);
+  int64_t want = ozec::g_tune.host_chunk.load();
+  const int64_t shared_chunk = ozec::g_tune.host_chunk_shared.load();
+  if (ctx->leased.load() > 1 && shared_chunk > 0) want = std::min(want, shared_chunk);
   size_t chunk = static_cast<size_t>(std::max<int64_t>(1, want));
   chunk = std::max(chunk, (len + kMaxChunks - 1) / kMaxChunks);
   chunk = std::max(gran, chunk / gran * gran);
@@ -1040,7 +1048,7 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
   std::lock_guard<std::mutex> lk(P.mu);
   const int k = enc->k, p = enc->p, rows = out_rows(enc), units = k + rows;
   const size_t C = std::min(num_stripes, stripes_per_chunk ? stripes_per_chunk
-                                                          : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk)));
+                                                          : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk.load())));
   const size_t nwin = with_crc ? (len + bpc - 1) / bpc : 0;
   const size_t dstripe = static_cast<size_t>(k + p) * len;               // device layout [C][k+p][len]
   const size_t dcrc_off = round_up(C * dstripe, kStageAlign);            // then crcs [C][units][nwin]
@@ -1365,7 +1373,7 @@ int ozec_reconstruct_crc_host_batch(ozec_coder *dec, const uint8_t *h_in, int64_
   std::lock_guard<std::mutex> lk(P.mu);
   const int e = n_erased;
   const size_t C = std::min(num_stripes, stripes_per_chunk ? stripes_per_chunk
-                                                          : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk)));
+                                                          : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk.load())));
   const size_t nwin = (len + bpc - 1) / bpc;
   // device layout of one chunk buffer: input slots [C][k+p][len], rebuilt [C][e][len], expected CRCs [C][k+p][nwin],
   // rebuilt CRCs [C][e][nwin], mismatch [C]
@@ -1596,25 +1604,75 @@ int ozec_parse_replication(const char *s, int *codec, int *k, int *p, int *chunk
   return OZEC_OK;
 }
 
+static bool listed(const int *ids, size_t n, int64_t v) {
+  for (size_t i = 0; i < n; ++i)
+    if (ids[i] == v) return true;
+  return false;
+}
+
 int ozec_set_tuning(const char *key, int64_t value) {
   if (!key) return fail(OZEC_EINVAL, "null key");
   const std::string k(key);
-  if (k == "grid") ozec::g_tune.grid = value;
-  else if (k == "gf_variant") ozec::g_tune.gf_variant = static_cast<int>(value);
-  else if (k == "crc_variant") ozec::g_tune.crc_variant = static_cast<int>(value);
-  else if (k == "crc_grid") ozec::g_tune.crc_grid = value;
-  else if (k == "crc_run") ozec::g_tune.crc_run = value;
-  else if (k == "unit_map") ozec::g_tune.unit_map = static_cast<int>(value);
-  else if (k == "host_chunk" && value > 0) ozec::g_tune.host_chunk = value;
-  else if (k == "host_chunk_shared" && value >= 0) ozec::g_tune.host_chunk_shared = value;
-  else if (k == "host_slots" && value > 0) ozec::g_tune.host_slots = value;
-  else if (k == "queue_batches" && value >= 0 && value <= 64) ozec::g_tune.queue_batches = value;
-  else if (k == "copy_threads" && value >= 0) ozec::set_copy_threads(static_cast<int>(value));
-  else if (k == "copy_stream") ozec::set_copy_stream(static_cast<int>(value));
-  else if (k == "e2e_chunk" && value > 0) ozec::g_tune.e2e_chunk = value;
-  else if (k == "e2e_rect") ozec::g_tune.e2e_rect = static_cast<int>(value);
-  else return fail(OZEC_EINVAL, "unknown tuning key " + k);
+  auto &t = ozec::g_tune;
+  auto bad = [&] { return fail(OZEC_EINVAL, "invalid value " + std::to_string(value) + " for tuning key " + k); };
+  if (k == "gf_variant" || k == "crc_variant") {
+    const bool gf = k == "gf_variant";
+    const int *ids = gf ? ozec::kGfVariants : ozec::kCrcVariants;
+    const size_t n = gf ? std::size(ozec::kGfVariants) : std::size(ozec::kCrcVariants);
+    if (value != 0 && !listed(ids, n, value)) return bad();
+    (gf ? t.gf_variant : t.crc_variant).store(static_cast<int>(value));
+  } else if (k == "grid" || k == "crc_grid" || k == "crc_run") {
+    if (value < 0) return bad();
+    (k == "grid" ? t.grid : k == "crc_grid" ? t.crc_grid : t.crc_run).store(value);
+  } else if (k == "unit_map") {
+    if (value != 0 && value != 1) return bad();
+    t.unit_map.store(static_cast<int>(value));
+  } else if (k == "host_chunk") {
+    if (value <= 0) return bad();
+    t.host_chunk.store(value);
+  } else if (k == "host_chunk_shared") {
+    if (value < 0) return bad();
+    t.host_chunk_shared.store(value);
+  } else if (k == "host_slots") {
+    if (value <= 0) return bad();
+    t.host_slots.store(value);
+  } else if (k == "queue_batches") {
+    if (value < 0 || value > 64) return bad();
+    t.queue_batches.store(value);
+  } else if (k == "copy_threads") {
+    if (value < 0 || value > 256) return bad();
+    ozec::set_copy_threads(static_cast<int>(value));
+  } else if (k == "copy_stream") {
+    if (!ozec::set_copy_stream(static_cast<int>(value))) return bad();
+  } else if (k == "e2e_chunk") {
+    if (value <= 0) return bad();
+    t.e2e_chunk.store(value);
+  } else if (k == "e2e_rect") {
+    if (value != 0 && value != 1) return bad();
+    t.e2e_rect.store(static_cast<int>(value));
+  } else {
+    return fail(OZEC_EINVAL, "unknown tuning key " + k);
+  }
   return OZEC_OK;
+}
+
+int ozec_tuning_variants(const char *key, int *ids, int cap) {
+  if (!key) return fail(OZEC_EINVAL, "null key");
+  const std::string k(key);
+  const int *v;
+  size_t n;
+  if (k == "gf_variant") {
+    v = ozec::kGfVariants;
+    n = std::size(ozec::kGfVariants);
+  } else if (k == "crc_variant") {
+    v = ozec::kCrcVariants;
+    n = std::size(ozec::kCrcVariants);
+  } else {
+    return fail(OZEC_EINVAL, "no variant list for tuning key " + k);
+  }
+  for (size_t i = 0; i < n && static_cast<int>(i) < cap; ++i)
+    if (ids) ids[i] = v[i];
+  return static_cast<int>(n);
 }
 
 uint32_t ozec_crc_combine(int checksum_type, uint32_t a, uint32_t b, uint64_t len_b) {

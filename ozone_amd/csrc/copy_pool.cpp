@@ -185,7 +185,11 @@ void set_copy_threads(int n) { Pool::get().resize(std::max(0, n)); }
 
 void set_copy_node(int node) { Pool::get().set_node(node); }
 
-void set_copy_stream(int mode) { g_stream_mode.store(mode < 0 ? -1 : mode > 0 ? 1 : 0); }
+bool set_copy_stream(int mode) {
+  if (mode < -1 || mode > 3) return false;
+  g_stream_mode.store(mode);
+  return true;
+}
 
 void parallel_copy(const std::vector<CopyTask> &tasks, CopyDir dir, bool shared) {
   size_t total = 0;

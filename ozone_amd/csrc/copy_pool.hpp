@@ -24,7 +24,7 @@ void set_copy_threads(int n);
 void set_copy_node(int node);
 // pieces copied with streaming (non-temporal) stores: 1 both directions, 2 into staging only, 3 only for copies that
 // share DRAM with other transfers, 0 plain memcpy, -1 auto (1 where AVX2 exists); set by
-// ozec_set_tuning("copy_stream", n)
-void set_copy_stream(int mode);
+// ozec_set_tuning("copy_stream", n); false (nothing changed) outside -1..3
+bool set_copy_stream(int mode);
 
 }  // namespace ozec

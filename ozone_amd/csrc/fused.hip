@@ -24,9 +24,9 @@
 //
 // Same results as encode_crc_g26 bit for bit (same G26 tables, same per-lane folding, same lane tree); the
 // launcher (launch_encode_crc) picks this kernel for the shapes and geometries above and falls back otherwise.
-#include <map>
+#include <new>
 #include <mutex>
-#include <utility>
+#include <vector>
 
 #include "fused_nb.hpp"
 
@@ -225,51 +225,92 @@ hipError_t launch_lv(const EncCrcArgs &e, hipStream_t st) {
   }
 }
 
-// variant (g_tune.crc_variant): 0 default; 50-59 step group / ring / occupancy / accumulator A/B
+// variant (g_tune.crc_variant): the streamed-input kernel's measured defaults, kept for A/B against the nibble kernel
+// (profiles/r02/lv/ab_variants_lv3.log, ab_opt_lv5.log): 56 = groups of D = 4 steps, ring of 4 input blocks, 5 waves
+// per SIMD (the rs-10-x form, 95 VGPRs), permutes before their XORs; 59 = ring of 2 at 6 waves (the rs-6-x form, 76
+// VGPRs), permutes first and selector masks in VGPRs.  (Variants 50-58 were taken out of the library.)
 template <int K, int R>
 hipError_t launch_lv_kr(const EncCrcArgs &e, hipStream_t st, int v) {
-  switch (v) {
-    case 51: return launch_lv<K, R, 4, 4, 4, 5>(e, st);
-    case 52: return launch_lv<K, R, 4, 4, 4, 6>(e, st);
-    case 53: return launch_lv<K, R, 4, 2, 4, 6>(e, st);
-    case 54: return launch_lv<K, R, 2, 4, 4, 5>(e, st);
-    case 55: return launch_lv<K, R, 4, 2, 4, 5>(e, st);
-    case 56: return launch_lv<K, R, 4, 4, 4, 5, false, 1>(e, st);
-    case 57: return launch_lv<K, R, 4, 4, 4, 5, false, 2>(e, st);
-    case 58: return launch_lv<K, R, 4, 4, 4, 5, false, 3>(e, st);
-    case 59: return launch_lv<K, R, 4, 2, 4, 6, false, 3>(e, st);
-    default: break;
+  if (v == 56) return launch_lv<K, R, 4, 4, 4, 5, false, 1>(e, st);
+  if (v == 59) return launch_lv<K, R, 4, 2, 4, 6, false, 3>(e, st);
+  return hipErrorInvalidValue;
+}
+
+// Counter slots of the persistent nibble kernel's WorkQueue.  A launch leases a zeroed slot and hands it back behind an
+// event recorded after the kernel on the launch stream; the slot is leased again only once that event has completed,
+// i.e. once the kernel's last wave has put the counters back to zero.  Slots are not tied to a stream handle, so
+// concurrent launches never share one, whatever the stream (the null stream, hipStreamPerThread, several streams of
+// one caller).  A capturing stream gets no slot: its launches take the non-persistent form.
+struct WorkSlot {
+  int device = -1;
+  int32_t *ctr = nullptr;
+  hipEvent_t done = nullptr;
+  bool recorded = false;  // `done` marks the last launch that used the slot
+  bool leased = false;
+};
+
+std::mutex g_ws_mu;
+std::vector<WorkSlot *> g_ws;  // never freed: a handful per device and process
+constexpr size_t kMaxWorkSlots = 256;
+
+WorkSlot *nb_work_lease(hipStream_t st) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return nullptr;
   }
-  // measured on MI355X (profiles/r02/lv/ab_variants_lv3.log): rs-6-3 ring of 2 at 6 waves per SIMD (76 VGPRs),
-  // rs-10-4 ring of 4 at 5 waves (95 VGPRs); both with groups of D = 4 steps
-  // (profiles/r02/lv/ab_opt_lv5.log: permutes before their XORs +0.3 %, selector masks in VGPRs +0.6 %)
-  if constexpr (K + R >= 12) return launch_lv<K, R, 4, 4, 4, 5, false, 1>(e, st);
-  else return launch_lv<K, R, 4, 2, 4, 6, false, 3>(e, st);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  for (WorkSlot *w : g_ws) {
+    if (w->device != dev || w->leased) continue;
+    if (w->recorded) {
+      const hipError_t q = hipEventQuery(w->done);
+      (void)hipGetLastError();  // hipErrorNotReady must not reach the launch's error check
+      if (q != hipSuccess) continue;
+    }
+    w->leased = true;
+    return w;
+  }
+  if (g_ws.size() >= kMaxWorkSlots) return nullptr;
+  auto *w = new (std::nothrow) WorkSlot();
+  if (!w) return nullptr;
+  w->device = dev;
+  void *p = nullptr;
+  if (hipMalloc(&p, kWqInts * sizeof(int32_t)) != hipSuccess) {
+    (void)hipGetLastError();
+    delete w;
+    return nullptr;
+  }
+  if (hipMemsetAsync(p, 0, kWqInts * sizeof(int32_t), st) != hipSuccess ||
+      hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(p);
+    delete w;
+    return nullptr;
+  }
+  w->ctr = static_cast<int32_t *>(p);
+  w->leased = true;
+  g_ws.push_back(w);
+  return w;
+}
+
+// give the slot back; `used`: a kernel that counts on it was enqueued on `st`
+void nb_work_return(WorkSlot *w, hipStream_t st, bool used) {
+  if (used) {
+    if (hipEventRecord(w->done, st) == hipSuccess) {
+      w->recorded = true;
+    } else {
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(st);  // no event: make sure the kernel is done before anyone else counts on the slot
+    }
+  }
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  w->leased = false;
 }
 
 }  // namespace
-
-// Counter slot of the WorkQueue for launches on `st` (per device and stream, zeroed once on that stream; launches
-// on one stream run in order and each leaves its slot at zero).  Null when no slot can be had.
-int32_t *nb_work_slot(hipStream_t st) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, int32_t *> slots;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = slots.find({dev, st});
-  if (it != slots.end()) return it->second;
-  if (slots.size() >= 4096) return nullptr;
-  void *p = nullptr;
-  if (hipMalloc(&p, kWqInts * sizeof(int32_t)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(p, 0, kWqInts * sizeof(int32_t), st) != hipSuccess) {
-    (void)hipFree(p);
-    return nullptr;
-  }
-  slots[{dev, st}] = static_cast<int32_t *>(p);
-  return static_cast<int32_t *>(p);
-}
-
 
 bool encode_crc_lv_supported(const EncCrcArgs &e) {
   const CodeArgs &a = e.code;
@@ -279,41 +320,52 @@ bool encode_crc_lv_supported(const EncCrcArgs &e) {
   return shape && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && a.len % e.crc.bpc == 0;
 }
 
+namespace {
+
+hipError_t launch_nb_shape(const EncCrcArgs &e, hipStream_t st, int v) {
+  const int k = e.code.k, r = e.code.rows;
+  if (k == 6 && r == 3) return launch_nb_6_3(e, st, v);
+  if (k == 6 && r == 2) return launch_nb_6_2(e, st, v);
+  if (k == 3 && r == 2) return launch_nb_3_2(e, st, v);
+  if (k == 10 && r == 4) return launch_nb_10_4(e, st, v);
+  if (k == 10 && r == 3) return launch_nb_10_3(e, st, v);
+  if (k == 10 && r == 2) return launch_nb_10_2(e, st, v);
+  if (k == 10 && r == 1) return launch_nb_10_1(e, st, v);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
 hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   const int k = e.code.k, r = e.code.rows;
-  // default: the nibble-table kernel (same-process A/Bs on MI355X).  Round 2 (profiles/r02/nb/): rs-10-x with a ring
-  // of 5 input blocks and one-step groups (62: C3r 62.9 %; encode_crc_lv 52.5 %), rs-6-x / rs-3-x with two-step
-  // groups in 12-wave workgroups (87: C5dev 66.9 %; encode_crc_lv 57.9 %); 56 / 59 pin the streamed-input kernel's
-  // defaults.  Round 3 (profiles/r03/ab/): the output registers shift for free (XO), and the grid is persistent, fed
-  // by the WorkQueue -- rs-10-x 150 (62's geometry; C3r 64.8 % vs 63.7 % for 102, 62.5 % for 62), rs-3-x 163
-  // (two-step groups in 16-wave workgroups), rs-6-x 167 (163 with a ring of 3 input blocks; C5dev 68.4 % for 163 vs
-  // 67.2 % for 87 on one box, 66.9 % for 167 vs 66.2 % for 163 on another); without a counter slot the same kernels
-  // on a one-wave-per-window grid (151 / 152).  Since the last round-3 build the window CRCs leave through one
-  // lane-parallel store / compare (EM: 170 = 150, 171 = 167, 172 = 163, 173 = 151, 174 = 152 with it; K + R fewer
-  // divergent blocks per window, SGPR spills 104 -> 12 for rs-10-4): C3r 5.711 -> 5.582 ms, C5dev 6.956 -> 6.911 ms,
-  // every fallback faster too (profiles/r03/em/ab_*.log, 7 rounds)
-  const bool queue = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) && nb_work_slot(st) != nullptr;
-  // rs-10-x: two-step groups with the second distance set for half the inputs only (177 = 170's ring in 16-wave
-  // workgroups, H = 5): 0.5-1.3 % faster than 170 in three same-process A/Bs on three boxes (profiles/r03/h/)
-  if (v == 0) v = k == 10 ? (queue ? 177 : 173) : !queue ? 174 : k == 6 ? 171 : 172;
-  if (v >= 60 && v < 200) {
-    if (k == 6 && r == 3) return launch_nb_6_3(e, st, v);
-    if (k == 6 && r == 2) return launch_nb_6_2(e, st, v);
-    if (k == 3 && r == 2) return launch_nb_3_2(e, st, v);
-    if (k == 10 && r == 4) return launch_nb_10_4(e, st, v);
-    if (k == 10 && r == 3) return launch_nb_10_3(e, st, v);
-    if (k == 10 && r == 2) return launch_nb_10_2(e, st, v);
-    if (k == 10 && r == 1) return launch_nb_10_1(e, st, v);
+  if (v == 56 || v == 59) {
+    if (k == 6 && r == 3) return launch_lv_kr<6, 3>(e, st, v);
+    if (k == 6 && r == 2) return launch_lv_kr<6, 2>(e, st, v);
+    if (k == 3 && r == 2) return launch_lv_kr<3, 2>(e, st, v);
+    if (k == 10 && r == 4) return launch_lv_kr<10, 4>(e, st, v);
+    if (k == 10 && r == 3) return launch_lv_kr<10, 3>(e, st, v);
+    if (k == 10 && r == 2) return launch_lv_kr<10, 2>(e, st, v);
+    if (k == 10 && r == 1) return launch_lv_kr<10, 1>(e, st, v);
     return hipErrorInvalidValue;
   }
-  if (k == 6 && r == 3) return launch_lv_kr<6, 3>(e, st, v);
-  if (k == 6 && r == 2) return launch_lv_kr<6, 2>(e, st, v);
-  if (k == 3 && r == 2) return launch_lv_kr<3, 2>(e, st, v);
-  if (k == 10 && r == 4) return launch_lv_kr<10, 4>(e, st, v);
-  if (k == 10 && r == 3) return launch_lv_kr<10, 3>(e, st, v);
-  if (k == 10 && r == 2) return launch_lv_kr<10, 2>(e, st, v);
-  if (k == 10 && r == 1) return launch_lv_kr<10, 1>(e, st, v);
-  return hipErrorInvalidValue;
+  // default: the nibble-table kernel (same-process A/Bs on MI355X).  Round 2 (profiles/r02/nb/): rs-10-x with a ring
+  // of 5 input blocks and one-step groups (62: C3r 62.9 %; encode_crc_lv 52.5 %), rs-6-x / rs-3-x with two-step
+  // groups in 12-wave workgroups (87: C5dev 66.9 %; encode_crc_lv 57.9 %).  Round 3 (profiles/r03/ab/): the output
+  // registers shift for free (XO), and the grid is persistent, fed by the WorkQueue -- rs-10-x 150 (62's geometry;
+  // C3r 64.8 % vs 63.7 % for 102, 62.5 % for 62), rs-3-x 163 (two-step groups in 16-wave workgroups), rs-6-x 167 (163
+  // with a ring of 3 input blocks; C5dev 68.4 % for 163 vs 67.2 % for 87 on one box); without a counter slot the same
+  // kernels on a one-wave-per-window grid (173 / 174).  The window CRCs leave through one lane-parallel store /
+  // compare (EM: 170 = 150, 171 = 167, 172 = 163 with it; C3r 5.711 -> 5.582 ms, C5dev 6.956 -> 6.911 ms,
+  // profiles/r03/em/ab_*.log); rs-10-x takes two-step groups with the second distance set for half the inputs (177,
+  // 0.5-1.3 % faster than 170 in three same-process A/Bs, profiles/r03/h/)
+  WorkSlot *ws = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) ? nb_work_lease(st) : nullptr;
+  if (v == 0) v = k == 10 ? (ws ? 177 : 173) : !ws ? 174 : k == 6 ? 171 : 172;
+  const bool used = ws && nb_variant_persistent(v);
+  EncCrcArgs ed = e;
+  ed.work = used ? ws->ctr : nullptr;
+  const hipError_t err = launch_nb_shape(ed, st, v);
+  if (ws) nb_work_return(ws, st, used && err == hipSuccess);
+  return err;
 }
 
 }  // namespace ozec

@@ -7,8 +7,6 @@
 
 namespace ozec {
 
-// Counter slot of the persistent kernel's WorkQueue for launches on `st` (fused.hip)
-int32_t *nb_work_slot(hipStream_t st);
 
 #define OZEC_NB_SHAPES(X) X(6, 3) X(6, 2) X(3, 2) X(10, 4) X(10, 3) X(10, 2) X(10, 1)
 #define OZEC_NB_DECL(K, R) hipError_t launch_nb_##K##_##R(const EncCrcArgs &e, hipStream_t st, int v);
@@ -63,13 +61,14 @@ __device__ __forceinline__ uint2 lds64(const void *base, uint32_t byte_off) {
   return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + byte_off);
 }
 
-// Dynamic work distribution of the persistent nibble kernel (DYN variants).  The (stripe, window) units are cut into
-// 8 contiguous ranges, one per XCD (the dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b starts
+// Dynamic work distribution of the persistent nibble kernel (DYN = 1).  The (stripe, window) units are cut into 8
+// contiguous ranges, one per XCD (the dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b starts
 // on range b % 8: each XCD streams one contiguous eighth of the batch), and a wave takes the next unit of its range
-// with one atomicAdd (a vector-memory atomic issued by lane 0 and broadcast with readfirstlane); a wave whose range is
-// used up moves on to the next range, so every unit is taken exactly once whatever the grid size or placement.  The
-// counters are a per-stream slot (launch_nb): launches on one stream run in order, and the last wave of a launch to
-// finish puts the slot back to zero for the next one.
+// with one atomicAdd (a vector-memory atomic issued by lane 0 and broadcast with readfirstlane), one unit ahead of
+// the one it works on; a wave whose range is used up moves on to the next range, so every unit is taken exactly once
+// whatever the grid size or placement.  The counters are a slot leased for the launch (fused.hip nb_work_lease):
+// the last wave of a launch to finish puts the slot back to zero, and the slot is reused only after an event recorded
+// behind the launch has completed.
 constexpr int kWqStride = 16;                 // ints between counters (64 B: one counter per cache line)
 constexpr int kWqDone = 8 * kWqStride;        // finished-wave counter
 constexpr int kWqInts = kWqDone + kWqStride;  // ints per slot
@@ -77,28 +76,14 @@ struct WorkQueue {
   int32_t *ctr;
   int64_t units;
   int q0, qi;
-  int64_t cur, end;  // claimed units [cur, end) not yet handed out (chunked claims)
-  int32_t seen;      // the own range's counter after this wave's last claim
-  int32_t per_range; // waves per range (chunk size of a guided claim: what is left / 2 per wave)
-  __device__ __forceinline__ int64_t next(int lane, bool guided) {
-    if (cur < end) return cur++;
+  __device__ __forceinline__ int64_t next(int lane) {
     while (qi < 8) {
       const int q = (q0 + qi) & 7;
       const int64_t lo = units * q / 8, hi = units * (q + 1) / 8;
-      int32_t c = 1;
-      if (guided && qi == 0) {
-        const int64_t left = hi - lo - seen;
-        c = static_cast<int32_t>(std::min<int64_t>(8, std::max<int64_t>(1, left / (2 * per_range))));
-      }
       int32_t t = 0;
-      if (lane == 0) t = atomicAdd(ctr + q * kWqStride, c);
+      if (lane == 0) t = atomicAdd(ctr + q * kWqStride, 1);
       t = __builtin_amdgcn_readfirstlane(t);
-      seen = t + c;
-      if (lo + t < hi) {
-        cur = lo + t;
-        end = std::min<int64_t>(hi, cur + c);
-        return cur++;
-      }
+      if (lo + t < hi) return lo + t;
       ++qi;
     }
     return units;
@@ -160,58 +145,44 @@ __device__ __forceinline__ void nb_emit_lane(const EncCrcArgs &e, int64_t s, int
 // K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
 // FENCE: dwords of a block whose lookups go between scheduling fences (2: halves, at most 16 results live; 1:
 // quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree;
-// DYN: 0 one wave per unit, no grid-stride; persistent grid (one resident set of workgroups, tables built once per
-// workgroup) fed by the WorkQueue with 1 a claim per unit, made one unit ahead, 3 guided claims of up to 8 units, 4 a
-// claim per unit made when it is needed; 2 persistent grid with the static grid-stride order, 5 the same with the
-// waves' starts staggered by up to one window (a probe: do waves in lockstep on the same step offsets contend?);
-// DO: steps per output-register group (a multiple of D): the R output registers are looked up with the G26 distance
-// sets of DO steps and shifted once per DO steps, the K input registers (whose distance sets live in the nibble
-// entries, K * 4 KiB per set) once per D steps
-// PADV / PADL: probes only (variants 140-147), PADV independent v_xor_b32 / PADL ds_read_b32 added per step: the
-// marginal cost of one more VALU or LDS instruction says which pipe sets the time
+// DYN: 0 one wave per unit, no grid-stride; 1 persistent grid (one resident set of workgroups, tables built once per
+// workgroup) fed by the WorkQueue, a claim per unit made one unit ahead
 // XO: the output registers move by one step with no shift lookups (kernels.hpp kXo*): each is XORed into the first
 // dword of its next output block, whose G26 lookups use the set advanced by kXoAdvance bytes; the advance is undone
 // once per window.  Saves R x 7 lookups per step (the input registers keep their D-step shifts: their nibble lookups
 // also yield the GF products, which must see the unmodified data)
-// NF: probe only (wrong results): table regions past the 16-bit offset range are read from the region 32 KiB below
-// instead, with no index OR -- the same LDS traffic without the far-addressing VALU, an upper bound for what
-// removing that VALU could give wide step groups
 // EM: the window CRCs leave through nb_emit_lane (one lane-parallel store / compare) instead of K + R unit blocks
 // H (< K, XO with D = 2 only): only inputs 0..H-1 get the second distance set (K + H instead of 2K tables of 4 KiB, so
 // rs-10-x two-step groups fit two workgroups per CU); inputs H..K-1 are looked up in set 0 and shifted by one step
 // after every step (table at kSh1), inputs 0..H-1 by two at the group end
-// LT (with H < K): the lane-tree shifts (used once per window) move behind the nibble tables, so that 5.3 KiB more of
-// the tables stay inside the 16-bit ds_read offset range (fewer index ORs)
-template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
-          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false, bool EM = false, int H = K, bool LT = false>
+// (Round-3 probes -- output-register groups, VALU / LDS pads, far-addressing without the index OR, late lane-tree
+// tables, guided and static persistent orders -- are measured in DESIGN 2.3 and were taken out of the library.)
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
+          bool EM = false, int H = K>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
   static_assert(D <= kNibSets, "distance sets of the nibble blob");
-  static_assert((DO * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
-  static_assert(DO % D == 0 && DO <= 4, "output groups of whole input groups; windows are multiples of 4 steps");
-  static_assert(!XO || DO == D, "with XO the output registers are not grouped");
+  static_assert((D * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
+  static_assert(DYN == 0 || DYN == 1, "one wave per unit, or the persistent WorkQueue grid");
   static_assert(H == K || (XO && D == 2 && H >= 0 && H < K), "partial second distance set: XO, two-step groups");
   constexpr int kSets = K + (D - 1) * H;  // (d, j) nibble tables of 4 KiB: all K inputs in set 0, inputs < H in sets >= 1
-  // one LDS block: G26 blob of DO sets (+ the D-step register shift when D < DO), then the (d, j, p) nibble tables,
-  // then the GF dwords of the setup.  Table regions past the 16-bit ds_read offset range are reached with bit 15 set
-  // in the index register (one v_or_b32).  XO: the input-register shift and the lane-tree shifts of the G26 blob,
-  // then the XO blob, instead of the G26 sets
-  static_assert(!LT || (XO && H < K), "late lane-tree tables only with a partial second distance set");
-  constexpr uint32_t kXoOff = LT ? 224 + 224 : 224 + 1344;  // XO: word offset of the XO blob
-  constexpr uint32_t kShIn = XO ? 0 : DO == D ? g26_gshift(D) : g26_words(DO);  // word offset of the input-register shift
-  constexpr uint32_t kTree = XO ? 224 : g26_tree(DO);  // and of the lane-tree shifts (LT: behind the tables)
-  constexpr uint32_t kSh1 = LT ? 224 : kXoOff + kXoWords;  // H < K: one-step register shift (inputs H..K-1)
-  constexpr uint32_t kTW = LT ? kXoOff + kXoWords
-                              : XO ? kXoOff + kXoWords + (H < K ? 224 : 0) : g26_words(DO) + (DO == D ? 0 : 224);
+  // one LDS block: G26 blob of D sets, then the (d, j, p) nibble tables, then the GF dwords of the setup.  Table
+  // regions past the 16-bit ds_read offset range are reached with bit 15 set in the index register (one v_or_b32).
+  // XO: the input-register shift and the lane-tree shifts of the G26 blob, then the XO blob, instead of the G26 sets
+  constexpr uint32_t kXoOff = 224 + 1344;  // XO: word offset of the XO blob
+  constexpr uint32_t kShIn = XO ? 0 : g26_gshift(D);  // word offset of the input-register shift
+  constexpr uint32_t kTree = XO ? 224 : g26_tree(D);  // and of the lane-tree shifts
+  constexpr uint32_t kSh1 = kXoOff + kXoWords;  // H < K: one-step register shift (inputs H..K-1)
+  constexpr uint32_t kTW = XO ? kXoOff + kXoWords + (H < K ? 224 : 0) : g26_words(D);
   constexpr uint32_t kTB = (kTW * 4 + 255) / 256 * 256;  // nibble tables
-  constexpr uint32_t kLds = kTB + kSets * 4096 + K * 32 * 4 + (LT ? 1344 * 4 : 0);
+  constexpr uint32_t kLds = kTB + kSets * 4096 + K * 32 * 4;
   static_assert(kLds <= 160 * 1024, "LDS per workgroup");
   __shared__ __attribute__((aligned(256))) uint8_t s_all[kLds];
   uint32_t *const s_t = reinterpret_cast<uint32_t *>(s_all);
   uint2 *const s_c = reinterpret_cast<uint2 *>(s_all + kTB);
   uint32_t *const s_gf = reinterpret_cast<uint32_t *>(s_all + kTB + kSets * 4096);
-  uint32_t *const s_tree = LT ? s_gf + K * 32 : s_t + kTree;  // lane-tree shifts
+  uint32_t *const s_tree = s_t + kTree;  // lane-tree shifts
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
   for (int t = threadIdx.x; t < K * 32; t += blockDim.x) {
@@ -221,18 +192,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     for (int r = 0; r < R; ++r) dw |= gf_mul_byte(a.coef[r * K + j], static_cast<uint32_t>(n) << (4 * h)) << (8 * r);
     s_gf[t] = dw;
   }
-  if constexpr (LT) {
-    load_tables(s_t, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224);
-    load_tables(s_tree, cr.g26[g26_slot(1, D)] + g26_tree(D), 1344);
-    load_tables(s_t + kXoOff, cr.xo, kXoWords);
-    load_tables(s_t + kSh1, cr.g26[g26_slot(1, 1)] + g26_gshift(1), 224);
-  } else if constexpr (XO) {
+  if constexpr (XO) {
     load_tables(s_t, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224 + 1344);
     load_tables(s_t + kXoOff, cr.xo, kXoWords);
     if constexpr (H < K) load_tables(s_t + kSh1, cr.g26[g26_slot(1, 1)] + g26_gshift(1), 224);
   } else {
-    load_tables(s_t, cr.g26[g26_slot(1, DO)], g26_words(DO));
-    if constexpr (DO != D) load_tables(s_t + kShIn, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224);
+    load_tables(s_t, cr.g26[g26_slot(1, D)], g26_words(D));
   }
   __syncthreads();
   for (int q = threadIdx.x; q < kSets * 512; q += blockDim.x) {
@@ -247,7 +212,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   const int64_t nwin = cr.nwin;
   const int64_t units = a.nstripes * nwin;
   const int32_t T = static_cast<int32_t>(cr.bpc >> 10);  // steps per window
-  const int32_t G = T / DO;                               // output groups per window
+  const int32_t G = T / D;                                // step groups per window
   const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
   uint32_t v4, vf0;  // index-op operands in VGPRs (VOP2/SDWA with no SGPR or literal operand issue fastest)
   asm volatile("v_mov_b32 %0, 4" : "=v"(v4));
@@ -257,16 +222,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
   const uint32_t in_extent = static_cast<uint32_t>(off_max + cr.bpc);
   const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
-  constexpr bool kQueue = DYN == 1 || DYN == 3 || DYN == 4;
-  WorkQueue wq{e.work, units, static_cast<int>(blockIdx.x & 7), 0, 0, 0, 0, static_cast<int32_t>(gridDim.x * WPB / 8)};
-  int64_t u = kQueue ? wq.next(lane, DYN == 3) : bid * WPB + wave;
-  if constexpr (DYN == 5) {
-    const int n = static_cast<int>((blockIdx.x * WPB + wave) % 16) * 3;  // ~4 us per s_sleep 127 at 2 GHz
-    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-  }
+  WorkQueue wq{e.work, units, static_cast<int>(blockIdx.x & 7), 0};
+  int64_t u = DYN == 1 ? wq.next(lane) : bid * WPB + wave;
   while (u < units) {
-    // DYN 1 / 3: the next unit is claimed before this one is worked on, so the atomic's round trip overlaps the work
-    const int64_t u_next = DYN == 1 || DYN == 3 ? wq.next(lane, DYN == 3) : u + static_cast<int64_t>(gridDim.x) * WPB;
+    // DYN 1: the next unit is claimed before this one is worked on, so the atomic's round trip overlaps the work
+    const int64_t u_next = DYN == 1 ? wq.next(lane) : u + static_cast<int64_t>(gridDim.x) * WPB;
     // wave-uniform by construction; said explicitly so the descriptors below stay in SGPRs (the 64-bit division
     // runs in the VALU, and without this the buffer accesses were wrapped in waterfall loops)
     const int64_t s = uniform64(u / nwin);
@@ -286,10 +246,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     for (int i = 0; i + 1 < NB; ++i) ring[i] = load(vstep(i / K), i % K);
     for (int32_t g = 0; g < G; ++g) {
 #pragma unroll
-      for (int rr = 0; rr < DO; ++rr) {
-        const int32_t t = g * DO + rr;
-        const int d = D - 1 - rr % D;  // distance set of this step's inputs
-        const int dout = DO - 1 - rr;  // and outputs
+      for (int rr = 0; rr < D; ++rr) {
+        const int32_t t = g * D + rr;
+        const int d = D - 1 - rr;  // distance set of this step's blocks
         const uint32_t vcur = vstep(t), vnext = vstep(t + 1);
         uint32_t A[16];
 #pragma unroll
@@ -310,10 +269,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
               const int i = 4 * c + q;
               const uint32_t reg = kTB + nb_region<K>(j < H ? d : 0, j, i);
               uint2 lo, hi;
-              if (reg + 256 <= 65536 || NF) {
-                const uint32_t rg = reg + 256 <= 65536 ? reg : reg - 0x8000u;
-                lo = lds64(s_all, rg + nib_lo_idx(xw[c], q, v4));
-                hi = lds64(s_all, rg + 8 + nib_hi_idx(xw[c], q, vf0));
+              if (reg + 256 <= 65536) {
+                lo = lds64(s_all, reg + nib_lo_idx(xw[c], q, v4));
+                hi = lds64(s_all, reg + 8 + nib_hi_idx(xw[c], q, vf0));
               } else {
                 lo = lds64(s_all, (reg - 0x8000u) + (nib_lo_idx(xw[c], q, v4) | 0x8000u));
                 hi = lds64(s_all, (reg + 8 - 0x8000u) + (nib_hi_idx(xw[c], q, vf0) | 0x8000u));
@@ -351,18 +309,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             px.x ^= S[K + r];
             S[K + r] = g26_block<true>(s_t + kXoOff, px);
           } else {
-            S[K + r] ^= g26_block<true>(s_t + dout * kG26Set, p);
+            S[K + r] ^= g26_block<true>(s_t + d * kG26Set, p);
           }
           __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (PADV > 0 || PADL > 0) {
-          uint32_t px[4] = {static_cast<uint32_t>(lane), vf0, v4, static_cast<uint32_t>(t)};
-#pragma unroll
-          for (int i = 0; i < PADV; ++i) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(px[i & 3]) : "v"(v4));
-#pragma unroll
-          for (int i = 0; i < PADL; ++i)
-            px[i & 3] ^= reinterpret_cast<volatile uint32_t *>(s_t)[(lane + 7 * i) & 31];
-          asm volatile("" ::"v"(px[0]), "v"(px[1]), "v"(px[2]), "v"(px[3]));
         }
         if constexpr (H < K) {
           if (rr + 1 < D) {
@@ -370,15 +319,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             for (int q = H; q < K; ++q) S[q] = g5_shift(s_t + kSh1, S[q]);
           }
         }
-        if (DO != D && rr % D == D - 1 && rr + 1 < DO) {  // input groups ending inside the output group
-#pragma unroll
-          for (int q = 0; q < K; ++q) S[q] = g5_shift(s_t + kShIn, S[q]);
-        }
       }
       if (g + 1 < G) {
 #pragma unroll
         for (int q = 0; q < (XO ? K : K + R); ++q)
-          S[q] = g5_shift(s_t + (q < H ? kShIn : q < K ? kSh1 : g26_gshift(DO)), S[q]);
+          S[q] = g5_shift(s_t + (q < H ? kShIn : q < K ? kSh1 : g26_gshift(D)), S[q]);
       }
     }
     const bool last = w == nwin - 1;
@@ -404,28 +349,29 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         if (lane == q) nb_emit<K, R>(e, s, w, q, v, init);
       }
     }
-    u = DYN == 4 ? wq.next(lane, false) : u_next;
+    u = u_next;
   }
-  if constexpr (kQueue) wq.finish(lane, static_cast<int32_t>(gridDim.x) * WPB);
+  if constexpr (DYN == 1) wq.finish(lane, static_cast<int32_t>(gridDim.x) * WPB);
 }
 
-template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, int DO = D,
-          int PADV = 0, int PADL = 0, bool XO = false, bool NF = false, bool EM = false, int H = K, bool LT = false>
+template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
+          bool EM = false, int H = K>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
-  if constexpr ((DO * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
+  if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
-    constexpr int kNB = (DO * K) % 2 == 0 ? 2 : (DO * K <= K + 1 ? DO * K : 1);
-    static_assert(kNB != NB && (DO * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF, EM, H, LT>(e, st);
+    constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
+    static_assert(kNB != NB && (D * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, DO, PADV, PADL, XO, NF, EM, H, LT>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
-    EncCrcArgs ed = e;
     if constexpr (DYN != 0) {
-      // persistent: one resident set of workgroups (occupancy x CUs), each building its tables once
+      // persistent: one resident set of workgroups (occupancy x CUs), each building its tables once; the caller has
+      // leased the WorkQueue counter slot (e.work, fused.hip nb_work_lease)
+      if (e.work == nullptr || units > (int64_t{1} << 30)) return hipErrorInvalidValue;
       static int resident = 0;  // per instantiation and process (one device type)
       if (resident == 0) {
         int dev = 0, cus = 0, per_cu = 0;
@@ -435,172 +381,52 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
           return hipErrorInvalidValue;
         resident = std::max(1, cus * std::max(1, per_cu));
       }
-      if constexpr (DYN != 2) {
-        ed.work = nb_work_slot(st);
-        if (ed.work == nullptr || units > (int64_t{1} << 30)) return hipErrorInvalidValue;
-      }
       g = std::min<int64_t>(resident, blocks);
     }
     // non-persistent: one wave per (stripe, window) unit, no grid-stride: every workgroup builds its K*D*4 KiB of
     // tables, and the dispatcher's refill of finished workgroups balances the CUs.  Measured on MI355X against a
     // static persistent grid (profiles/r02/nb/ab_grid_*.log): C3r 56.2 % -> 63.5 %, C5dev 60.1 % -> 65.7 %.
-    if (g_tune.crc_grid > 0) g = std::min<int64_t>(g_tune.crc_grid, blocks);
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, ed);
+    const int64_t cg = g_tune.crc_grid;
+    if (cg > 0) g = std::min<int64_t>(cg, blocks);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, e);
     return hipGetLastError();
   }
 }
 
-// variant (g_tune.crc_variant): 60-69 nibble-table kernel step groups / ring / occupancy A/B
+// whether variant v of the nibble kernel runs on the persistent WorkQueue grid (needs a leased counter slot)
+constexpr bool nb_variant_persistent(int v) { return v == 150 || v == 163 || v == 167 || v == 170 || v == 171 ||
+                                                     v == 172 || v == 176 || v == 177; }
+
+// variant (g_tune.crc_variant, kernels.hpp kCrcVariants): the measured alternates of the nibble-table kernel
 template <int K, int R>
 hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
   constexpr int kD2 = K * 2 * 4096 + g26_words(2) * 4 <= 65536 ? 2 : 1;  // D = 2 where its tables fit
   constexpr int kNB = K % 2 == 0 && K > 2 ? K / 2 : K;                    // a deeper ring dividing the group
-  constexpr auto lds_of = [](int d) { return (g26_words(d) * 4 + 255) / 256 * 256 + K * d * 4096 + K * 128; };
-  constexpr int kDmax = lds_of(4) <= 160 * 1024 ? 4 : lds_of(2) <= 160 * 1024 ? 2 : 1;  // one workgroup per CU
-  // partial second distance sets (XO, D = 2): the XO blob ahead of the tables is (224 + 1344 + 1056 + 224) words
-  constexpr int kXoTB = ((224 + 1344 + kXoWords + 224) * 4 + 255) / 256 * 256;
-  constexpr int kHp = std::max(0, std::min(K - 1, (65536 - kXoTB) / 4096 - K));
   constexpr int kHh = K / 2;
   switch (v) {
-    case 61: return launch_nb<K, R, 1, 2, 8, 4>(e, st);
+    // round-2 defaults, non-persistent (profiles/r02/nb/): rs-10-x one-step groups with a ring of K / 2 (62), rs-6-x /
+    // rs-3-x two-step groups in 12-wave workgroups (87)
     case 62: return launch_nb<K, R, 1, kNB, 8, 4>(e, st);
-    case 63: return launch_nb<K, R, kD2, 2, 8, 4>(e, st);
-    case 64: return launch_nb<K, R, kD2, kNB, 8, 4>(e, st);
-    case 65: return launch_nb<K, R, 1, 2, 8, 5>(e, st);
-    case 66: return launch_nb<K, R, 1, 2, 8, 4, 4>(e, st);
-    case 67: return launch_nb<K, R, 1, 2, 4, 4>(e, st);
-    case 68: return launch_nb<K, R, kD2, 2, 16, 4>(e, st);
-    case 69: return launch_nb<K, R, kD2, 2, 12, 4>(e, st);
-    case 70: return launch_nb<K, R, 1, 2, 8, 6>(e, st);
-    case 71: return launch_nb<K, R, 1, 2, 8, 8>(e, st);
-    case 72: return launch_nb<K, R, kD2, 2, 16, 8>(e, st);
-    case 73: return launch_nb<K, R, 1, kNB, 8, 5>(e, st);
-    case 74: return launch_nb<K, R, 1, 2, 8, 4, 2, false>(e, st);
-    case 75: return launch_nb<K, R, 1, kNB, 8, 4, 2, false>(e, st);
-    case 76: return launch_nb<K, R, kD2, 2, 16, 4, 2, false>(e, st);
-    // two-step groups for every K (tables past the 64 KiB offset range), four-step groups where they fit
-    case 77: return launch_nb<K, R, 2, kNB, 16, 4>(e, st);
-    case 78: return launch_nb<K, R, 2, 2, 16, 4>(e, st);
-    case 79: return launch_nb<K, R, K <= 6 ? 4 : 2, 2, 16, 4>(e, st);
-    // lookups fenced per dword (8 results live) for occupancy
-    case 80: return launch_nb<K, R, 1, kNB, 8, 4, 1>(e, st);
-    case 81: return launch_nb<K, R, 1, kNB, 8, 6, 1>(e, st);
-    case 82: return launch_nb<K, R, kD2, 2, 16, 4, 1>(e, st);
-    case 83: return launch_nb<K, R, kD2, 2, 16, 8, 1>(e, st);
-    case 84: return launch_nb<K, R, 1, 2, 8, 6, 1>(e, st);
-    // workgroup sizes that fill the VGPR-limited wave slots (occupancy is per workgroup)
-    case 85: return launch_nb<K, R, 1, kNB, 10, 4>(e, st);
-    case 86: return launch_nb<K, R, kD2, 2, 14, 4>(e, st);
     case 87: return launch_nb<K, R, kD2, 2, 12, 4>(e, st);
-    case 88: return launch_nb<K, R, 1, kNB, 10, 5>(e, st);
-    case 89: return launch_nb<K, R, 1, kNB, 12, 4>(e, st);
-    case 93: return launch_nb<K, R, K == 10 ? 1 : kD2, K == 10 ? kNB : 2, K == 10 ? 8 : 12, 4, 0>(e, st);
-    case 94: return launch_nb<K, R, K == 10 ? 1 : kD2, K == 10 ? kNB : 2, K == 10 ? 8 : 12, 4, 4>(e, st);
-    case 95: return launch_nb<K, R, K == 10 ? 1 : kD2, 2, K == 10 ? 8 : 12, 4, 0>(e, st);
-    // persistent grid fed by the WorkQueue: the widest step groups whose tables fit one workgroup per CU (rs-10-x:
-    // D = 2, 95 KiB; rs-6-x / rs-3-x: D = 4, 117 / 69 KiB), and the round-2 geometries made persistent
-    case 100: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 1>(e, st);
-    case 101: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 1>(e, st);
-    case 102: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1>(e, st);
-    case 103: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 1>(e, st);
-    case 104: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1>(e, st);
-    case 105: return launch_nb<K, R, kDmax, 2, 12, 4, 2, true, 1>(e, st);
-    // the same geometry (round-2 rs-10-x default) with the static persistent order, guided claims, late claims
-    case 106: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 2>(e, st);
-    case 107: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 3>(e, st);
-    case 108: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 4>(e, st);
-    case 109: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 3>(e, st);
-    case 110: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 3>(e, st);
-    case 111: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 2>(e, st);
-    // deeper input rings: the loads of a whole step (K blocks) in flight ahead of the lookups
-    // probe: the round-2 rs-10-x default with one occupancy query of its kernel first (does the query change how the
-    // kernel runs?)
-    case 115: {
-      static bool asked = false;
-      if (!asked) {
-        int per_cu = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, encode_crc_nb<K, R, 1, kNB, 8, 4>, 8 * 64, 0);
-        asked = true;
-      }
-      return launch_nb<K, R, 1, kNB, 8, 4>(e, st);
-    }
-    case 120: return launch_nb<K, R, 1, K, 8, 4>(e, st);
-    case 121: return launch_nb<K, R, kD2, K, 12, 4>(e, st);
-    case 122: return launch_nb<K, R, kD2, K, 8, 4>(e, st);
-    case 123: return launch_nb<K, R, 1, K, 8, 5>(e, st);
-    case 112: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 5>(e, st);
-    case 113: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 5>(e, st);
-    case 114: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 5>(e, st);
-    // output registers shifted once per 2 / 4 steps (the input registers as before)
-    case 130: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 2>(e, st);
-    case 131: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 4>(e, st);
-    case 132: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, 4>(e, st);
-    case 133: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, 2>(e, st);
-    case 134: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 1, 4>(e, st);
-    case 135: return launch_nb<K, R, 1, 2, 8, 4, 2, true, 0, 4>(e, st);
-    // probes: the rs-10-x (62) and rs-6-x (87) defaults with 64 / 192 more VALU or 16 / 48 more LDS reads per step
-    case 140: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 64, 0>(e, st);
-    case 141: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 192, 0>(e, st);
-    case 142: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 16>(e, st);
-    case 143: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 48>(e, st);
-    case 144: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 64, 0>(e, st);
-    case 145: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 192, 0>(e, st);
-    case 146: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 16>(e, st);
-    case 147: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 48>(e, st);
-    // round 3: free output-register shifts (XO) on the rs-10-x default (102 / 62) and rs-6-x default (87)
-    // geometries, and the geometries the saved LDS work may favour
-    case 150: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, 1, 0, 0, true>(e, st);
-    case 151: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 0, true>(e, st);
-    case 152: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 0, true>(e, st);
-    case 153: return launch_nb<K, R, 1, 2, 8, 4, 2, true, 0, 1, 0, 0, true>(e, st);
-    case 154: return launch_nb<K, R, 1, kNB, 8, 5, 2, true, 0, 1, 0, 0, true>(e, st);
-    case 155: return launch_nb<K, R, kD2, 2, 16, 4, 2, true, 0, kD2, 0, 0, true>(e, st);
-    case 156: return launch_nb<K, R, 1, 2, 12, 4, 2, true, 0, 1, 0, 0, true>(e, st);
-    case 157: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 1, kD2, 0, 0, true>(e, st);
-    case 158: return launch_nb<K, R, 1, kNB, 10, 4, 2, true, 0, 1, 0, 0, true>(e, st);
-    // XO with the widest input step groups whose tables fit one workgroup per CU (rs-10-x: D = 2; rs-6-x: D = 4),
-    // persistent (WorkQueue) and not, and the rs-6-x default geometry in 8-wave workgroups
-    case 159: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 1, kDmax, 0, 0, true>(e, st);
-    case 160: return launch_nb<K, R, kDmax, 2, 16, 4, 2, true, 0, kDmax, 0, 0, true>(e, st);
-    case 161: return launch_nb<K, R, kDmax, kNB, 16, 4, 2, true, 1, kDmax, 0, 0, true>(e, st);
-    case 162: return launch_nb<K, R, kD2, 2, 8, 4, 2, true, 0, kD2, 0, 0, true>(e, st);
-    case 163: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true>(e, st);
-    // the XO defaults (150: rs-10-x, 163: rs-6-x / rs-3-x) without lookup fences, with one fence per input block,
-    // with a deeper ring, a full-step ring, 14-wave workgroups
-    case 164: return launch_nb<K, R, 1, kNB, 8, 4, 0, true, 1, 1, 0, 0, true>(e, st);
-    case 165: return launch_nb<K, R, 1, kNB, 8, 4, 4, true, 1, 1, 0, 0, true>(e, st);
-    case 166: return launch_nb<K, R, 2, 2, 16, 4, 0, true, 1, 2, 0, 0, true>(e, st);
-    case 167: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true>(e, st);
-    case 168: return launch_nb<K, R, 2, 2, 14, 4, 2, true, 1, 2, 0, 0, true>(e, st);
-    case 169: return launch_nb<K, R, 1, K, 8, 4, 2, true, 1, 1, 0, 0, true>(e, st);
-    // probes (wrong results, NF): the XO D = 2 geometries (rs-10-x: 163 / 161) without the far-addressing VALU
-    case 148: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true, true>(e, st);
-    case 149: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, true>(e, st);
-    // the XO defaults (150 / 167 / 163) and their non-persistent fallbacks (151 / 152) with the lane-parallel emit
-    case 170: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, 1, 0, 0, true, false, true>(e, st);
-    case 171: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true>(e, st);
-    case 172: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true, false, true>(e, st);
-    case 173: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, 1, 0, 0, true, false, true>(e, st);
-    case 174: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, kD2, 0, 0, true, false, true>(e, st);
-    // two-step groups with the second distance set for the first H inputs only (kHp: the most whose tables stay in
-    // the 16-bit ds_read offset range; kHh: half the inputs), the rest shifted every step; 8-wave workgroups (two per
-    // CU by LDS) on the 170 geometry, and 16-wave workgroups
-    case 175: return launch_nb<K, R, 2, kNB, 8, 4, 2, true, 1, 2, 0, 0, true, false, true, kHp>(e, st);
-    case 176: return launch_nb<K, R, 2, kNB, 8, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh>(e, st);
-    case 177: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh>(e, st);
-    case 178: return launch_nb<K, R, 2, 2, 8, 4, 2, true, 1, 2, 0, 0, true, false, true, kHp>(e, st);
-    // 16-wave workgroups (measured faster than 8 for two-step groups) over H = kHp, kHh with a ring of 2, K - 3
-    case 179: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, kHp>(e, st);
-    case 180: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh>(e, st);
-    case 181: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, std::max(1, K - 3)>(e, st);
-    case 182: return launch_nb<K, R, 2, kNB, 12, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh>(e, st);
-    // the same with the lane-tree tables behind the nibble tables (LT): 177, 181, and H = kHh + 1
-    case 183: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, kHh, true>(e, st);
-    case 184: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, std::max(1, K - 3), true>(e, st);
-    case 185: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, 2, 0, 0, true, false, true, std::min(K - 1, kHh + 1), true>(e, st);
+    // round 3, free output-register shifts (XO) on the persistent WorkQueue grid: 150 = 62's geometry, 163 = two-step
+    // groups in 16-wave workgroups, 167 = 163 with a ring of K / 2
+    case 150: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true>(e, st);
+    case 163: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, true>(e, st);
+    case 167: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true>(e, st);
+    // the same with the lane-parallel emit (EM; the defaults, fused.hip): 170 = 150, 171 = 167, 172 = 163, and the
+    // non-persistent fallbacks 173 = 151 (62 + XO), 174 = 152 (87 + XO)
+    case 170: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true>(e, st);
+    case 171: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true, true>(e, st);
+    case 172: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, true, true>(e, st);
+    case 173: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, true, true>(e, st);
+    case 174: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, true, true>(e, st);
+    // two-step groups with the second distance set for the first K / 2 inputs only (H), the rest shifted every step:
+    // 8-wave (176) and 16-wave (177, the rs-10-x default) workgroups
+    case 176: return launch_nb<K, R, 2, kNB, 8, 4, 2, true, 1, true, true, kHh>(e, st);
+    case 177: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true, true, kHh>(e, st);
     default: break;
   }
-  return launch_nb<K, R, 1, 2, 8, 4>(e, st);
+  return hipErrorInvalidValue;
 }
 }  // namespace
 }  // namespace ozec

@@ -250,70 +250,7 @@ __global__ __launch_bounds__(kBlock) void gf_code_bytes(const CodeArgs a, int64_
   }
 }
 
-// One wave per (cell, window).  Lane l owns B consecutive 16-B blocks of every 64*B-block step and folds them
-// into its register (state XORed into the next block's first 4 bytes); between steps the register jumps
-// (63*B)*16 bytes.  Windows are front-padded with virtual zero blocks to a whole number of steps.
-// Requires 16-B aligned cells and bpc % 16 == 0 (the tail of a short last window goes byte-by-byte).
-template <int B>
-__global__ __launch_bounds__(kBlock) void crc_windows_vec(const CrcArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_t[kG5Words];
-  load_tables(s_t, a.tables[g5_slot(B)], kG5Words);
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: unit index lives in SGPRs
-  const int64_t units = a.ncells * a.nwin;
-  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
-  for (int64_t u = bid * (kBlock / 64) + wave; u < units; u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
-    const int64_t c = u / a.nwin;
-    const int64_t w = u - c * a.nwin;
-    const bool last = w == a.nwin - 1;
-    const int64_t N = last ? a.len - w * a.bpc : a.bpc;
-    const int64_t m = N >> 4;
-    const int64_t T = (m + 64 * B - 1) / (64 * B);
-    const int64_t P = T * 64 * B - m;  // virtual zero blocks in front
-    const uint8_t *win = a.base + c * a.cell_stride + w * a.bpc;
-    uint32_t S = 0;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    // step t's blocks; only step 0 holds virtual (front-padding) blocks, so only it needs the lane predicate
-    auto load_step = [&](int64_t t, uint4 (&dst)[B], bool pad) {
-#pragma unroll
-      for (int q = 0; q < B; ++q) {
-        const int64_t vb = t * 64 * B + lane * B + q - P;
-        if (!pad || vb >= 0) {
-          const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(win + vb * 16));
-          dst[q] = make_uint4(d[0], d[1], d[2], d[3]);
-        } else {
-          dst[q] = make_uint4(0, 0, 0, 0);
-        }
-      }
-    };
-    auto fold_step = [&](int64_t t, const uint4 (&src)[B]) {
-      if (t > 0) S = g5_shift(s_t + kG5Step, S);
-#pragma unroll
-      for (int q = 0; q < B; ++q) {
-        uint4 b = src[q];
-        b.x ^= S;
-        S = g5_block(s_t, b);
-      }
-    };
-    // two register sets used alternately (no copies between steps), next step's loads in flight
-    uint4 xa[B], xb[B];
-    load_step(0, xa, true);
-    int64_t t = 0;
-    for (; t + 1 < T; t += 2) {
-      load_step(t + 1, xb, false);
-      fold_step(t, xa);
-      if (t + 2 < T) load_step(t + 2, xa, false);
-      fold_step(t + 1, xb);
-    }
-    if (t < T) fold_step(t, xa);
-    S = g5_lane_tree(s_t, S, lane);
-    for (int64_t i = m * 16; i < N; ++i) S = (S >> 8) ^ s_t[kG5T0 + ((S ^ win[i]) & 0xff)];
-    if (lane == 0) crc_emit(a, c, w, S, last);
-  }
-}
-
-// One wave per (cell, window), as crc_windows_vec, but lane l folds every block of its group of D steps
+// One wave per (cell, window).  Lane l owns 16-B blocks l, l+64, ... of the window and folds every block of its group of D steps
 // into its register through the table set of the block's distance to the group end (no per-step register
 // shift): S = shift_group(S) ^ XOR_{steps r, blocks s} G26[r*B+s](block).  Windows are front-padded with
 // virtual zero blocks to whole groups; virtual blocks are not loaded and add nothing.
@@ -511,179 +448,20 @@ __global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Fused encode + CRC: one wave per (stripe, window); each step a lane takes B consecutive 16-B blocks of
-// every data unit (lanes interleaved, 64*B blocks per step), produces the parity blocks and folds all K+R
-// units into their CRC registers while the bytes are in VGPRs.  PF: issue the next step's loads before
-// computing the current one.  Coefficient tables as in gf_code_vec (SREG: SGPR/VGPR split, else LDS).
+// Fused encode + CRC: one wave per (stripe, window); each step a lane takes the 16-B blocks of every data unit
+// (lanes interleaved, 64 blocks per step), produces the parity blocks and folds all K+R units into their CRC
+// registers while the bytes are in VGPRs.
 // XORC (all-ones single row: the XOR codec): the output is the XOR of the inputs, and since the raw CRC
 // register recursion is GF(2)-linear in (register, data), the output's register is the XOR of the inputs'
 // registers at every step -- its CRC costs no table lookups.
-template <int K, int R, bool SREG, int B, bool PF, int WAVES = 1, bool XORC = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_vec(
-    const EncCrcArgs e, const TabArgs<K * R> tabs) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_t[kG5Words];
-  __shared__ __attribute__((aligned(16))) uint32_t s_w[5][K * R];
-  const CodeArgs &a = e.code;
-  const CrcArgs &cr = e.crc;
-  load_tables(s_t, cr.tables[g5_slot(B)], kG5Words);
-  for (int t = threadIdx.x; t < K * R; t += blockDim.x)
-#pragma unroll
-    for (int q = 0; q < 5; ++q) s_w[q][t] = tabs.w[t][q];
-  __syncthreads();
-  uint32_t vlo0[SREG ? K * R : 1], vmid0[SREG ? K * R : 1];
-  if constexpr (SREG) {
-#pragma unroll
-    for (int t = 0; t < K * R; ++t) {
-      vlo0[t] = s_w[0][t];
-      vmid0[t] = s_w[2][t];
-    }
-  }
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: unit index lives in SGPRs
-  const int64_t nwin = cr.nwin;
-  const int64_t units = a.nstripes * nwin;
-  const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
-  for (int64_t u = bid * (kBlock / 64) + wave; u < units; u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
-    const int64_t s = u / nwin;
-    const int64_t w = u - s * nwin;
-    const bool last = w == nwin - 1;
-    const int64_t N = last ? a.len - w * cr.bpc : cr.bpc;
-    const int64_t m = N >> 4;
-    const int64_t T = (m + 64 * B - 1) / (64 * B);
-    const int64_t P = T * 64 * B - m;
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, s) + w * cr.bpc);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
-    uint32_t S[K + R];
-#pragma unroll
-    for (int q = 0; q < K + R; ++q) S[q] = 0;
-    uint4 x[B][K], xn[PF ? B : 1][K];
-    auto load = [&](int64_t t, uint4 (&dst)[B][K]) {
-      const bool pad = t == 0 && P > 0;  // wave-uniform: only step 0 holds virtual front blocks
-#pragma unroll
-      for (int q = 0; q < B; ++q) {
-        const int64_t vb = t * 64 * B + lane * B + q - P;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          if (t < T && (!pad || vb >= 0)) {
-            const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<uint32_t>(vb) * 16u,
-                                                                 static_cast<int>(a.in_off[j]), 2);
-            dst[q][j] = make_uint4(d[0], d[1], d[2], d[3]);
-          } else {
-            dst[q][j] = make_uint4(0, 0, 0, 0);
-          }
-        }
-      }
-    };
-    if constexpr (PF) load(0, x);
-    for (int64_t t = 0; t < T; ++t) {
-      if constexpr (!SREG) asm volatile("" ::: "memory");
-      if constexpr (PF) {
-        load(t + 1, xn);
-      } else {
-        load(t, x);
-      }
-#pragma unroll
-      for (int q = 0; q < B; ++q) {
-        const int64_t vb = t * 64 * B + lane * B + q - P;
-        uint4 acc[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          if constexpr (XORC) {
-            acc[0].x ^= x[q][j].x;
-            acc[0].y ^= x[q][j].y;
-            acc[0].z ^= x[q][j].z;
-            acc[0].w ^= x[q][j].w;
-            continue;
-          }
-          const Sel sx = make_sel(x[q][j].x), sy = make_sel(x[q][j].y), sz = make_sel(x[q][j].z),
-                    sw = make_sel(x[q][j].w);
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int tt = r * K + j;
-            uint4 mm;
-            if constexpr (SREG) {
-              const RegTab tb{vlo0[tt], vmid0[tt], tabs.w[tt][1], tabs.w[tt][3], tabs.w[tt][4]};
-              mm.x = gf_mul4_reg(tb, sx);
-              mm.y = gf_mul4_reg(tb, sy);
-              mm.z = gf_mul4_reg(tb, sz);
-              mm.w = gf_mul4_reg(tb, sw);
-            } else {
-              const PermTab tb{s_w[0][tt], s_w[1][tt], s_w[2][tt], s_w[3][tt], s_w[4][tt]};
-              mm.x = gf_mul4_lds(tb, sx);
-              mm.y = gf_mul4_lds(tb, sy);
-              mm.z = gf_mul4_lds(tb, sz);
-              mm.w = gf_mul4_lds(tb, sw);
-            }
-            acc[r].x ^= mm.x;
-            acc[r].y ^= mm.y;
-            acc[r].z ^= mm.z;
-            acc[r].w ^= mm.w;
-          }
-        }
-        if (vb >= 0) {
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
-            __builtin_amdgcn_raw_buffer_store_b128(d, rout, static_cast<uint32_t>(vb) * 16u,
-                                                   static_cast<int>(a.out_off[r]), 2);
-          }
-        }
-        // CRC: the first block of a step jumps the register (63*B)*16 bytes, then every block folds in
-#pragma unroll
-        for (int j = 0; j < (XORC ? K : K + R); ++j) {
-          uint4 b = j < K ? x[q][j] : acc[j - K];
-          if (q == 0) b.x ^= t > 0 ? g5_shift(s_t + kG5Step, S[j]) : 0u;
-          else b.x ^= S[j];
-          S[j] = g5_block(s_t, b);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if constexpr (PF) {
-#pragma unroll
-        for (int q = 0; q < B; ++q)
-#pragma unroll
-          for (int j = 0; j < K; ++j) x[q][j] = xn[q][j];
-      }
-    }
-    if constexpr (XORC) {
-      S[K] = 0;
-#pragma unroll
-      for (int j = 0; j < K; ++j) S[K] ^= S[j];
-    }
-    const uint32_t init = last ? cr.init_last : cr.init_full;
-#pragma unroll
-    for (int q = 0; q < K + R; ++q) {
-      const uint32_t v = g5_lane_tree(s_t, S[q], lane);
-      if (lane == q) {
-        if (!e.verify) {
-          cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
-        } else if (q >= K) {
-          cr.out[(s * R + (q - K)) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
-        } else if (cr.expected) {
-          const int64_t idx = (s * e.exp_units + e.in_unit[q]) * nwin + w;
-          const uint32_t ex = cr.expected_be ? __builtin_bswap32(cr.expected[idx]) : cr.expected[idx];
-          if (crc_finish(v, init, 0, 0) != ex)
-            atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[q] * nwin + w));
-        }
-      }
-    }
-  }
-}
-
 // Fused encode + CRC on the G26 scheme (B = 1): one wave per (stripe, window), D steps per group, every
 // unit's register updated with S ^= G26[D-1-rr](block) and shifted once per group.  GF coefficient tables
 // (TM): 1 = {lo0, lo1, mid0, mid1} from LDS in one ds_read_b128 broadcast + top as an SGPR operand;
 // 2 = lo1/mid1/top as SGPR operands, {lo0, mid0} from LDS in one ds_read_b64 broadcast; 3 = as 1 with top from
 // LDS too (ds_read_b32 broadcast).
-// PAD > 0 (diagnostic variants only): PAD extra independent VALU ops per step, to measure what one more VALU
-// instruction costs the kernel (scripts/gpu_valu_pad.sh; DESIGN §2.3 "what bounds it").
 // XO (XOR codec only): the input registers move by one step with no shift lookups (kernels.hpp kXo*; as
 // crc_windows_g26s), the parity's register is still the XOR of theirs, and the advance is undone once per window.
-template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false, bool HV = false, int PAD = 0,
-          int PADK = 0, bool VMASK = false, bool XO = false>
+template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false, bool HV = false, bool XO = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_g26(const EncCrcArgs e, const TabArgs<K * R> tabs) {
   constexpr int E = D;
   static_assert(D >= 1, "group of at least one step");
@@ -739,9 +517,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     };
     static_assert(!PF || D % 2 == 0, "prefetch alternates two register sets");
     uint4 xa[K], xb[K];
-    uint32_t pad[4] = {0, 0, 0, 0};
-    uint32_t vmask = 0x7cu;
-    if constexpr (VMASK) asm volatile("v_mov_b32 %0, 0x7c" : "=v"(vmask));  // materialised once, lives in a VGPR
+    const uint32_t vmask = 0x7cu;
     if (PF && G > 0) load_x(0, xa);
     for (int32_t g = 0; g < G; ++g) {
 #pragma unroll
@@ -813,30 +589,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
           if constexpr (XO) {
             uint4 xs = x[j];
             xs.x ^= S[j];
-            S[j] = g26_block<HV, VMASK>(s_t + kXoOff, xs, vmask);
+            S[j] = g26_block<HV, false>(s_t + kXoOff, xs, vmask);
           } else {
-            S[j] ^= g26_block<HV, VMASK>(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K], vmask);
+            S[j] ^= g26_block<HV, false>(s_t + (D - 1 - rr) * kG26Set, j < K ? x[j] : acc[j - K], vmask);
           }
           __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (PAD > 0) {  // PADK: 0 v_xor_b32 (fast class), 1 v_perm_b32 (slow class), 2 ds_read_b32
-#pragma unroll
-          for (int i = 0; i < PAD; i += 4) {
-            if constexpr (PADK == 0)
-              asm volatile("v_xor_b32 %0, %0, %4\n\tv_xor_b32 %1, %1, %4\n\tv_xor_b32 %2, %2, %4\n\tv_xor_b32 %3, %3, %4"
-                           : "+v"(pad[0]), "+v"(pad[1]), "+v"(pad[2]), "+v"(pad[3])
-                           : "v"(S[0]));
-            else if constexpr (PADK == 1)
-              asm volatile("v_perm_b32 %0, %0, %4, %4\n\tv_perm_b32 %1, %1, %4, %4\n\tv_perm_b32 %2, %2, %4, %4\n\t"
-                           "v_perm_b32 %3, %3, %4, %4"
-                           : "+v"(pad[0]), "+v"(pad[1]), "+v"(pad[2]), "+v"(pad[3])
-                           : "v"(S[0]));
-            else
-              asm volatile("ds_read_b32 %0, %4\n\tds_read_b32 %1, %4 offset:256\n\tds_read_b32 %2, %4 offset:512\n\t"
-                           "ds_read_b32 %3, %4 offset:768\n\ts_waitcnt lgkmcnt(0)"
-                           : "=v"(pad[0]), "=v"(pad[1]), "=v"(pad[2]), "=v"(pad[3])
-                           : "v"(static_cast<uint32_t>(lane * 4)));
-          }
         }
       }
       if (!XO && g + 1 < G) {
@@ -853,7 +610,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 #pragma unroll
       for (int q = 0; q <= K; ++q) S[q] = g5_shift(s_t + kXoOff + kXoInv, S[q]);
     }
-    if constexpr (PAD > 0) S[0] ^= (pad[0] ^ pad[1] ^ pad[2] ^ pad[3]) & 0u;  // keeps the pad live, changes nothing
     const uint32_t init = last ? cr.init_last : cr.init_full;
 #pragma unroll
     for (int q = 0; q < K + R; ++q) {
@@ -1066,7 +822,8 @@ hipError_t launch_krv(const CodeArgs &a, hipStream_t st, int64_t default_grid) {
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
   const int64_t units = a.nstripes * ((nvec + kBlock * VPT - 1) / (kBlock * VPT));
   const TabArgs<K * R> tabs = host_tabs<K * R>(a);
-  int64_t grid = g_tune.grid > 0 ? g_tune.grid : default_grid;
+  const int64_t tg = g_tune.grid;
+  int64_t grid = tg > 0 ? tg : default_grid;
   grid = std::max<int64_t>(1, std::min<int64_t>(grid, units));
   hipLaunchKernelGGL((gf_code_vec<K, R, kSreg, VPT, LAUX, SAUX, OPT>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0,
                      st, a, tabs);
@@ -1076,24 +833,17 @@ hipError_t launch_krv(const CodeArgs &a, hipStream_t st, int64_t default_grid) {
 // Defaults measured on MI355X (scripts/tune.py, scripts/tune_all.py, profiles/r01/tune_*.log): one 4 KiB chunk
 // per block on a non-persistent grid (XCD-contiguous block order, xcd_remap) with non-temporal loads and stores,
 // for register-table and LDS-table kernels alike (C2 77.9 %, C3 77.9 % of the HBM roofline).
-// ozec_set_tuning("gf_variant", 1..6) pins one (VPT, load policy, store policy) combination.
+// ozec_set_tuning("gf_variant", v) pins an alternate for A/B (kernels.hpp kGfVariants): 1 plain (cached) loads and
+// stores, 5 two 16-B vectors per lane per unit (8 KiB chunks, 8192 blocks), 11 parity in three-input XOR chains
+// (-6.5 % VALU, no faster: profiles/r02/gf/ab_gf_variants.log).  (The other cache-policy and selector-mask variants of
+// rounds 1-2 were taken out of the library.)
 template <int K, int R>
 hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
   constexpr int64_t kAll = int64_t{1} << 40;
-  switch (g_tune.gf_variant) {
+  switch (g_tune.gf_variant.load(std::memory_order_relaxed)) {
     case 1: return launch_krv<K, R, 1, 0, 0>(a, st, kAll);
-    case 2: return launch_krv<K, R, 1, 2, 0>(a, st, kAll);
-    case 3: return launch_krv<K, R, 1, 0, 2>(a, st, kAll);
-    case 4: return launch_krv<K, R, 1, 2, 2>(a, st, kAll);
     case 5: return launch_krv<K, R, 2, 0, 0>(a, st, 8192);
-    case 6: return launch_krv<K, R, 2, 2, 2>(a, st, 8192);
-    case 7: return launch_krv<K, R, 1, 2, 16>(a, st, kAll);   // sc1 (write-through) stores
-    case 8: return launch_krv<K, R, 1, 2, 18>(a, st, kAll);   // sc1 nt stores
-    case 9: return launch_krv<K, R, 1, 18, 18>(a, st, kAll);  // sc1 nt loads and stores
-    case 10: return launch_krv<K, R, 1, 16, 2>(a, st, kAll);  // sc1 loads
-    case 11: return launch_krv<K, R, 1, 2, 2, 1>(a, st, kAll);  // XOR chains
-    case 12: return launch_krv<K, R, 1, 2, 2, 2>(a, st, kAll);  // selector masks in VGPRs
-    case 13: return launch_krv<K, R, 1, 2, 2, 3>(a, st, kAll);  // both
+    case 11: return launch_krv<K, R, 1, 2, 2, 1>(a, st, kAll);
     default: break;
   }
   return launch_krv<K, R, 1, 2, 2>(a, st, kAll);
@@ -1168,11 +918,12 @@ namespace {
 // blocks when that knob is set.  The grid is not persistent: blocks start in order, so the waves in flight
 // stream neighbouring stretches of HBM.
 int64_t stream_per_wave(int64_t total, int64_t bpc) {
-  if (g_tune.crc_grid > 0) {
-    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(g_tune.crc_grid * (kBlock / 64), total));
+  const int64_t cg = g_tune.crc_grid, cr = g_tune.crc_run;
+  if (cg > 0) {
+    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(cg * (kBlock / 64), total));
     return (total + waves - 1) / waves;
   }
-  const int64_t run = g_tune.crc_run > 0 ? g_tune.crc_run : int64_t{256} << 10;
+  const int64_t run = cr > 0 ? cr : int64_t{256} << 10;
   return std::max<int64_t>(1, run / bpc);
 }
 
@@ -1217,35 +968,21 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
   const bool vec = aligned16(reinterpret_cast<intptr_t>(a.base)) && (a.ncells == 1 || aligned16(a.cell_stride)) &&
                    aligned16(a.bpc);
   if (vec) {
-    const int v = g_tune.crc_variant;
-    // streaming kernel for windows of whole 4 KiB groups, (D, ring) = (4, 2) with free register shifts (XO); variants
-    // 20-24 for A/B (scripts/tune_crc.py): (4, 2), (8, 4), (4, 4), (8, 8), (2, 2) with D-step groups; 25-27 with XO:
-    // (4, 4), (4, 2), (8, 4)
-    if ((v == 0 || v >= 20) && a.bpc % (v == 21 || v == 23 || v == 27 ? 8192 : v == 24 ? 2048 : 4096) == 0) {
-      switch (v) {
-        case 25: return launch_crc_stream<4, 4, true>(a, st);
-        case 26: return launch_crc_stream<4, 2, true>(a, st);
-        case 27: return launch_crc_stream<8, 4, true>(a, st);
-        case 20: return launch_crc_stream<4, 2>(a, st);
-        case 21: return launch_crc_stream<8, 4>(a, st);
-        case 23: return launch_crc_stream<8, 8>(a, st);
-        case 24: return launch_crc_stream<2, 2>(a, st);
-        case 22: return launch_crc_stream<4, 4>(a, st);  // the round-2 default
-        // default (round 3): free register shifts, ring of 2 (CRC32C 78.5 -> 80.3 %, verify 77.8 -> 80.3 % in
-        // same-process A/Bs, profiles/r03/ab/crcxo_*.log)
-        default: return launch_crc_stream<4, 2, true>(a, st);
-      }
+    const int v = g_tune.crc_variant.load(std::memory_order_relaxed);
+    // streaming kernel for windows of whole 4 KiB groups, (D, ring) = (4, 2) with free register shifts (XO): CRC32C
+    // 78.5 -> 80.3 %, verify 77.8 -> 80.3 % in same-process A/Bs (profiles/r03/ab/crcxo_*.log) against the D-step
+    // groups of rounds 1-2, which variants 20 (ring of 2) and 22 (ring of 4, the round-2 default) keep for A/B
+    if (a.bpc % 4096 == 0) {
+      if (v == 20) return launch_crc_stream<4, 2>(a, st);
+      if (v == 22) return launch_crc_stream<4, 4>(a, st);
+      return launch_crc_stream<4, 2, true>(a, st);
     }
     // per-window kernel: G26 tables, B = 1 block per lane per step, groups of D = 4 steps, two steps of loads in
     // flight, 16384 blocks (scripts/tune_crc.py)
-    const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : 16384;
+    const int64_t cg = g_tune.crc_grid;
+    const int64_t g = cg > 0 ? cg : 16384;
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
-    switch (v) {
-      case 1: hipLaunchKernelGGL(crc_windows_vec<2>, grid, block, 0, st, a); break;  // round-1 kernel, for A/B
-      case 11: hipLaunchKernelGGL((crc_windows_g26<1, 4, 1>), grid, block, 0, st, a); break;
-      case 12: hipLaunchKernelGGL((crc_windows_g26<2, 2, 1>), grid, block, 0, st, a); break;
-      default: hipLaunchKernelGGL((crc_windows_g26<1, 4, 2>), grid, block, 0, st, a); break;
-    }
+    hipLaunchKernelGGL((crc_windows_g26<1, 4, 2>), grid, block, 0, st, a);
   } else {
     hipLaunchKernelGGL(crc_windows_bytes, dim3(grid_for(units, kBlock)), dim3(kBlock), 0, st, a);
   }
@@ -1270,21 +1007,12 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
   // defaults measured on MI355X (scripts/tune_crc.py, profiles/r01/session2/tune_g26*.log): one wave per window
   // with no grid-stride, G26 tables in groups of D = 2 steps, coefficient tables {lo0,lo1,mid0,mid1} by one
   // ds_read_b128 broadcast and `top` as an SGPR operand (all from LDS past 18 coefficients: SGPR budget)
-  const int64_t g = g_tune.crc_grid > 0 ? g_tune.crc_grid : (units + 3) / 4;
+  const int64_t cg = g_tune.crc_grid;
+  const int64_t g = cg > 0 ? cg : (units + 3) / 4;
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
   constexpr int kTM = K * R <= 18 ? 1 : 3;
   constexpr int kW = K + R >= 12 ? 3 : 4;  // rs-10-x: 14 unit registers and operands do not fit 128 VGPRs
-  const int v = g_tune.crc_variant;
-  if (v == 1) {  // round-1 kernel (5-bit groups at fixed offsets, register shift every step), kept for A/B
-    if constexpr (R == 1) {
-      if (e.code.all_ones) {
-        hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false, 1, true>), grid, block, 0, st, e, tabs);
-        return hipGetLastError();
-      }
-    }
-    hipLaunchKernelGGL((encode_crc_vec<K, R, false, 1, false>), grid, block, 0, st, e, tabs);
-    return hipGetLastError();
-  }
+  const int v = g_tune.crc_variant.load(std::memory_order_relaxed);
   if constexpr (R == 1 && K <= 6) {
     // XOR codec, every window full: the streaming kernel, for A/B only (variants 20 / 21: ring of 2 / 4 steps).
     // On C4 it reaches 62-71 % of the HBM roofline against 72-73 % for the per-window kernel below at every grid
@@ -1300,55 +1028,19 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
       // XOR codec: D = 4 with the next step's loads in flight (C4 77.9 % vs 75.8 % for D = 2, ab_c4.log)
       if (v == 3) hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1>), grid, block, 0, st, e, tabs);
       else if (v == 4)  // free register shifts (XO)
-        hipLaunchKernelGGL((encode_crc_g26<K, R, 4, true, 1, 4, true, false, 0, 0, false, true>), grid, block, 0, st, e, tabs);
+        hipLaunchKernelGGL((encode_crc_g26<K, R, 4, true, 1, 4, true, false, true>), grid, block, 0, st, e, tabs);
       else if (v == 5)
-        hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1, 4, true, false, 0, 0, false, true>), grid, block, 0, st, e, tabs);
+        hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1, 4, true, false, true>), grid, block, 0, st, e, tabs);
       else hipLaunchKernelGGL((encode_crc_g26<K, R, 4, true, 1, 4, true>), grid, block, 0, st, e, tabs);
       return hipGetLastError();
     }
   }
-  if constexpr (K == 6 && R == 3) {  // the headline shape carries the tuning variants (scripts/tune_crc.py)
-    switch (v) {
-      case 11: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, 1>), grid, block, 0, st, e, tabs); break;
-      case 12: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 1, 4, true>), grid, block, 0, st, e, tabs); break;
-      case 13: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 3>), grid, block, 0, st, e, tabs); break;
-      case 14: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 2>), grid, block, 0, st, e, tabs); break;
-      // CRC lookups of a block in two fenced halves (g26_block<true>: at most 14 results live) and groups of D = 4
-      // steps: 123 VGPRs, 0 spilled.  Interleaved A/Bs (profiles/r01/session4/ab_c5*.log): halves at D = 2 +0.6 %
-      // over the fence-free block (105 instead of 114 VGPRs), D = 4 on top +2.7 %; 5 waves per SIMD gained nothing.
-      // 15: fence-free D = 2 (the default until session 4); 16: halves, D = 2, 5 waves; 17: halves, D = 2.
-      case 15: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM>), grid, block, 0, st, e, tabs); break;
-      case 16: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 5, false, true>), grid, block, 0, st, e, tabs); break;
-      case 17: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs); break;
-      case 40: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 64>), grid, block, 0, st, e, tabs); break;
-      case 41: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 192>), grid, block, 0, st, e, tabs); break;
-      case 42: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 192, 1>), grid, block, 0, st, e, tabs); break;
-      case 43: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 192, 2>), grid, block, 0, st, e, tabs); break;
-      case 44: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true, 0, 0, true>), grid, block, 0, st, e, tabs); break;
-      default: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs); break;
-    }
-  } else {
-    switch (v) {
-      case 11: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, kW>), grid, block, 0, st, e, tabs); break;
-      case 12: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW, true>), grid, block, 0, st, e, tabs); break;
-      case 13: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, 1, kW>), grid, block, 0, st, e, tabs); break;
-      case 14: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, 2>), grid, block, 0, st, e, tabs); break;
-      case 17: hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, kW, false, true>), grid, block, 0, st, e, tabs); break;
-      case 40:
-        if constexpr (K == 10 && R == 4)
-          hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW, false, false, 64>), grid, block, 0, st, e, tabs);
-        break;
-      case 41:
-        if constexpr (K == 10 && R == 4)
-          hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW, false, false, 192>), grid, block, 0, st, e, tabs);
-        break;
-      case 44:
-        if constexpr (K == 10 && R == 4)
-          hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW, false, false, 0, 0, true>), grid, block, 0, st, e, tabs);
-        break;
-      default: hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW>), grid, block, 0, st, e, tabs); break;
-    }
-  }
+  // per-window kernel (variant 49 pins it for the RS shapes the nibble kernel also takes): CRC lookups of a block in
+  // two fenced halves; groups of D = 4 steps for rs-6-3 (123 VGPRs, 0 spilled), D = 2 where 14 unit registers and
+  // their operands must fit 128 VGPRs (profiles/r01/session4/ab_c5*.log; the other round-1 geometries, 11-17, were
+  // slower and are gone)
+  if constexpr (K == 6 && R == 3) hipLaunchKernelGGL((encode_crc_g26<K, R, 4, false, kTM, 4, false, true>), grid, block, 0, st, e, tabs);
+  else hipLaunchKernelGGL((encode_crc_g26<K, R, 2, false, kTM, kW>), grid, block, 0, st, e, tabs);
   return hipGetLastError();
 }
 
@@ -1371,7 +1063,7 @@ hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   if (!rebase32(e.code)) return hipErrorInvalidValue;
   // full windows of the RS shapes: the nibble-table kernel (fused.hip; 50-59 the streamed-input kernel); variant 49
   // pins the per-window kernel
-  const int v = g_tune.crc_variant;
+  const int v = g_tune.crc_variant.load(std::memory_order_relaxed);
   if ((v == 0 || (v >= 50 && v < 200)) && encode_crc_lv_supported(e)) return launch_encode_crc_lv(e, st, v);
   const int k = e.code.k, r = e.code.rows;
 #define OZEC_SHAPE_LAUNCH(KK, RR) \

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 
 #include "../../include/ozec.h"
@@ -135,23 +136,39 @@ constexpr int kXoAdvance = 1024 - 16;
 constexpr int kXoInv = kG26Set;
 constexpr int kXoWords = kG26Set + 224;
 
-// Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.
+// Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.  Process-wide harness knobs for A/B and profiling
+// runs (bench.py --tune, scripts/ab.py): every field is an atomic, so setting one while other threads launch is not a
+// data race, but a set knob applies to every caller's next launch -- a production process leaves them at 0.
 struct TuneKnobs {
-  int64_t grid = 0;       // blocks for the coding kernels
-  int gf_variant = 0;     // coding-kernel variant 1..6 (VPT / cache policy), see launch_kr
-  int crc_variant = 0;    // CRC kernel: 1/4 = B (default 2); fused: 2 no XOR-codec register shortcut,
-                          //   3 SGPR tables, 5 prefetch, 6 B = 2, 7 both, 8 = at least 5 waves per SIMD
-  int64_t crc_grid = 0;   // blocks for the CRC / fused kernels
-  int64_t crc_run = 0;    // streaming CRC kernels: bytes of consecutive windows per wave (default 256 KiB)
-  int unit_map = 0;       // CodeArgs::unit_map for the coding kernels
-  int64_t host_chunk = 4 << 20;  // host-buffer calls: bytes per unit per pipelined chunk (per-chunk stream
-                                 // latency ~20 us: 256 KiB chunks ran 16 MiB CRC updates at 2.7 GB/s, 4 MiB at 18)
-  int64_t host_chunk_shared = 512 << 10;  // the same while other host-buffer calls hold slots (0: host_chunk always)
-  int64_t host_slots = 8;          // host-buffer calls: staging slots (concurrent calls) per GPU
-  int64_t queue_batches = 0;       // stripe queue: batches in the ring (0 = default), read at queue creation
-  int64_t e2e_chunk = 32;          // ozec_encode_crc_host_batch: stripes per pipelined chunk when the caller passes 0
-  int e2e_rect = 1;                // ozec_encode_crc_host_batch: one rectangular copy per chunk (0: one per stripe)
+  std::atomic<int64_t> grid{0};       // blocks for the coding kernels
+  std::atomic<int> gf_variant{0};     // coding-kernel alternate, one of kGfVariants (kernels.hip launch_kr)
+  std::atomic<int> crc_variant{0};    // CRC / fused-kernel alternate, one of kCrcVariants
+  std::atomic<int64_t> crc_grid{0};   // blocks for the CRC / fused kernels
+  std::atomic<int64_t> crc_run{0};    // streaming CRC kernels: bytes of consecutive windows per wave (default 256 KiB)
+  std::atomic<int> unit_map{0};       // CodeArgs::unit_map for the coding kernels
+  std::atomic<int64_t> host_chunk{4 << 20};  // host-buffer calls: bytes per unit per pipelined chunk (per-chunk stream
+                                             // latency ~20 us: 256 KiB chunks ran 16 MiB CRC updates at 2.7 GB/s, 4 MiB
+                                             // at 18)
+  std::atomic<int64_t> host_chunk_shared{512 << 10};  // the same while other host-buffer calls hold slots (0: host_chunk)
+  std::atomic<int64_t> host_slots{8};        // host-buffer calls: staging slots (concurrent calls) per GPU
+  std::atomic<int64_t> queue_batches{0};     // stripe queue: batches in the ring (0 = default), read at queue creation
+  std::atomic<int64_t> e2e_chunk{32};        // host batches: stripes per pipelined chunk when the caller passes 0
+  std::atomic<int> e2e_rect{1};              // host batches: one rectangular copy per chunk (0: one per stripe)
 };
+
+// Kernel alternates the library holds besides the defaults, selectable with ozec_set_tuning for A/B (0 = default).
+// Every id has a parity test (tests/variants.py lists them; tests/test_variants.py checks the lists agree with
+// ozec_tuning_variants); ozec_set_tuning rejects any other id.
+//   gf_variant (coding kernel gf_code_vec, kernels.hip launch_kr): 1, 5, 11
+//   crc_variant, by kernel family:
+//     streaming CRC (launch_crc_windows): 20, 22 -- D-step groups instead of the XO default
+//     fused XOR codec (launch_enc_crc_kr, R = 1 all-ones): 2 no register shortcut, 3 D = 2, 4 / 5 XO with D = 4 / 2,
+//       20 / 21 streaming kernel with a ring of 2 / 4 steps
+//     fused RS (launch_encode_crc): 49 per-window kernel, 56 / 59 streamed-input kernel (fused.hip), 62 / 87 / 150 /
+//       163 / 167 / 170-174 / 176 / 177 nibble-table kernel (fused_nb.hpp launch_nb_kr)
+constexpr int kGfVariants[] = {1, 5, 11};
+constexpr int kCrcVariants[] = {2, 3, 4, 5, 20, 21, 22, 49, 56, 59, 62, 87, 150, 163, 167, 170, 171, 172, 173, 174, 176, 177};
+
 extern TuneKnobs g_tune;
 
 hipError_t launch_code(const CodeArgs &a, hipStream_t stream);

@@ -156,6 +156,16 @@ int pinned_free(void *p) {
   return 0;
 }
 
+const void *pinned_alloc_base(const void *p) {
+  void *base = nullptr;
+  if (hipPointerGetAttribute(&base, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void *>(p))) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return base;
+}
+
 int bind_thread_to_node(int node) {
   if (node < 0) return 0;
   std::string s;

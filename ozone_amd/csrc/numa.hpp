@@ -18,6 +18,9 @@ int page_node(const void *p);
 // pinned host allocation whose pages live on the device's node; free with pinned_free
 int pinned_alloc(size_t bytes, int device, void **out);
 int pinned_free(void *p);
+// start of the pinned / registered host allocation holding p (null when p is not in one): a DMA (a 2D copy's rows
+// included) must lie within one allocation
+const void *pinned_alloc_base(const void *p);
 // pin the calling thread / the copy-pool workers to the CPUs of `node` (intersected with the process mask)
 int bind_thread_to_node(int node);
 

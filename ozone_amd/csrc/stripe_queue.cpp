@@ -65,15 +65,7 @@ struct Pending {
 // one pinned pool (or from the staging area) form such runs; per-copy overhead was what held the queue at 84 % of
 // the link while the host batch, which copies rectangles, reached 98 %.
 // Start of the pinned allocation holding host pointer p (null when unknown): a 2D copy's rows must lie in one.
-const void *alloc_base(const void *p) {
-  void *base = nullptr;
-  if (hipPointerGetAttribute(&base, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
-                             reinterpret_cast<hipDeviceptr_t>(const_cast<void *>(p))) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  return base;
-}
+const void *alloc_base(const void *p) { return ozec::pinned_alloc_base(p); }
 
 struct CopyRun {
   const uint8_t *src = nullptr;
@@ -327,7 +319,8 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
   q->cell_len = cell_len;
   q->S = stripes_per_batch;
   q->nwin_max = q->nwin(cell_len);
-  q->batches.resize(ozec::g_tune.queue_batches >= 2 ? static_cast<size_t>(ozec::g_tune.queue_batches) : kDefaultBatches);
+  const int64_t qb = ozec::g_tune.queue_batches.load();
+  q->batches.resize(qb >= 2 ? static_cast<size_t>(qb) : kDefaultBatches);
   for (Batch &b : q->batches) {
     b.pend.resize(q->S);
     hipError_t e = q->h2d ? hipSuccess : hipStreamCreateWithFlags(&q->h2d, hipStreamNonBlocking);

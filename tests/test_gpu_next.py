@@ -5,6 +5,7 @@ import pytest
 
 import oracle
 from synth import SEED, cells
+import variants
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -65,13 +66,10 @@ def _stripe_units(codec, k, p, n, S, first):
     ("rs", 5, 2, [0, 6], 1 << 16, 16384),         # unfused fallback (shape not instantiated)
     ("rs", 6, 3, [0, 2, 7], 50000, 1000),         # unfused fallback (bpc not a multiple of 16)
 ])
-@pytest.mark.parametrize("variant", [0, 4, 5, 49, 54, 61, 62, 63, 65, 66, 67, 73, 74, 75, 77, 78, 79, 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, 111, 112, 113, 114, 120, 121, 122, 123, 130, 131, 132, 133, 134, 135,
-                                     150, 151, 152, 153, 154, 155, 156, 157, 158, 159, 160, 161, 162, 163, 164, 165, 166, 167, 168, 169,
-                                     170, 171, 172, 173, 174, 175, 176, 177, 178, 179, 180, 181, 182, 183, 184, 185])
+@pytest.mark.parametrize("variant", [0] + variants.RS_FUSED + [4, 5])
 def test_reconstruct_crc_batch(codec, k, p, erased, n, bpc, variant):
-    """Fused reconstruction (verify + decode + CRC) vs the oracle: default (streamed-input kernel where it applies),
-    49 (the per-window kernel), 54 (streamed-input, 8 waves per SIMD), 61-67 (nibble-table kernel: rings, step
-    groups, occupancy, unfenced lookups, 4-wave workgroups), 150-158 (free output-register shifts, XO)."""
+    """Fused reconstruction (verify + decode + CRC) vs the oracle for the default and every fused alternate the library
+    holds (49 per-window, 56 / 59 streamed-input, 62-177 nibble-table; 4 / 5 the XOR codec's XO forms)."""
     lib = L.lib()
     assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
     try:

@@ -10,6 +10,7 @@ import pytest
 import oracle
 from golden_io import case_id, case_inputs, ec_cases, load, matches
 from synth import SEED, cells, splitmix64_bytes
+import variants
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -143,11 +144,11 @@ def test_decode_batch_vs_oracle(k, p, erased):
         assert all((got[s, i] == units[s, e]).all() for i, e in enumerate(erased)), s
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 11, 12, 13])
+@pytest.mark.parametrize("variant", variants.GF)
 @pytest.mark.parametrize("k,p,erased", [(6, 3, None), (3, 2, None), (10, 4, [0, 1, 2, 3]), (10, 4, [1, 4, 10, 13]),
                                         (6, 3, [0, 2, 7]), (10, 4, [0, 13])])
 def test_coding_kernel_variants_vs_oracle(variant, k, p, erased):
-    """Every coding-kernel tuning variant (gf_variant: chunk size, cache policy, XOR chains, selector masks in VGPRs)
+    """Every coding-kernel tuning variant (gf_variant: plain cache policy, two vectors per lane, XOR chains)
     is bit-exact against the oracle for encode (erased None) and decode shapes, with a ragged tail."""
     lib = L.lib()
     n, S = 3 * 4096 + 48, 5
@@ -212,7 +213,7 @@ def test_checksum_batch_vs_oracle(ctype, otype, bpc):
         assert (got[c] == oracle.crc_windows(otype, data[c], bpc)).all(), c
 
 
-@pytest.mark.parametrize("variant", [0, 1, 11, 13, 20, 21, 22, 23, 24, 25, 26, 27])
+@pytest.mark.parametrize("variant", [0] + variants.CRC_STREAM)
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
 def test_checksum_stream_runs_cross_cells(variant, ctype, otype):
     """crc_windows_g26s (the streaming kernel): per-wave runs of full windows that cross cell boundaries
@@ -407,13 +408,13 @@ def test_encode_crc_xor_free_shift_vs_oracle(variant, k, n, bpc, S, ctype, otype
             assert (crcs[s, u] == oracle.crc_windows(otype, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [61, 63, 100, 101, 150, 151, 152, 170, 171, 172, 173, 174, 175, 176, 177, 178, 179, 180, 181, 182, 183, 184, 185])
+@pytest.mark.parametrize("variant", [v for v in variants.RS_FUSED if v >= 62])
 @pytest.mark.parametrize("k,p,n,bpc,S", [(6, 3, 1 << 17, 16384, 3), (10, 4, 1 << 16, 4096, 2), (3, 2, 1 << 17, 8192, 3),
                                          (6, 2, 1 << 15, 32768, 2), (10, 1, 1 << 16, 16384, 2)])
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
 def test_encode_crc_nibble_kernel_vs_oracle(variant, k, p, n, bpc, S, ctype, otype):
-    """The nibble-table fused kernel (fused.hip encode_crc_nb; 61: one-step groups, 63: two-step groups where the
-    tables fit) for both CRC types and every RS shape it takes, bit-exact vs the oracle."""
+    """The nibble-table fused kernel (fused_nb.hpp encode_crc_nb, every alternate the library holds) for both CRC types
+    and every RS shape it takes, bit-exact vs the oracle."""
     lib = L.lib()
     data = np.stack([np.stack(cells(SEED, 54000 + s * k, k, n)) for s in range(S)])
     nwin = n // bpc
@@ -433,13 +434,13 @@ def test_encode_crc_nibble_kernel_vs_oracle(variant, k, p, n, bpc, S, ctype, oty
             assert (crcs[s, u] == oracle.crc_windows(otype, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [100, 101, 102, 106, 107, 108, 109])
+@pytest.mark.parametrize("variant", variants.NB_PERSISTENT)
 @pytest.mark.parametrize("grid", [1, 3, 0])
 def test_encode_crc_work_queue_any_grid_and_streams(variant, grid):
     """The persistent nibble kernel's work queue (fused.hip WorkQueue): every (stripe, window) unit is done exactly
-    once for a grid of 1 workgroup (it drains all 8 ranges), 3 (ranges shared unevenly) and the resident set; the
-    counter slot is back at zero after each launch (five launches in a row on one stream give the same result), and
-    two streams have their own slots (concurrent launches of different batches, both vs the oracle)."""
+    once for a grid of 1 workgroup (it drains all 8 ranges), 3 (ranges shared unevenly) and the resident set; a leased
+    counter slot is back at zero after each launch (five launches in a row give the same result), and launches on two
+    streams at once lease different slots (concurrent batches, both vs the oracle)."""
     lib = L.lib()
     k, p, n, bpc, S = 6, 3, 1 << 17, 16384, 5
     data = [np.stack([np.stack(cells(SEED, 57000 + b * 100 + s * k, k, n)) for s in range(S)]) for b in range(2)]
@@ -469,17 +470,52 @@ def test_encode_crc_work_queue_any_grid_and_streams(variant, grid):
         lib.ozec_set_tuning(b"crc_grid", 0)
 
 
-@pytest.mark.parametrize("variant", [11, 12, 13, 14, 15, 16, 17, 49, 51, 52, 53, 54, 55, 56, 57, 58,
-                                     61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 86, 87, 88, 89, 93, 94, 95,
-                                     100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, 111, 112, 113, 114, 120, 121, 122, 123, 130, 131, 132, 133, 134, 135,
-                                     150, 151, 152, 153, 154, 155, 156, 157, 158, 159, 160, 161, 162, 163, 164, 165, 166, 167, 168, 169,
-                                     170, 171, 172, 173, 174, 175, 176, 177, 178, 179, 180, 181, 182, 183, 184, 185])
+@pytest.mark.parametrize("stream", [2, 0])  # hipStreamPerThread, the null stream
+def test_encode_crc_concurrent_launches_on_one_stream_handle(stream):
+    """Four threads launch the persistent default kernels at once, all on one stream handle (hipStreamPerThread is a
+    different stream in every thread; the null stream is shared).  The WorkQueue counter slots are leased per launch,
+    never per handle, so no launch skips or repeats a unit of another's: every batch vs the oracle."""
+    import threading
+    k, p, n, bpc, S, T = 6, 3, 1 << 17, 16384, 6, 4
+    data = [np.stack([np.stack(cells(SEED, 58000 + b * 100 + s * k, k, n)) for s in range(S)]) for b in range(T)]
+    ins = [t(d) for d in data]
+    outs = [torch.full((S, p, n), 0xA5, dtype=torch.uint8, device=DEV) for _ in range(T)]
+    crcs = [torch.zeros((S, k + p, n // bpc), dtype=torch.int32, device=DEV) for _ in range(T)]
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    torch.cuda.synchronize()
+    errors = []
+
+    def run(b):
+        try:
+            for _ in range(5):
+                e.encode_crc_batch(ins[b], k * n, n, outs[b], p * n, n, S, n, ck.ChecksumType.CRC32C, bpc, crcs[b],
+                                   stream=stream)
+            L.lib().ozec_synchronize()
+        except Exception as ex:  # noqa: BLE001 -- reported below
+            errors.append(ex)
+
+    threads = [threading.Thread(target=run, args=(b,)) for b in range(T)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for b in range(T):
+        par, cr = h(outs[b]), h(crcs[b]).view(np.uint32)
+        for s in range(S):
+            ref = oracle.rs_encode(k, p, list(data[b][s]))
+            assert all((par[s, r] == ref[r]).all() for r in range(p)), (b, s)
+            for u, cell in enumerate(list(data[b][s]) + ref):
+                assert (cr[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (b, s, u)
+
+
+@pytest.mark.parametrize("variant", variants.RS_FUSED)
 @pytest.mark.parametrize("n,bpc,S", [(1 << 18, 16384, 3), (50000, 4096, 2), (1 << 17, 4096, 2), (1 << 17, 65536, 3)])
 def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
-    """Every tuning variant of the rs-6-3 fused encode + CRC32C kernel (per-window kernel: D = 4, prefetch, table
-    placements, CRC lookups in two fenced halves at 4 and 5 waves per SIMD; 49 pins it; streamed-input kernel
-    (fused.hip) at 4-8 waves per SIMD, rings of 2 and 4 blocks, D = 2 and 4: 51-58) is bit-exact against the
-    oracle.  Geometries the streamed kernel does not take (a short last window) go to the per-window kernel."""
+    """Every fused RS variant of the rs-6-3 encode + CRC32C kernels (49 the per-window kernel, 56 / 59 the streamed-input
+    kernel, 62-177 the nibble-table kernel) is bit-exact against the oracle.  Geometries the streamed and nibble
+    kernels do not take (a short last window) go to the per-window kernel."""
     lib = L.lib()
     k, p = 6, 3
     data = np.stack([np.stack(cells(SEED, 52000 + s * k, k, n)) for s in range(S)])
@@ -501,13 +537,10 @@ def test_encode_crc_rs63_variants_vs_oracle(variant, n, bpc, S):
             assert (crcs[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [0, 11, 17, 49, 51, 54, 55, 57, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 79, 80, 81, 82, 83, 84, 85, 86, 87, 88, 89, 93, 94, 95,
-                                     100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, 111, 112, 113, 114, 120, 121, 122, 123, 130, 131, 132, 133, 134, 135,
-                                     150, 151, 152, 153, 154, 155, 156, 157, 158, 159, 160, 161, 162, 163, 164, 165, 166, 167, 168, 169,
-                                     170, 171, 172, 173, 174, 175, 176, 177, 178, 179, 180, 181, 182, 183, 184, 185])
+@pytest.mark.parametrize("variant", [0] + variants.RS_FUSED)
 @pytest.mark.parametrize("k,p", [(10, 4), (6, 2), (3, 2), (10, 3), (10, 2), (10, 1)])
 def test_encode_crc_other_shapes_variants_vs_oracle(variant, k, p):
-    """Fused encode + CRC32C variants of the other RS shapes (D = 2 default, D = 4, D = 4 with fenced halves)."""
+    """Fused encode + CRC32C variants of the other RS shapes (every fused RS alternate the library holds)."""
     lib = L.lib()
     n, bpc, S = 1 << 17, 16384, 2
     data = np.stack([np.stack(cells(SEED, 53000 + s * k, k, n)) for s in range(S)])
@@ -528,7 +561,7 @@ def test_encode_crc_other_shapes_variants_vs_oracle(variant, k, p):
             assert (crcs[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (s, u)
 
 
-@pytest.mark.parametrize("variant", [0, 4, 5, 13, 20, 21])
+@pytest.mark.parametrize("variant", [0] + variants.XOR_FUSED)
 @pytest.mark.parametrize("k,n,bpc,S", [(2, 1 << 18, 16384, 5), (3, 65536, 4096, 7), (6, 1 << 17, 8192, 3)])
 def test_encode_xor_crc_stream_runs_cross_stripes(variant, k, n, bpc, S):
     """encode_xor_crc_g26s (XOR codec, all windows full): per-wave runs of (stripe, window) units that cross
@@ -601,7 +634,7 @@ def test_full_size_rs_10_4_decode_4_erased():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("variant", [0, 13])
+@pytest.mark.parametrize("variant", [0, 20])
 def test_full_size_xor_2_1_crc_4096_stripes(variant):
     """BASELINE config C4 shape (4096 stripes of xor-2-1-1024k + CRC32C/16 KiB): parity equals torch's XOR of the
     inputs and every window CRC equals the CRC-only kernel's, for the streaming (0) and per-window (13) fused
@@ -839,6 +872,43 @@ def test_host_path_pinned_buffers_dma_in_place(codec, k, p, n):
     got = [int.from_bytes(b, "big") for b in cd.get_checksums()]
     assert got == [int(x) for x in oracle.crc_windows(oracle.CRC32C, data[1], bpc)]
     pool.free()
+
+
+@pytest.mark.parametrize("n", [1 << 16, 1 << 18])
+def test_host_path_separately_pinned_cells_at_one_stride(n):
+    """cells at one constant stride that are pinned as SEPARATE allocations (one ozec_host_register per cell
+    of one pageable buffer) are not one DMA source -- the rectangular copy is only taken when the whole span lies in
+    one allocation (capi.cpp range_pinned); these go per unit (256 KiB cells) or through staging (64 KiB), and the
+    results equal the oracle.  Encode and decode, both cell sizes."""
+    from ozone_amd.stripe_queue import host_register, host_unregister
+    k, p = 6, 3
+    page = 4096
+    buf = np.zeros((2 * (k + p) + 1) * n + page, np.uint8)
+    base = (-buf.ctypes.data) % page
+    cells_ = [buf[base + i * n: base + (i + 1) * n] for i in range(k + p)]  # adjacent, page-aligned, one stride
+    regs = []
+    try:
+        for c in cells_:
+            host_register(c.ctypes.data, n, -1)
+            regs.append(c.ctypes.data)
+        data = cells(SEED, 97000, k, n)
+        for c, d in zip(cells_, data):
+            c[:] = d
+        ref = oracle.rs_encode(k, p, data)
+        for c in cells_[k:]:
+            c[:] = 0xA5
+        enc("rs", k, p).encode(cells_[:k], cells_[k:])
+        assert all((a == b).all() for a, b in zip(cells_[k:], ref))
+        outs = [cells_[0], cells_[7]]
+        truth = [data[0].copy(), ref[1].copy()]
+        for o in outs:
+            o[:] = 0
+        dins = [None] + cells_[1:7] + [None] + cells_[8:]
+        dec("rs", k, p).decode(dins, [0, 7], outs)
+        assert all((o == t_).all() for o, t_ in zip(outs, truth))
+    finally:
+        for a in regs:
+            host_unregister(a)
 
 
 def test_encode_crc_batch_xor_p2_zero_fills_extra_parity():

@@ -117,12 +117,19 @@ def test_factories_implement_raw_erasure_coder_factory():
             assert "public" in mine[k]["mods"]
 
 
+SVC_DIR = os.path.join(ROOT, "java", "src", "main", "resources", "META-INF", "services")
+ACCEL_SVC = "org.apache.hadoop.ozone.common.ChecksumAccelerator"
+
+
+def _listed(name):
+    return [ln.strip() for ln in open(os.path.join(SVC_DIR, name)) if ln.strip() and not ln.startswith("#")]
+
+
 def test_services_file_is_the_reference_plugin_seam():
-    svc_dir = os.path.join(ROOT, "java", "src", "main", "resources", "META-INF", "services")
-    assert sorted(os.listdir(svc_dir)) == json.load(open(os.path.join(ROOT, "tests", "java_api",
-                                                                      "reference_api.json")))["services"]
-    listed = [ln.strip() for ln in open(os.path.join(svc_dir, os.listdir(svc_dir)[0])) if ln.strip()
-              and not ln.startswith("#")]
+    ref_services = json.load(open(os.path.join(ROOT, "tests", "java_api", "reference_api.json")))["services"]
+    # the reference's coder seam, plus the checksum seam the hook patch adds to hdds-common
+    assert sorted(os.listdir(SVC_DIR)) == sorted(ref_services + [ACCEL_SVC])
+    listed = _listed(ref_services[0])
     for fq in listed:
         pkg, _, cls = fq.rpartition(".")
         assert cls in OURS and OURS[cls]["package"] == pkg, fq
@@ -161,28 +168,119 @@ def _patch():
     return open(os.path.join(ROOT, "java", "patches", "hdds-common-checksum-hook.patch")).read()
 
 
+CM = "hadoop-hdds/common/src/main/java/org/apache/hadoop/ozone/common/"
+
+
+def _patch_files():
+    """{path: (added source lines, new file?)} of the hook patch"""
+    out, cur = {}, None
+    lines = _patch().splitlines()
+    for i, ln in enumerate(lines):
+        if ln.startswith("+++ b/"):
+            cur = ln[6:]
+            out[cur] = ([], i + 1 < len(lines) and lines[i + 1].startswith("@@ -0,0 "))
+        elif cur and ln.startswith("+"):
+            out[cur][0].append(ln[1:])
+    return out
+
+
+def _added_code(lines):
+    """added lines without comments and string literals"""
+    return javasig.strip("\n".join(lines))
+
+
 def test_checksum_hook_patch_targets_exist():
-    p = _patch()
-    files = re.findall(r"^\+\+\+ b/(\S+)", p, re.M)
-    assert files == ["hadoop-hdds/common/src/main/java/org/apache/hadoop/ozone/common/Checksum.java",
-                     "hadoop-hdds/common/src/main/java/org/apache/hadoop/ozone/common/ChecksumByteBufferFactory.java"]
+    files = _patch_files()
+    assert sorted(files) == sorted(CM + f for f in ("Checksum.java", "ChecksumAccelerator.java",
+                                                    "ChecksumAccelerators.java", "ChecksumByteBufferFactory.java"))
+    assert files[CM + "ChecksumAccelerator.java"][1] and files[CM + "ChecksumAccelerators.java"][1]  # new files
     assert "computeChecksum(ChunkBuffer)" in _sigs(REF["Checksum"])
     fac = _sigs(REF["ChecksumByteBufferFactory"])
     assert fac["crc32Impl()"]["ret"] == fac["crc32CImpl()"]["ret"] == "ChecksumByteBuffer"
-    added = "\n".join(ln[1:] for ln in p.splitlines() if ln.startswith("+") and not ln.startswith("+++"))
-    assert "HipChecksum.useGpu(checksumType, data)" in added
-    assert "HipChecksum.computeChecksum(checksumType, data, bytesPerChecksum)" in added
-    assert "HipChecksumByteBuffer.enabled()" in added and "new HipChecksumByteBuffer(OzecNative.CHECKSUM_CRC32C, host)" in added
+    chk = _added_code(files[CM + "Checksum.java"][0])
+    assert "ChecksumAccelerators.computeChecksum(checksumType, data, bytesPerChecksum)" in chk
+    assert "if (accelerated != null)" in chk and "return accelerated;" in chk
+    f = _added_code(files[CM + "ChecksumByteBufferFactory.java"][0])
+    assert "ChecksumAccelerators.wrap(false, new ChecksumByteBufferImpl(new CRC32()))" in f
+    assert "ChecksumAccelerators.wrap(true, crc32CHostImpl())" in f
     # the patched computeChecksum(ChunkBuffer) keeps the reference's variable names
     assert set(REF["Checksum"]["fields"]) >= {"checksumType", "bytesPerChecksum"}
 
 
+# what the hook patch may name: the JDK, hdds-common's own package (the reference's classes and the two the patch adds)
+# and the imports the patched files already have (the proto ChecksumType, slf4j)
+_ALLOWED_IMPORTS = re.compile(r"^(java\.|org\.apache\.hadoop\.ozone\.common\.[A-Z]|org\.slf4j\."
+                              r"|org\.apache\.hadoop\.hdds\.protocol\.datanode\.proto\.ContainerProtos\.ChecksumType$)")
+
+
+def test_checksum_hook_patch_names_nothing_outside_hdds_common():
+    """hdds-common must not depend on the HIP jar (the reactor would have a module cycle, and every Ozone
+    process without the jar would fail on its first CRC).  Every import the patch adds is the JDK, hdds-common's package
+    or an import the patched file already had; no added line names a class of this repo's jar or its packages."""
+    ref_src = {}
+    for path, (added, new) in _patch_files().items():
+        code = _added_code(added)
+        for imp in re.findall(r"^\s*import\s+(?:static\s+)?([\w.]+)\s*;", code, re.M):
+            assert _ALLOWED_IMPORTS.match(imp), (path, imp)
+        for ours in list(OURS) + ["OzecNative", "ozec", "erasurecode", "Hip"]:
+            assert not re.search(r"\b" + ours, code), (path, ours)
+        body = re.sub(r"^\s*(import|package)\s+[\w.]+\s*;", "", code, flags=re.M)
+        names = set(re.findall(r"\b([A-Z]\w*)\b", body))
+        # every class named is in hdds-common's package, imported, the JDK's java.lang, or declared by the patch
+        declared = {"ChecksumAccelerator", "ChecksumAccelerators"}
+        imported = {i.rpartition(".")[2] for i in re.findall(r"import\s+([\w.]+);", code)}
+        if not new and os.path.isdir(REF_CHECKOUT):
+            ref_src[path] = open(os.path.join(REF_CHECKOUT, path)).read()
+            imported |= {i.rpartition(".")[2] for i in re.findall(r"import\s+([\w.]+);", ref_src[path])}
+        java_lang = {"Exception", "RuntimeException", "LinkageError", "Throwable", "Override", "Class", "String"}
+        hdds_common = set(REF) | {"ChunkBuffer", "ChecksumData", "ChecksumByteBuffer", "ChecksumByteBufferImpl",
+                                  "OzoneChecksumException", "Checksum"}
+        unknown = {n for n in names if not n.isupper()} - declared - imported - java_lang - hdds_common - {"CRC32"}
+        assert not unknown, (path, unknown)
+
+
+def test_checksum_seam_without_a_provider_is_the_reference():
+    """No JVM here, so the no-provider behaviour is checked on the patched source: the accelerator is looked up once
+    with ServiceLoader and every failure to load is caught; with no provider (INSTANCE null) wrap() returns the
+    runtime's CRC unchanged and computeChecksum() returns null, which the patched Checksum answers with the
+    reference's own window loop."""
+    acc = "\n".join(_patch_files()[CM + "ChecksumAccelerators.java"][0])
+    code = javasig.strip(acc)
+    assert "ServiceLoader.load(" in code and "ChecksumAccelerator.class" in code
+    assert "catch (ServiceConfigurationError | LinkageError | RuntimeException e)" in code
+    assert "return INSTANCE == null ? host : INSTANCE.wrap(crc32c, host);" in code
+    assert re.search(r"return INSTANCE == null \? null\s*: INSTANCE\.computeChecksum\(type, data, bytesPerChecksum\);", code)
+    assert "private static final ChecksumAccelerator INSTANCE = load();" in code
+    iface = javasig.classes("\n".join(_patch_files()[CM + "ChecksumAccelerator.java"][0]))["ChecksumAccelerator"]
+    assert {javasig.sig_key(m) for m in iface["methods"]} == {
+        "isAvailable()", "wrap(boolean,ChecksumByteBuffer)", "computeChecksum(ChecksumType,ChunkBuffer,int)"}
+
+
+def test_hip_checksum_accelerator_is_the_registered_provider():
+    assert _listed(ACCEL_SVC) == ["org.apache.hadoop.ozone.common.HipChecksumAccelerator"]
+    info = OURS["HipChecksumAccelerator"]
+    assert info["package"] == "org.apache.hadoop.ozone.common" and "ChecksumAccelerator" in info["implements"]
+    iface = javasig.classes("\n".join(_patch_files()[CM + "ChecksumAccelerator.java"][0]))["ChecksumAccelerator"]
+    mine = _sigs(info, public_only=True)
+    for m in iface["methods"]:
+        k = javasig.sig_key(m)
+        assert k in mine and mine[k]["ret"] == m["ret"], k
+    assert ["public"] == [x for x in ([m["mods"] for m in info["methods"] if m["ctor"] and not m["params"]] or [[]])[0]
+                          if x == "public"]  # ServiceLoader needs a public no-argument constructor
+    # the batch path leaves the ChunkBuffer consumed, as data.iterate(bytesPerChecksum) does (ADVICE r3)
+    hc = javasig.strip(OURS["HipChecksum"]["src"])
+    assert "b.position(b.limit());" in hc and "data instanceof ChunkBufferImplWithByteBuffer" in hc
+
+
 @pytest.mark.skipif(not os.path.isdir(REF_CHECKOUT), reason="reference checkout absent")
 def test_checksum_hook_patch_applies_to_the_reference(tmp_path):
-    for rel in re.findall(r"^\+\+\+ b/(\S+)", _patch(), re.M):
+    for rel, (_, new) in _patch_files().items():
         dst = tmp_path / rel
         dst.parent.mkdir(parents=True, exist_ok=True)
-        dst.write_text(open(os.path.join(REF_CHECKOUT, rel)).read())
+        if new:  # the two files the patch adds to hdds-common
+            assert not os.path.exists(os.path.join(REF_CHECKOUT, rel)), rel
+        else:
+            dst.write_text(open(os.path.join(REF_CHECKOUT, rel)).read())
     r = subprocess.run(["patch", "-p1", "--dry-run", "-i", os.path.join(ROOT, "java", "patches",
                                                                        "hdds-common-checksum-hook.patch")],
                        cwd=tmp_path, capture_output=True, text=True)

@@ -240,6 +240,28 @@ def test_crc_composer_natives_vs_oracle(J, java, ctype, hint, stripe):
         call(J, "composerFree", c)
 
 
+def test_crc_composer_update_bytes_composes_up_to_a_failing_read(J, java):
+    """CrcComposer.update(byte[], ...) reads one CRC at a time (CrcUtil.readInt), so the CRCs before a read past the
+    array are composed when the IOException comes, as in the reference: the digest after the failure equals a fresh
+    composer that saw only those CRCs."""
+    crcs = np.array([0x11223344, 0x55667788, 0x99AABBCC], dtype=">u4").view(np.uint8)  # 12 bytes, big-endian
+    c = call(J, "composerCreate", 3, 4, 0)
+    ref = call(J, "composerCreate", 3, 4, 0)
+    try:
+        call(J, "composerUpdateBytes", c, java.bytes(crcs), 4, 12, 4)  # reads offsets 4, 8, then 12 fails
+        assert java.exception() == ("java/io/IOException", "readInt out of bounds: buf.length=12, offset=12")
+        call(J, "composerUpdateBytes", ref, java.bytes(crcs), 4, 8, 4)
+        assert java.exception() is None
+        a = np.zeros(8, np.uint8)
+        b = np.zeros(8, np.uint8)
+        na = call(J, "composerDigest", c, java.bytes(a))
+        nb = call(J, "composerDigest", ref, java.bytes(b))
+        assert na == nb == 4 and (a == b).all()
+    finally:
+        call(J, "composerFree", c)
+        call(J, "composerFree", ref)
+
+
 def test_crc_composer_natives_raise_the_reference_exceptions(J, java):
     c = call(J, "composerCreate", 3, 4, 10)
     try:
@@ -254,7 +276,9 @@ def test_crc_composer_natives_raise_the_reference_exceptions(J, java):
         assert ex == ("java/io/IOException", "Trying to update CRC from byte array with length '6' at offset '0' "
                                              "which is not a multiple of 4!")
         call(J, "composerUpdateBytes", c, java.bytes(np.zeros(8, np.uint8)), 6, 4, 4)
-        assert java.exception()[0] == "java/lang/ArrayIndexOutOfBoundsException"
+        assert java.exception() == ("java/io/IOException", "readInt out of bounds: buf.length=8, offset=6")
+        call(J, "composerUpdateBytes", c, java.bytes(np.zeros(8, np.uint8)), -4, 8, 4)
+        assert java.exception() == ("java/lang/ArrayIndexOutOfBoundsException", "Index -4 out of bounds for length 8")
         call(J, "composerUpdate", c, 1, -4)
         assert java.exception()[0] == "java/lang/IllegalArgumentException"
         call(J, "composerDigest", c, java.bytes(np.zeros(0, np.uint8)))  # pending bytes do not fit

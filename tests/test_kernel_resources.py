@@ -1,5 +1,5 @@
 """The default kernels of the shipped libozec.so use no scratch memory and spill no VGPRs (CPU test: reads the gfx950
-code objects' metadata notes, scripts/kernel_resources.py).  Probe variants may spill; the defaults the launchers pick
+code objects' metadata notes, scripts/kernel_resources.py).  Alternates may spill; the defaults the launchers pick
 (fused.hip launch_encode_crc_lv, kernels.hip gf_code_vec launch) must not, and must fit the CU's 160 KiB of LDS."""
 import os
 import sys
@@ -20,9 +20,9 @@ def _b(v):
 
 
 def _nb(K, R, D, NB, WPB, DYN, H):
-    """Mangled template-argument run of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, D, 0, 0, XO, false, EM, H, false>."""
-    return "encode_crc_nbI" + "".join([_i(K), _i(R), _i(D), _i(NB), _i(WPB), _i(4), _i(2), _b(1), _i(DYN), _i(D),
-                                       _i(0), _i(0), _b(1), _b(0), _b(1), _i(H), _b(0)])
+    """Mangled template-argument run of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H> (XO, EM on)."""
+    return "encode_crc_nbI" + "".join([_i(K), _i(R), _i(D), _i(NB), _i(WPB), _i(4), _i(2), _b(1), _i(DYN), _b(1),
+                                       _b(1), _i(H)])
 
 
 def _defaults():

@@ -47,7 +47,10 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED = 0x00EC5EED
 METRIC = "EC encode GB/s (data bytes) rs-6-3-1024k @1/8 GPUs + % HBM roofline"
 WORKLOADS = ["c1", "c2", "c3", "c3r", "c3r_host", "c4", "c4s", "c5", "c5dev", "crc", "verify", "host", "queue", "queue_pageable",
-             "stream"]
+             "stream", "fused"]
+# the fused legs of the default line (the kernels C5 and the reconstruction coordinator run, under the
+# driver's clock): (workload, erased units) -- C5dev rs-6-3 encode + CRC32C, C3r with both erasure sets of BASELINE.md
+FUSED_LEGS = [("c5dev", (0, 1, 2, 3)), ("c3r", (0, 1, 2, 3)), ("c3r", (1, 4, 10, 13))]
 
 
 def parse(argv=None):
@@ -65,6 +68,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the C5 end-to-end leg of the default line")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-fused", action="store_true", help="skip the fused-kernel legs (C5dev, C3r) of the default line")
     ap.add_argument("--e2e-stripes", type=int, default=8192, help="C5 batch size (all GPUs together)")
     ap.add_argument("--e2e-steps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0, help="C5: stripes per pipelined chunk (0 = library default)")
@@ -427,6 +431,7 @@ class Workload:
             self._step = lambda: self.dec.reconstruct_crc_batch(
                 self.units, stride, n, present, self.erased, self.out, 4 * n, n, S, n, self.crc_type, self.bpc,
                 self.out_crc, d_expected=self.stored, d_mismatch=self.mism)
+            self._check = lambda: bool((self.mism == -1).all().item())  # every stripe's read units verified
         else:  # c4s (xor-2-1 stripe-major) / c5dev (rs-6-3): fused encode + CRC, device-resident
             self.crcs = torch.empty((S, units, self.nwin), dtype=torch.int32, device=dev)
             self.data_bytes = S * k * n
@@ -728,72 +733,172 @@ def _kernel_match(pat, name):
     return any(p in name for p in (pat if isinstance(pat, tuple) else (pat,)))
 
 
+def log(msg):
+    """progress on stderr (stdout carries only the one JSON line)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _rocprof_passes(child, tag_opts, timeout=300):
+    """Run the bench child command under rocprofv3 once per (tag, options) pass -- counters that do not fit one pass
+    get passes of their own -- and return {tag: [csv files]} (the caller removes the parent directory)."""
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        raise OSError("rocprofv3 not found")
+    work = tempfile.mkdtemp(prefix="ozec_pmc_")
+    env = dict(os.environ, TMPDIR="/tmp")
+    env.pop("WORLD_SIZE", None)
+    files = {"_dir": work}
+    for tag, opts in tag_opts:
+        d = os.path.join(work, tag)
+        cmd = [prof] + opts + ["--kernel-trace", "--stats", "-d", d, "-o", "run", "--output-format", "csv", "--"] + child
+        log(f"rocprofv3 pass {tag}: {' '.join(child[2:6])}")
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd="/tmp", env=env)
+        if r.returncode != 0:
+            raise OSError(f"rocprofv3 {tag} pass rc={r.returncode}: {r.stderr.strip()[-300:]}")
+        files[tag] = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs]
+    return files
+
+
+_PMC_PASSES = (("FETCH_SIZE", ["--pmc", "FETCH_SIZE"]), ("WRITE_SIZE", ["--pmc", "WRITE_SIZE"]), ("stats", []))
+
+
+def _leg_stats(files, pat, group, ngroups, steps, alg_bytes):
+    """One workload's numbers from the three passes: the kernel's dispatches matching `pat` come in `ngroups`
+    consecutive groups of equal size (one per leg of the child that launches that kernel), this leg is group `group`,
+    and its timed dispatches are the group's last `steps`."""
+    import csv
+    out = {}
+
+    def mine(rows, name_key, order_key):
+        rows = [r for r in rows if _kernel_match(pat, r[name_key])]
+        rows.sort(key=lambda r: int(r[order_key]))
+        per = len(rows) // ngroups
+        return rows[group * per:(group + 1) * per]
+    st = [f for f in files["stats"] if f.endswith("kernel_stats.csv")]
+    tr = [f for f in files["stats"] if f.endswith("kernel_trace.csv")]
+    disp = mine(list(csv.DictReader(open(tr[0]))), "Kernel_Name", "Start_Timestamp")
+    timed = disp[-steps:]
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
+    out["rocprof_kernel"] = timed[-1]["Kernel_Name"]
+    out["rocprof_avg_ms"] = round(float(np.mean(dur)), 4)
+    out["rocprof_min_ms"] = round(float(np.min(dur)), 4)
+    out["rocprof_timed_dispatches"] = len(dur)
+    out["kernel_vgpr"] = int(timed[-1].get("VGPR_Count") or 0)
+    out["kernel_lds_bytes"] = int(timed[-1].get("LDS_Block_Size") or 0)
+    out["kernel_scratch_bytes"] = int(timed[-1].get("Scratch_Size") or 0)
+    rows = [row for row in csv.DictReader(open(st[0])) if _kernel_match(pat, row["Name"])]
+    if rows:
+        out["rocprof_stats_avg_all_calls_ms"] = round(float(rows[0]["AverageNs"]) / 1e6, 4)
+    for tag in ("FETCH_SIZE", "WRITE_SIZE"):
+        cc = [f for f in files[tag] if f.endswith("counter_collection.csv")]
+        vals = [float(r["Counter_Value"]) for r in mine([r for r in csv.DictReader(open(cc[0]))
+                                                         if r["Counter_Name"] == tag], "Kernel_Name", "Dispatch_Id")]
+        if not vals:
+            raise KeyError(f"no {tag} rows for kernel {pat}")
+        out[tag + "_KiB"] = sum(vals) / len(vals)
+        out[tag + "_dispatches"] = len(vals)
+    hbm = int(round((2 * out["FETCH_SIZE_KiB"] + out["WRITE_SIZE_KiB"]) * 1024))
+    out["hbm_bytes_per_launch"] = hbm
+    out["traffic_over_algorithmic"] = round(hbm / alg_bytes, 5)
+    out["correction"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB (gfx950 FETCH_SIZE counts half of wide reads)"
+    out["frac_rocprof_avg"] = round(alg_bytes / (out["rocprof_avg_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+    return hbm, out
+
+
+def _child_base(args, workload):
+    base = [sys.executable, os.path.abspath(__file__), "--workload", workload, "--steps", str(args.steps),
+            "--warmup", str(args.warmup), "--no-cpu", "--no-e2e", "--no-pmc", "--erased", args.erased] + \
+        (["--stripes", str(args.stripes)] if args.stripes else [])
+    for kv in args.tune:
+        base += ["--tune", kv]
+    return base
+
+
 def pmc_traffic(args, alg_bytes):
     """HBM bytes per launch of the workload's dominant kernel, measured now: the same bench command as a CHILD
     process under rocprofv3, one --pmc pass per counter (FETCH_SIZE, WRITE_SIZE: they do not fit one pass), plus
     a --kernel-trace --stats pass for the rocprof average duration.  gfx950: FETCH_SIZE reports half of wide
     streaming reads (MI355X_MICROARCH.md, HBM) -> bytes = (2 * FETCH_SIZE + WRITE_SIZE) KiB * 1024."""
-    import csv
     pat = KERNEL_PAT.get(args.workload)
-    prof = shutil.which("rocprofv3")
-    if not pat or not prof:
-        return None, {"error": "no kernel pattern / rocprofv3 for this workload"}
+    if not pat:
+        return None, {"error": "no kernel pattern for this workload"}
     # the child runs exactly the main run's warm-up and timed steps, so the rocprof durations of the timed dispatches
     # are taken at the same clock state as the HIP events (VERDICT r2: a 3-step child ran 11-20 % slow)
-    base = [sys.executable, os.path.abspath(__file__), "--workload", args.workload, "--steps", str(args.steps),
-            "--warmup", str(args.warmup), "--no-cpu", "--no-e2e", "--no-pmc"] + \
-        (["--stripes", str(args.stripes)] if args.stripes else [])
-    for kv in args.tune:
-        base += ["--tune", kv]
-    out = {}
-    work = tempfile.mkdtemp(prefix="ozec_pmc_")
-    env = dict(os.environ, TMPDIR="/tmp")
-    env.pop("WORLD_SIZE", None)
+    files = {}
     try:
-        for tag, opts in (("FETCH_SIZE", ["--pmc", "FETCH_SIZE"]), ("WRITE_SIZE", ["--pmc", "WRITE_SIZE"]),
-                          ("stats", [])):
-            d = os.path.join(work, tag)
-            cmd = [prof] + opts + ["--kernel-trace", "--stats", "-d", d, "-o", "run", "--output-format", "csv",
-                                   "--"] + base
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd="/tmp", env=env)
-            if r.returncode != 0:
-                return None, {"error": f"rocprofv3 {tag} pass rc={r.returncode}: {r.stderr.strip()[-300:]}"}
-            files = [os.path.join(dp, f) for dp, _, fs in os.walk(d) for f in fs]
-            if tag == "stats":
-                st = [f for f in files if f.endswith("kernel_stats.csv")]
-                rows = [row for row in csv.DictReader(open(st[0])) if _kernel_match(pat, row["Name"])]
-                out["rocprof_kernel"] = rows[0]["Name"]
-                out["rocprof_calls"] = int(rows[0]["Calls"])
-                out["rocprof_avg_all_calls_ms"] = round(float(rows[0]["AverageNs"]) / 1e6, 4)
-                out["rocprof_min_ms"] = round(float(rows[0]["MinNs"]) / 1e6, 4)
-                # the timed dispatches: the last `steps` of the kernel in the trace (the warm-up's come first)
-                tr = [f for f in files if f.endswith("kernel_trace.csv")]
-                disp = [row for row in csv.DictReader(open(tr[0])) if _kernel_match(pat, row["Kernel_Name"])]
-                disp.sort(key=lambda row: int(row["Start_Timestamp"]))
-                timed = disp[-args.steps:]
-                dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
-                out["rocprof_avg_ms"] = round(float(np.mean(dur)), 4)
-                out["rocprof_timed_dispatches"] = len(dur)
-                out["kernel_vgpr"] = int(timed[-1].get("VGPR_Count") or 0)
-                out["kernel_lds_bytes"] = int(timed[-1].get("LDS_Block_Size") or 0)
-                out["kernel_scratch_bytes"] = int(timed[-1].get("Scratch_Size") or 0)
-            else:
-                cc = [f for f in files if f.endswith("counter_collection.csv")]
-                vals = [float(row["Counter_Value"]) for row in csv.DictReader(open(cc[0]))
-                        if _kernel_match(pat, row["Kernel_Name"]) and row["Counter_Name"] == tag]
-                if not vals:
-                    return None, {"error": f"no {tag} rows for kernel {pat}"}
-                out[tag + "_KiB"] = sum(vals) / len(vals)
-                out[tag + "_dispatches"] = len(vals)
+        files = _rocprof_passes(_child_base(args, args.workload), _PMC_PASSES)
+        return _leg_stats(files, pat, 0, 1, args.steps, alg_bytes)
     except (OSError, subprocess.SubprocessError, IndexError, KeyError, ValueError) as e:
         return None, {"error": f"{type(e).__name__}: {e}"}
     finally:
-        shutil.rmtree(work, ignore_errors=True)
-    hbm = int(round((2 * out["FETCH_SIZE_KiB"] + out["WRITE_SIZE_KiB"]) * 1024))
-    out["hbm_bytes_per_launch"] = hbm
-    out["traffic_over_algorithmic"] = round(hbm / alg_bytes, 5)
-    out["correction"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1 KiB (gfx950 FETCH_SIZE counts half of wide reads)"
-    return hbm, out
+        if files.get("_dir"):
+            shutil.rmtree(files["_dir"], ignore_errors=True)
+
+
+def time_workload(wl, steps, warmup, dist):
+    """W untimed steps, then K steps bracketed by a barrier + synchronize, each step between HIP events on the launch
+    stream: (wall seconds, mean event ms per step)"""
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+    for _ in range(warmup):
+        wl.step()
+    barrier()
+    st = torch.cuda.current_stream()  # every device-resident workload launches on it (rawcoder._stream_ptr)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(st)
+        wl.step()
+        b.record(st)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    return elapsed, float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def fused_legs(args, rank, world, dist, red_dev):
+    """The fused kernels of C5 (rs-6-3 encode + CRC32C) and of reconstruction (rs-10-4 verify + decode + CRC32C,
+    both erasure sets), device-resident, timed like the headline and reduced max over ranks: the kernel's roofline
+    fraction from HIP events, and at N = 1 the rocprofv3 average and PMC traffic of the same timed dispatches from
+    one child run of all legs (3 passes)."""
+    from ozone_amd.shard import max_over_ranks
+    legs = []
+    for name, erased in FUSED_LEGS:
+        log(f"fused leg {name} {erased}")
+        wl = Workload(name, rank, world, args.stripes, erased=list(erased))
+        elapsed, kern_ms = time_workload(wl, args.steps, args.warmup, dist)
+        elapsed = max_over_ranks(elapsed, dist, device=red_dev)
+        kern_ms = max_over_ranks(kern_ms, dist, device=red_dev)
+        leg = {"workload": wl.config["workload"], "kernel": wl.kernel, "stripes_per_gpu": wl.S,
+               "value": round(wl.data_bytes * world * args.steps / elapsed / 1e9, 2), "unit": "GB/s (data bytes)",
+               "ms_per_step": round(elapsed / args.steps * 1e3, 4), "kernel_ms": round(kern_ms, 4),
+               "alg_bytes_per_launch": wl.alg_bytes,
+               "frac": round(wl.alg_bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+        if hasattr(wl, "_check"):
+            leg["verified"] = wl._check()
+        legs.append(leg)
+        wl.free()
+        del wl
+    if rank == 0 and world == 1 and not args.no_pmc:
+        files = {}
+        try:
+            files = _rocprof_passes(_child_base(args, "fused"), _PMC_PASSES, timeout=400)
+            for i, (name, _) in enumerate(FUSED_LEGS):
+                same = [j for j, (nm, _) in enumerate(FUSED_LEGS) if nm == name]
+                traffic, detail = _leg_stats(files, KERNEL_PAT[name], same.index(i), len(same), args.steps,
+                                             legs[i]["alg_bytes_per_launch"])
+                legs[i]["traffic"] = traffic
+                legs[i]["pmc"] = detail
+                legs[i]["rocprof_avg_ms"] = detail["rocprof_avg_ms"]
+                legs[i]["frac_rocprof_avg"] = detail["frac_rocprof_avg"]
+        except (OSError, subprocess.SubprocessError, IndexError, KeyError, ValueError) as e:
+            legs.append({"pmc_error": f"{type(e).__name__}: {e}"})
+        finally:
+            if files.get("_dir"):
+                shutil.rmtree(files["_dir"], ignore_errors=True)
+    return legs
 
 
 # ------------------------------------------------------------------------------------------ per-call latency
@@ -951,6 +1056,10 @@ def main():
     # OZEC_BENCH_SAME_DEVICE=1 + OZEC_DIST_BACKEND=gloo rehearse the N-rank path on a one-GPU box
     dev_idx = 0 if os.environ.get("OZEC_BENCH_SAME_DEVICE") == "1" else local
     torch.cuda.set_device(dev_idx)
+    # one process per GPU here: this rank's coders, host batches and staging use its own GPU only (libozec's default
+    # would spread one process's coders over every visible GPU, ozec_set_devices)
+    from ozone_amd import rawcoder as _rc
+    _rc.set_devices([dev_idx])
     numa_node = bind_process_to_gpu_node(dev_idx)
     backend = os.environ.get("OZEC_DIST_BACKEND", "nccl")
     dist = None
@@ -998,6 +1107,14 @@ def main():
             dist.destroy_process_group()
         return 0
 
+    if args.workload == "fused":  # the fused legs alone (the rocprofv3 child of the default line)
+        legs = fused_legs(args, rank, world, dist, red_dev)
+        if rank == 0:
+            emit({"metric": "fused legs", "value": None, "legs": legs})
+        if dist is not None:
+            dist.destroy_process_group()
+        return 0
+
     if args.workload == "stream":
         if rank == 0:
             emit({"metric": "per-call latency of the drop-in entry points (us)", "value": None,
@@ -1007,27 +1124,10 @@ def main():
 
     global HOST_PINNED
     HOST_PINNED = bool(args.host_pinned)
+    log(f"workload {args.workload}: setting up")
     wl = Workload(args.workload, rank, world, args.stripes, args.threads, erased, args.queue_batch)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        wl.step()
-    barrier()
-    st = torch.cuda.current_stream()  # every device-resident workload launches on it (rawcoder._stream_ptr)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(st)
-        wl.step()
-        b.record(st)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    log(f"workload {args.workload}: {args.warmup} warm-up + {args.steps} timed steps")
+    elapsed, kern_ms = time_workload(wl, args.steps, args.warmup, dist)
     per_rank = gather_per_rank({"elapsed_s": round(elapsed, 5), "kernel_ms": round(kern_ms, 4), "numa_node": numa_node,
                                 "device": dev_id, "cpus": len(os.sched_getaffinity(0))}, dist)
     elapsed = max_over_ranks(elapsed, dist, device=red_dev)
@@ -1067,13 +1167,20 @@ def main():
         result["verified"] = wl._check()
     wl.free()
     del wl
+    if args.workload == "c2" and not args.no_fused:
+        try:
+            result["fused"] = fused_legs(args, rank, world, dist, red_dev)
+        except Exception as e:  # the headline stands on its own
+            result["fused"] = [{"error": f"{type(e).__name__}: {e}"}]
     if args.workload == "c2" and not args.no_e2e:
+        log("C5 end-to-end leg")
         try:
             result["e2e"] = e2e_leg(args, rank, world, dist, dev_idx, backend)
         except Exception as e:  # the device-resident line stands on its own
             result["e2e"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1:
         if not args.no_pmc and args.workload in KERNEL_PAT:
+            log("PMC traffic passes of the headline kernel")
             traffic, detail = pmc_traffic(args, result["roofline"]["alg_bytes_per_launch"])
             result["roofline"]["traffic"] = traffic
             result["roofline"]["pmc"] = detail
@@ -1088,6 +1195,7 @@ def main():
                                 "steps); rocprof_avg_ms: rocprofv3 durations of the same kernel's timed dispatches in a "
                                 "child run with the same warm-up and steps; frac uses kernel_ms")
         if not args.no_cpu:
+            log("CPU baseline")
             result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
             if "e2e" in result and "value" in result["e2e"]:
                 result["e2e"]["cpu_baseline"] = cpu_baseline("c5", args.cpu_seconds)

@@ -58,13 +58,30 @@ int ozec_version(void);
 /* number of visible GPUs; 0 when none (the factory then throws, so CodecUtil falls back to rs_java:
  * CodecUtil.createRawEncoderWithFallback, EC/rawcoder/util/CodecUtil.java:55-82) */
 int ozec_device_count(void);
-/* select the GPU used by subsequently created coders and host calls on this thread */
+/* hipSetDevice for the calling thread: the device of its device-pointer calls, and under OZEC_DEVICE_POLICY_CURRENT of
+ * the coders it creates and its host calls */
 int ozec_set_device(int device);
+/* ---- the GPUs of one drop-in process (one JVM per datanode / client drives every GPU of the node):
+ * the device list is every visible GPU, or the OZEC_DEVICES environment variable ("0,2,5" / "all"), or this call
+ * (n = 0 restores the default; duplicates allowed).  A coder is bound to one listed GPU when it is created (the
+ * policy below); its host-buffer calls and stripe queues run there.  ozec_encode_crc_host_batch and
+ * ozec_reconstruct_crc_host_batch split one batch into contiguous stripe ranges over the whole list, one pipeline per
+ * GPU, run at once.  Coder-less host calls (CRCs of host buffers, ozec_host_alloc placement) run on a listed GPU each
+ * thread is given on first use.  Device-pointer entry points run on the caller's current device. */
+int ozec_set_devices(const int *devices, int n);
+/* the device list: writes up to cap ordinals, returns how many there are */
+int ozec_get_devices(int *devices, int cap);
+#define OZEC_DEVICE_POLICY_ROUND_ROBIN 0 /* coders take the listed GPUs in turn (the default)                   */
+#define OZEC_DEVICE_POLICY_NUMA 1        /* in turn among the listed GPUs on the creating thread's NUMA node      */
+#define OZEC_DEVICE_POLICY_CURRENT 2     /* the creating thread's current device (one process per GPU)           */
+/* also OZEC_DEVICE_POLICY=round_robin|numa|current in the environment */
+int ozec_set_device_policy(int policy);
+int ozec_device_policy(void);
 /* wait for all work queued on the calling thread's current device (host-buffer calls are already synchronous) */
 int ozec_synchronize(void);
 /* give back the host-batch pipeline's chunk buffers (4 device + 4 pinned buffers of one chunk each: about 1.1 GiB
  * of HBM and, for pageable callers, of pinned memory with rs-6-3 1 MiB cells and 32-stripe chunks) and the staging
- * buffers of the idle host-call slots of the current device; the next call allocates again */
+ * buffers of the idle host-call slots, on every GPU the process has used; the next call allocates again */
 int ozec_release_staging(void);
 
 /* ---- coder lifecycle: RawErasureCoderFactory.createEncoder/createDecoder
@@ -83,6 +100,8 @@ void ozec_coder_free(ozec_coder *coder);
 int ozec_coder_retain(ozec_coder *coder);
 /* 1 after ozec_coder_release, else 0 */
 int ozec_coder_is_closed(const ozec_coder *coder);
+/* the GPU the coder's host-buffer calls run on (negative: error) */
+int ozec_coder_device(const ozec_coder *coder);
 int ozec_coder_info(const ozec_coder *coder, int *codec, int *num_data, int *num_parity, int *is_decoder);
 
 /* ---- encode: RawErasureEncoder.doEncode -> RSUtil.encodeData (EC/rawcoder/util/RSUtil.java:87-133),
@@ -237,8 +256,8 @@ uint32_t ozec_crc_combine(int checksum_type, uint32_t crc_a, uint32_t crc_b, uin
  * memory), else through pinned staging.  The buffers given to submit must stay valid and unmodified until wait()
  * has returned for that ticket (or until ozec_stripe_queue_free). */
 /* pinned host memory for cell buffers (the JNI side wraps it with NewDirectByteBuffer).  Its pages are placed on
- * the host NUMA node closest to the GPU (ozec_host_alloc: the calling thread's current device), so DMA never
- * crosses the inter-socket fabric; every staging buffer libozec allocates itself is placed the same way. */
+ * the host NUMA node closest to the GPU (ozec_host_alloc: the calling thread's GPU, see ozec_set_devices), so DMA
+ * never crosses the inter-socket fabric; every staging buffer libozec allocates itself is placed the same way. */
 int ozec_host_alloc(size_t bytes, void **out);
 int ozec_host_alloc_on(size_t bytes, int device, void **out);
 int ozec_host_free(void *p);

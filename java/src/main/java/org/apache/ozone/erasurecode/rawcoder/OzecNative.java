@@ -8,6 +8,13 @@ import java.nio.ByteBuffer;
  * JVM; {@link #checkAvailable()} throws when the library or a GPU is missing, which makes the HIP coder
  * constructors throw and CodecUtil fall back to the next coder (CodecUtil.java:62-78).
  * System property {@code ozone.ec.hip.library} may name the library file; otherwise java.library.path is searched.
+ *
+ * <p>One JVM drives every GPU of its node (a datanode or client is one process): {@code ozone.ec.hip.devices} (e.g.
+ * {@code 0,1,2,3}; default: every visible GPU) lists them and {@code ozone.ec.hip.device.policy}
+ * ({@code round_robin}, the default; {@code numa}; {@code current}) says how coders are bound to them -- each coder
+ * (one per ECKeyOutputStream, ECKeyOutputStream.java:117, and per reconstruction, ECBlockReconstructedStripeInputStream
+ * .java:232) runs its calls and stripe queues on its own GPU, and a host batch is split over all listed GPUs
+ * (ozec_set_devices, include/ozec.h).
  */
 public final class OzecNative {
   public static final int CODEC_RS = 0;
@@ -32,6 +39,29 @@ public final class OzecNative {
       failure = t;
     }
     LOAD_FAILURE = failure;
+    if (failure == null) {
+      configureDevices(System.getProperty("ozone.ec.hip.devices"), System.getProperty("ozone.ec.hip.device.policy"));
+    }
+  }
+
+  /** Apply the device properties; a bad value leaves the library's default (every visible GPU, round robin). */
+  static void configureDevices(String devices, String policy) {
+    try {
+      if (devices != null && !devices.trim().isEmpty() && !"all".equals(devices.trim())) {
+        final String[] parts = devices.split(",");
+        final int[] list = new int[parts.length];
+        for (int i = 0; i < parts.length; ++i) {
+          list[i] = Integer.parseInt(parts[i].trim());
+        }
+        setDevices(list);
+      }
+      if (policy != null) {
+        setDevicePolicy("numa".equals(policy) ? DEVICE_POLICY_NUMA
+            : "current".equals(policy) ? DEVICE_POLICY_CURRENT : DEVICE_POLICY_ROUND_ROBIN);
+      }
+    } catch (RuntimeException e) {
+      // NumberFormatException or a device the node does not have: keep the default
+    }
   }
 
   private OzecNative() {
@@ -52,6 +82,21 @@ public final class OzecNative {
   }
 
   public static native int deviceCount();
+
+  public static final int DEVICE_POLICY_ROUND_ROBIN = 0;
+  public static final int DEVICE_POLICY_NUMA = 1;
+  public static final int DEVICE_POLICY_CURRENT = 2;
+
+  // ---- the GPUs of this process (ozec_set_devices / ozec_get_devices / ozec_set_device_policy / ozec_coder_device)
+  /** The GPUs coders and host batches use from now on; an empty array restores every visible GPU. */
+  public static native void setDevices(int[] devices);
+
+  public static native int[] getDevices();
+
+  public static native void setDevicePolicy(int policy);
+
+  /** The GPU a coder handle's calls run on. */
+  static native int coderDevice(long handle);
 
   // ---- coders (ozec_encoder_create / ozec_decoder_create / ozec_coder_release + ozec_coder_free)
   static native long coderCreate(boolean decoder, int codec, int numData, int numParity);

@@ -10,14 +10,18 @@
  *   encodeDirect / decodeDirect   <- AbstractNativeRawEncoder.doEncode :49-73 / AbstractNativeRawDecoder.doDecode :49-75
  *                                    -> hadoop's performEncodeImpl / performDecodeImpl (HadoopNativeECAccessorUtil :32-58)
  *   encodeArrays / decodeArrays   <- doEncode(ByteArrayEncodingState) / doDecode(ByteArrayDecodingState); the reference
- *                                    copies heap arrays into direct buffers (:75-86), here they are pinned in place
+ *                                    copies heap arrays into direct buffers (:80-93), here into a per-thread pinned
+ *                                    arena (GetByteArrayRegion / SetByteArrayRegion, never a critical pin across
+ *                                    device work: heap_* below)
  *   coderCreate / coderRelease    <- NativeRSRawEncoder ctor / release (EC/rawcoder/NativeRSRawEncoder.java:39-62)
  *   crcUpdate* / checksumWindows* <- ChecksumByteBuffer.update (CM/ChecksumByteBuffer.java:32-44) and
  *                                    Checksum.computeChecksum (CM/Checksum.java:157-200)
  *   queue*                        <- the stripe queue of ECKeyOutputStream (hadoop-ozone/client/.../ECKeyOutputStream.java:501-543)
  */
 #include <jni.h>
+#include <pthread.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../include/ozec.h"
@@ -65,16 +69,16 @@ static int collect_direct(JNIEnv *env, jobjectArray arr, jintArray offs, ozm_buf
   return 0;
 }
 
-/* Java byte[][] (+ int[] offsets): references first (JNI calls are not allowed inside a critical region), then
- * every array pinned with GetPrimitiveArrayCritical; unpin() releases them. */
+/* Java byte[][] (+ int[] offsets) -> the arrays' local references, lengths and offsets (no address: heap arrays are
+ * copied, see heap_* below); refs_free() deletes the references. */
 typedef struct {
   jbyteArray arr[MAX_BUFS];
   int n;
-} pinned_set;
+} array_set;
 
-static int collect_arrays(JNIEnv *env, jobjectArray arr, jintArray offs, ozm_buf *bufs, pinned_set *ps,
+static int collect_arrays(JNIEnv *env, jobjectArray arr, jintArray offs, ozm_buf *bufs, array_set *as,
                           ozm_status *st) {
-  ps->n = 0;
+  as->n = 0;
   if (!arr || !offs) return ozm_fail(OZEC_EINVAL, "Invalid buffer array, null", st);
   const jsize len = (*env)->GetArrayLength(env, arr);
   if (len > MAX_BUFS || (*env)->GetArrayLength(env, offs) < len)
@@ -82,31 +86,145 @@ static int collect_arrays(JNIEnv *env, jobjectArray arr, jintArray offs, ozm_buf
   jint o[MAX_BUFS];
   (*env)->GetIntArrayRegion(env, offs, 0, len, o);
   for (jsize i = 0; i < len; ++i) {
-    ps->arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, arr, i);
+    as->arr[i] = (jbyteArray)(*env)->GetObjectArrayElement(env, arr, i);
     memset(&bufs[i], 0, sizeof(bufs[i]));
-    if (ps->arr[i]) {
+    if (as->arr[i]) {
       bufs[i].present = 1;
-      bufs[i].capacity = (*env)->GetArrayLength(env, ps->arr[i]);
+      bufs[i].capacity = (*env)->GetArrayLength(env, as->arr[i]);
       bufs[i].offset = o[i];
     }
   }
-  ps->n = (int)len;
+  as->n = (int)len;
   return 0;
 }
 
-static void pin(JNIEnv *env, pinned_set *ps, ozm_buf *bufs) {
-  for (int i = 0; i < ps->n; ++i)
-    if (ps->arr[i]) bufs[i].base = (*env)->GetPrimitiveArrayCritical(env, ps->arr[i], NULL);
+static void refs_free(JNIEnv *env, array_set *as) {
+  for (int i = 0; i < as->n; ++i)
+    if (as->arr[i]) (*env)->DeleteLocalRef(env, as->arr[i]);
+  as->n = 0;
 }
 
-/* mode 0 copies back (outputs) if the VM handed out a copy; JNI_ABORT for inputs, which are never modified */
-static void unpin(JNIEnv *env, pinned_set *ps, ozm_buf *bufs, jint mode) {
-  for (int i = 0; i < ps->n; ++i)
-    if (ps->arr[i]) {
-      if (bufs[i].base) (*env)->ReleasePrimitiveArrayCritical(env, ps->arr[i], (void *)bufs[i].base, mode);
-      (*env)->DeleteLocalRef(env, ps->arr[i]);
+/* ---------------------------------------------------------------- heap arrays: copied, never pinned across the GPU
+ * A byte[] pinned with GetPrimitiveArrayCritical for the whole call would hold the VM's GC locker through staging, H2D,
+ * kernel and D2H (~0.3 ms per rs-6-3 stripe of 1 MiB cells; every ECKeyOutputStream writer passes heap buffers,
+ * ECKeyOutputStream.java:701).  Instead each call copies the regions it reads with GetByteArrayRegion into this
+ * thread's pinned arena (ozec_host_alloc: pinned, on the device's NUMA node), runs on the arena -- libozec DMAs pinned
+ * memory in place, one rectangular copy each way for cells at one stride -- and copies the outputs back with
+ * SetByteArrayRegion: the two host copies libozec's own staging would make, with no JNI pin while libozec works, as the
+ * reference's bridge copies heap arrays into direct buffers (AbstractNativeRawEncoder.java:80-93).  Calls are cut in
+ * column chunks of HEAP_CHUNK bytes per cell (coding is byte-position-wise), so the arena stays at (k + p) x 4 MiB. */
+#define HEAP_CHUNK ((int64_t)4 << 20)
+#define ARENA_ALIGN 256
+
+typedef struct {
+  uint8_t *p;
+  size_t cap;
+} arena_t;
+
+static pthread_key_t g_arena_key;
+static pthread_once_t g_arena_once = PTHREAD_ONCE_INIT;
+static int g_arena_key_ok;
+
+static void arena_destroy(void *v) {
+  arena_t *a = (arena_t *)v;
+  if (!a) return;
+  if (a->p) (void)ozec_host_free(a->p);
+  free(a);
+}
+
+static void arena_make_key(void) { g_arena_key_ok = pthread_key_create(&g_arena_key, arena_destroy) == 0; }
+
+/* this thread's pinned arena of at least `bytes`, NULL (status set) when it cannot be had */
+static uint8_t *arena(size_t bytes, ozm_status *st) {
+  (void)pthread_once(&g_arena_once, arena_make_key);
+  if (!g_arena_key_ok) {
+    ozm_fail(OZEC_ENOMEM, "no thread-local arena", st);
+    return NULL;
+  }
+  arena_t *a = (arena_t *)pthread_getspecific(g_arena_key);
+  if (!a) {
+    a = (arena_t *)calloc(1, sizeof *a);
+    if (!a || pthread_setspecific(g_arena_key, a) != 0) {
+      free(a);
+      ozm_fail(OZEC_ENOMEM, "no thread-local arena", st);
+      return NULL;
     }
-  ps->n = 0;
+  }
+  if (a->cap < bytes) {
+    if (a->p) (void)ozec_host_free(a->p);
+    a->p = NULL;
+    a->cap = 0;
+    const size_t cap = (bytes + ((size_t)1 << 20) - 1) >> 20 << 20;
+    int rc = ozec_host_alloc(cap, (void **)&a->p);
+    if (rc) {
+      a->p = NULL;
+      ozm_fail(rc, NULL, st);
+      return NULL;
+    }
+    a->cap = cap;
+  }
+  return a->p;
+}
+
+static int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+/* the present arrays' regions [offset + off, + cl) into consecutive arena slots of `stride` bytes from slot `first`
+ * (absent ones take no slot); stage[i] describes the copy as a buffer at offset 0 */
+static void copy_in(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl, uint8_t *base,
+                    int64_t stride, int first, ozm_buf *stage) {
+  int slot = first;
+  for (int i = 0; i < as->n; ++i) {
+    memset(&stage[i], 0, sizeof(stage[i]));
+    if (!as->arr[i]) continue;
+    uint8_t *dst = base + (int64_t)slot++ * stride;
+    (*env)->GetByteArrayRegion(env, as->arr[i], (jsize)(bufs[i].offset + off), (jsize)cl, (jbyte *)dst);
+    stage[i].present = 1;
+    stage[i].base = dst;
+    stage[i].capacity = cl;
+  }
+}
+
+static void out_slots(const array_set *as, int64_t cl, uint8_t *base, int64_t stride, int first, ozm_buf *stage) {
+  for (int i = 0; i < as->n; ++i) {
+    memset(&stage[i], 0, sizeof(stage[i]));
+    stage[i].present = as->arr[i] != NULL;
+    stage[i].base = base + (int64_t)(first + i) * stride;
+    stage[i].capacity = cl;
+  }
+}
+
+static void copy_out(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl,
+                     const ozm_buf *stage) {
+  for (int i = 0; i < as->n; ++i)
+    if (as->arr[i])
+      (*env)->SetByteArrayRegion(env, as->arr[i], (jsize)(bufs[i].offset + off), (jsize)cl,
+                                 (const jbyte *)stage[i].base);
+}
+
+static int present_count(const array_set *as) {
+  int n = 0;
+  for (int i = 0; i < as->n; ++i) n += as->arr[i] != NULL;
+  return n;
+}
+
+/* encode (erased == NULL) or decode of heap arrays already validated by ozm_*_check */
+static int heap_code(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_buf *ib, const array_set *ao,
+                     const ozm_buf *ob, const int *erased, int ne, int64_t len, ozm_status *st) {
+  ozm_buf si[MAX_BUFS], so[MAX_BUFS];
+  const int nin = present_count(ai);
+  for (int64_t off = 0; off < len; off += HEAP_CHUNK) {
+    const int64_t cl = len - off < HEAP_CHUNK ? len - off : HEAP_CHUNK;
+    const int64_t stride = round_up(cl, ARENA_ALIGN);
+    uint8_t *a = arena((size_t)((int64_t)(nin + ao->n) * stride), st);
+    if (!a) return st->code;
+    copy_in(env, ai, ib, off, cl, a, stride, 0, si);
+    out_slots(ao, cl, a, stride, nin, so);
+    int rc = erased ? ozm_decode(h, si, ai->n, erased, ne, so, ao->n, cl, st)
+                    : ozm_encode(h, si, ai->n, so, ao->n, cl, st);
+    if (rc) return rc;
+    copy_out(env, ao, ob, off, cl, so);
+  }
+  return 0;
 }
 
 static int int_array(JNIEnv *env, jintArray a, int *out, int max, int *n, ozm_status *st) {
@@ -133,6 +251,44 @@ JNIEXPORT jint JNICALL JNI_FN(deviceCount)(JNIEnv *env, jclass cls) {
   (void)env;
   (void)cls;
   return ozec_device_count();
+}
+
+/* ---- the GPUs of this JVM (ozec_set_devices; OzecNative reads ozone.ec.hip.devices / ozone.ec.hip.device.policy) */
+JNIEXPORT void JNICALL JNI_FN(setDevices)(JNIEnv *env, jclass cls, jintArray devices) {
+  (void)cls;
+  int d[MAX_BUFS], n = 0;
+  ozm_status st;
+  if (devices && int_array(env, devices, d, MAX_BUFS, &n, &st)) {
+    throw_status(env, &st);
+    return;
+  }
+  int rc = ozec_set_devices(d, n);
+  if (rc) throw_rc(env, rc);
+}
+
+JNIEXPORT jintArray JNICALL JNI_FN(getDevices)(JNIEnv *env, jclass cls) {
+  (void)cls;
+  int d[MAX_BUFS];
+  int n = ozec_get_devices(d, MAX_BUFS);
+  if (n > MAX_BUFS) n = MAX_BUFS;
+  jintArray a = (*env)->NewIntArray(env, n);
+  if (a) (*env)->SetIntArrayRegion(env, a, 0, n, (const jint *)d);
+  return a;
+}
+
+JNIEXPORT void JNICALL JNI_FN(setDevicePolicy)(JNIEnv *env, jclass cls, jint policy) {
+  (void)cls;
+  int rc = ozec_set_device_policy(policy);
+  if (rc) throw_rc(env, rc);
+}
+
+JNIEXPORT jint JNICALL JNI_FN(coderDevice)(JNIEnv *env, jclass cls, jlong h) {
+  (void)cls;
+  if (!h) {
+    throw_rc(env, OZEC_ECLOSED);
+    return -1;
+  }
+  return ozec_coder_device((ozec_coder *)(intptr_t)h);
 }
 
 /* RawErasureCoderFactory.createEncoder/createDecoder: throws when no GPU is usable, so CodecUtil falls back
@@ -174,18 +330,15 @@ JNIEXPORT void JNICALL JNI_FN(encodeArrays)(JNIEnv *env, jclass cls, jlong h, jo
                                             jobjectArray out, jintArray outOff) {
   (void)cls;
   ozm_buf ib[MAX_BUFS], ob[MAX_BUFS];
-  pinned_set pi, po;
+  array_set ai, ao;
   ozm_status st;
-  pi.n = po.n = 0;
-  int rc = collect_arrays(env, in, inOff, ib, &pi, &st);
-  if (!rc) rc = collect_arrays(env, out, outOff, ob, &po, &st);
-  if (!rc) {
-    pin(env, &pi, ib);
-    pin(env, &po, ob);
-    rc = ozm_encode((ozec_coder *)(intptr_t)h, ib, pi.n, ob, po.n, len, &st); /* no JNI call in between */
-  }
-  unpin(env, &po, ob, 0);
-  unpin(env, &pi, ib, JNI_ABORT);
+  ai.n = ao.n = 0;
+  int rc = collect_arrays(env, in, inOff, ib, &ai, &st);
+  if (!rc) rc = collect_arrays(env, out, outOff, ob, &ao, &st);
+  if (!rc) rc = ozm_encode_check((ozec_coder *)(intptr_t)h, ib, ai.n, ob, ao.n, len, &st);
+  if (!rc) rc = heap_code(env, (ozec_coder *)(intptr_t)h, &ai, ib, &ao, ob, NULL, 0, len, &st);
+  refs_free(env, &ao);
+  refs_free(env, &ai);
   if (rc) throw_status(env, &st);
 }
 
@@ -208,19 +361,16 @@ JNIEXPORT void JNICALL JNI_FN(decodeArrays)(JNIEnv *env, jclass cls, jlong h, jo
   ozm_buf ib[MAX_BUFS], ob[MAX_BUFS];
   int er[MAX_BUFS];
   int ne = 0;
-  pinned_set pi, po;
+  array_set ai, ao;
   ozm_status st;
-  pi.n = po.n = 0;
+  ai.n = ao.n = 0;
   int rc = int_array(env, erased, er, MAX_BUFS, &ne, &st);
-  if (!rc) rc = collect_arrays(env, in, inOff, ib, &pi, &st);
-  if (!rc) rc = collect_arrays(env, out, outOff, ob, &po, &st);
-  if (!rc) {
-    pin(env, &pi, ib);
-    pin(env, &po, ob);
-    rc = ozm_decode((ozec_coder *)(intptr_t)h, ib, pi.n, er, ne, ob, po.n, len, &st);
-  }
-  unpin(env, &po, ob, 0);
-  unpin(env, &pi, ib, JNI_ABORT);
+  if (!rc) rc = collect_arrays(env, in, inOff, ib, &ai, &st);
+  if (!rc) rc = collect_arrays(env, out, outOff, ob, &ao, &st);
+  if (!rc) rc = ozm_decode_check((ozec_coder *)(intptr_t)h, ib, ai.n, er, ne, ob, ao.n, len, &st);
+  if (!rc) rc = heap_code(env, (ozec_coder *)(intptr_t)h, &ai, ib, &ao, ob, er, ne, len, &st);
+  refs_free(env, &ao);
+  refs_free(env, &ai);
   if (rc) throw_status(env, &st);
 }
 
@@ -254,68 +404,98 @@ JNIEXPORT jint JNICALL JNI_FN(crcUpdateArray)(JNIEnv *env, jclass cls, jint type
   if (!arr) {
     rc = ozm_crc_update(type, &s, &b, len, &st);
   } else {
+    /* bounds first (no address read), then the region in arena chunks: the register carries across them */
     b.present = 1;
     b.capacity = (*env)->GetArrayLength(env, arr);
     b.offset = off;
-    b.base = (*env)->GetPrimitiveArrayCritical(env, arr, NULL);
-    rc = ozm_crc_update(type, &s, &b, len, &st);
-    if (b.base) (*env)->ReleasePrimitiveArrayCritical(env, arr, (void *)b.base, JNI_ABORT);
+    b.base = (void *)arr; /* a placeholder address for the check: never read */
+    const uint8_t *unused;
+    rc = len == 0 ? 0 : ozm_resolve(&b, 1, 0, len, &unused, &st);
+    for (int64_t o = 0; !rc && o < len; o += HEAP_CHUNK) {
+      const int64_t cl = len - o < HEAP_CHUNK ? len - o : HEAP_CHUNK;
+      uint8_t *a = arena((size_t)cl, &st);
+      if (!a) {
+        rc = st.code;
+        break;
+      }
+      (*env)->GetByteArrayRegion(env, arr, (jsize)(off + o), (jsize)cl, (jbyte *)a);
+      ozm_buf c = {a, 0, cl, 1};
+      rc = ozm_crc_update(type, &s, &c, cl, &st);
+    }
   }
   if (rc) throw_status(env, &st);
   return (jint)s;
 }
 
-/* Checksum.computeChecksum of one direct buffer region: big-endian CRC bytes of every window into out; returns the
- * number of bytes written (4 per window) */
-JNIEXPORT jint JNICALL JNI_FN(checksumWindowsDirect)(JNIEnv *env, jclass cls, jint type, jobject buf, jint off, jint len,
-                                                     jint bpc, jbyteArray out) {
-  (void)cls;
-  ozm_buf b = {0};
+/* Checksum.computeChecksum of one buffer region (data: a direct buffer, or a byte[] copied into the arena in chunks
+ * of whole windows): big-endian CRC bytes of every window into out (SetByteArrayRegion, no pin across the GPU call);
+ * returns the number of bytes written (4 per window) */
+static jint checksum_windows(JNIEnv *env, jint type, jobject direct, jbyteArray data, jint off, jint len, jint bpc,
+                             jbyteArray out) {
   ozm_status st;
-  int64_t written = 0;
   if (!out) {
     ozm_fail(OZEC_EINVAL, "null checksum output", &st);
     throw_status(env, &st);
     return 0;
   }
-  b.present = buf != NULL;
-  if (buf) {
-    b.base = (*env)->GetDirectBufferAddress(env, buf);
-    b.capacity = (int64_t)(*env)->GetDirectBufferCapacity(env, buf);
-    b.offset = off;
+  ozm_buf b = {0};
+  b.present = direct != NULL || data != NULL;
+  if (direct) {
+    b.base = (*env)->GetDirectBufferAddress(env, direct);
+    b.capacity = (int64_t)(*env)->GetDirectBufferCapacity(env, direct);
+  } else if (data) {
+    b.base = (void *)data; /* a placeholder address for the bounds check: never read */
+    b.capacity = (*env)->GetArrayLength(env, data);
   }
+  b.offset = off;
   const jsize cap = (*env)->GetArrayLength(env, out);
-  uint8_t *o = (uint8_t *)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
-  int rc = ozm_checksum_windows(type, &b, len, bpc, o, cap, &written, &st);
-  if (o) (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
+  int rc = 0;
+  int64_t total = 0;
+  const uint8_t *unused;
+  if (bpc <= 0) rc = ozm_fail(OZEC_EINVAL, "bytesPerChecksum must be positive", &st);
+  else if (len != 0 && (rc = ozm_resolve(&b, 1, 0, len, &unused, &st)) == 0 &&
+           (int64_t)cap < 4 * (((int64_t)len + bpc - 1) / bpc))
+    rc = ozm_fail(OZEC_EINVAL, "checksum output too small", &st);
+  /* whole windows per round trip (at least one): the arena holds the chunk's data (byte[] only) and its CRCs */
+  const int64_t chunk = bpc <= 0 ? 1 : HEAP_CHUNK < bpc ? bpc : HEAP_CHUNK / bpc * bpc;
+  for (int64_t o = 0; !rc && o < len; o += chunk) {
+    const int64_t cl = len - o < chunk ? len - o : chunk;
+    const int64_t nw = (cl + bpc - 1) / bpc, dbytes = direct ? 0 : round_up(cl, ARENA_ALIGN);
+    uint8_t *a = arena((size_t)(dbytes + 4 * nw), &st);
+    if (!a) {
+      rc = st.code;
+      break;
+    }
+    ozm_buf c = b;
+    if (!direct) {
+      (*env)->GetByteArrayRegion(env, data, (jsize)(off + o), (jsize)cl, (jbyte *)a);
+      c.base = a;
+      c.offset = 0;
+      c.capacity = cl;
+    } else {
+      c.offset = off + o;
+    }
+    int64_t written = 0;
+    rc = ozm_checksum_windows(type, &c, cl, bpc, a + dbytes, 4 * nw, &written, &st);
+    if (!rc) {
+      (*env)->SetByteArrayRegion(env, out, (jsize)total, (jsize)written, (const jbyte *)(a + dbytes));
+      total += written;
+    }
+  }
   if (rc) throw_status(env, &st);
-  return (jint)written;
+  return (jint)total;
+}
+
+JNIEXPORT jint JNICALL JNI_FN(checksumWindowsDirect)(JNIEnv *env, jclass cls, jint type, jobject buf, jint off, jint len,
+                                                     jint bpc, jbyteArray out) {
+  (void)cls;
+  return checksum_windows(env, type, buf, NULL, off, len, bpc, out);
 }
 
 JNIEXPORT jint JNICALL JNI_FN(checksumWindowsArray)(JNIEnv *env, jclass cls, jint type, jbyteArray data, jint off,
                                                     jint len, jint bpc, jbyteArray out) {
   (void)cls;
-  ozm_buf b = {0};
-  ozm_status st;
-  int64_t written = 0;
-  if (!out) {
-    ozm_fail(OZEC_EINVAL, "null checksum output", &st);
-    throw_status(env, &st);
-    return 0;
-  }
-  const jsize cap = (*env)->GetArrayLength(env, out);
-  if (data) {
-    b.present = 1;
-    b.capacity = (*env)->GetArrayLength(env, data);
-    b.offset = off;
-    b.base = (*env)->GetPrimitiveArrayCritical(env, data, NULL);
-  }
-  uint8_t *o = (uint8_t *)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
-  int rc = ozm_checksum_windows(type, &b, len, bpc, o, cap, &written, &st);
-  if (o) (*env)->ReleasePrimitiveArrayCritical(env, out, o, 0);
-  if (data && b.base) (*env)->ReleasePrimitiveArrayCritical(env, data, (void *)b.base, JNI_ABORT);
-  if (rc) throw_status(env, &st);
-  return (jint)written;
+  return checksum_windows(env, type, NULL, data, off, len, bpc, out);
 }
 
 /* ---------------------------------------------------------------- pinned memory + stripe queue (§8(f) row 3) */

@@ -29,18 +29,18 @@ int ozm_fail(int rc, const char *msg, ozm_status *st) {
 
 static int ok(ozm_status *st) { return ozm_fail(OZEC_OK, "", st); }
 
-int ozm_resolve(const ozm_buf *bufs, int n, int allow_absent, int64_t len, const uint8_t **out, ozm_status *st) {
+/* presence, offsets and capacities of n buffers for `len` bytes each; with need_base, their addresses too */
+static int check_bufs(const ozm_buf *bufs, int n, int allow_absent, int64_t len, int need_base, ozm_status *st) {
   char msg[160];
-  if (n < 0 || (n > 0 && (!bufs || !out))) return ozm_fail(OZEC_EINVAL, "Invalid buffer array", st);
+  if (n < 0 || (n > 0 && !bufs)) return ozm_fail(OZEC_EINVAL, "Invalid buffer array", st);
   if (len < 0) return ozm_fail(OZEC_EINVAL, "Invalid data length, negative", st);
   for (int i = 0; i < n; ++i) {
     const ozm_buf *b = &bufs[i];
     if (!b->present) {
       if (!allow_absent) return ozm_fail(OZEC_EINVAL, "Invalid buffer found, not allowing null", st);
-      out[i] = NULL;
       continue;
     }
-    if (!b->base) { /* GetDirectBufferAddress of a heap buffer, or a failed pin */
+    if (need_base && !b->base) { /* GetDirectBufferAddress of a heap buffer */
       snprintf(msg, sizeof(msg), "Invalid buffer [%d]: no native address (not a direct buffer)", i);
       return ozm_fail(OZEC_EINVAL, msg, st);
     }
@@ -49,8 +49,14 @@ int ozm_resolve(const ozm_buf *bufs, int n, int allow_absent, int64_t len, const
                (long long)b->offset, (long long)len, (long long)b->capacity);
       return ozm_fail(OZEC_EINVAL, msg, st);
     }
-    out[i] = (const uint8_t *)b->base + b->offset;
   }
+  return ok(st);
+}
+
+int ozm_resolve(const ozm_buf *bufs, int n, int allow_absent, int64_t len, const uint8_t **out, ozm_status *st) {
+  if (n > 0 && !out) return ozm_fail(OZEC_EINVAL, "Invalid buffer array", st);
+  if (check_bufs(bufs, n, allow_absent, len, 1, st)) return st ? st->code : OZEC_EINVAL;
+  for (int i = 0; i < n; ++i) out[i] = bufs[i].present ? (const uint8_t *)bufs[i].base + bufs[i].offset : NULL;
   return ok(st);
 }
 
@@ -63,8 +69,8 @@ static int coder_shape(ozec_coder *c, int want_decoder, int *k, int *p, ozm_stat
   return ok(st);
 }
 
-int ozm_encode(ozec_coder *enc, const ozm_buf *in, int nin, const ozm_buf *out, int nout, int64_t len,
-               ozm_status *st) {
+int ozm_encode_check(ozec_coder *enc, const ozm_buf *in, int nin, const ozm_buf *out, int nout, int64_t len,
+                     ozm_status *st) {
   int k = 0, p = 0;
   char msg[96];
   if (coder_shape(enc, 0, &k, &p, st)) return st ? st->code : OZEC_EINVAL;
@@ -76,25 +82,39 @@ int ozm_encode(ozec_coder *enc, const ozm_buf *in, int nin, const ozm_buf *out, 
     snprintf(msg, sizeof(msg), "Invalid outputs length %d !=%d", nout, p);
     return ozm_fail(OZEC_EINVAL, msg, st);
   }
+  if (k > OZEC_MAX_K || p > OZEC_MAX_ROWS) return ozm_fail(OZEC_EUNSUPPORTED, "schema exceeds the kernel limits", st);
+  if (check_bufs(in, nin, 0, len, 0, st) || check_bufs(out, nout, 0, len, 0, st)) return st ? st->code : OZEC_EINVAL;
+  return ok(st);
+}
+
+int ozm_encode(ozec_coder *enc, const ozm_buf *in, int nin, const ozm_buf *out, int nout, int64_t len,
+               ozm_status *st) {
+  if (ozm_encode_check(enc, in, nin, out, nout, len, st)) return st ? st->code : OZEC_EINVAL;
   const uint8_t *ip[OZEC_MAX_K];
   const uint8_t *op[OZEC_MAX_ROWS];
-  if (k > OZEC_MAX_K || p > OZEC_MAX_ROWS) return ozm_fail(OZEC_EUNSUPPORTED, "schema exceeds the kernel limits", st);
   if (ozm_resolve(in, nin, 0, len, ip, st) || ozm_resolve(out, nout, 0, len, op, st)) return st ? st->code : OZEC_EINVAL;
   int rc = ozec_encode(enc, ip, (uint8_t *const *)op, (size_t)len);
   return rc ? ozm_fail(rc, NULL, st) : ok(st);
 }
 
-int ozm_decode(ozec_coder *dec, const ozm_buf *in, int nin, const int *erased, int nerased, const ozm_buf *out,
-               int nout, int64_t len, ozm_status *st) {
+int ozm_decode_check(ozec_coder *dec, const ozm_buf *in, int nin, const int *erased, int nerased, const ozm_buf *out,
+                     int nout, int64_t len, ozm_status *st) {
   int k = 0, p = 0;
   if (coder_shape(dec, 1, &k, &p, st)) return st ? st->code : OZEC_EINVAL;
   if (nin != k + p) return ozm_fail(OZEC_EINVAL, "Invalid inputs length", st); /* DecodingState.java:35-51 */
   if (nerased != nout || (nerased > 0 && !erased))
     return ozm_fail(OZEC_EINVAL, "erasedIndexes and outputs mismatch in length", st);
   if (nerased > p) return ozm_fail(OZEC_EINVAL, "Too many erased, not recoverable", st);
+  if (nin > 256 || nout > OZEC_MAX_ROWS) return ozm_fail(OZEC_EUNSUPPORTED, "schema exceeds the kernel limits", st);
+  if (check_bufs(in, nin, 1, len, 0, st) || check_bufs(out, nout, 0, len, 0, st)) return st ? st->code : OZEC_EINVAL;
+  return ok(st);
+}
+
+int ozm_decode(ozec_coder *dec, const ozm_buf *in, int nin, const int *erased, int nerased, const ozm_buf *out,
+               int nout, int64_t len, ozm_status *st) {
+  if (ozm_decode_check(dec, in, nin, erased, nerased, out, nout, len, st)) return st ? st->code : OZEC_EINVAL;
   const uint8_t *ip[256];
   const uint8_t *op[OZEC_MAX_ROWS];
-  if (nin > 256 || nout > OZEC_MAX_ROWS) return ozm_fail(OZEC_EUNSUPPORTED, "schema exceeds the kernel limits", st);
   if (ozm_resolve(in, nin, 1, len, ip, st) || ozm_resolve(out, nout, 0, len, op, st)) return st ? st->code : OZEC_EINVAL;
   int rc = ozec_decode(dec, ip, erased, nerased, (uint8_t *const *)op, (size_t)len);
   return rc ? ozm_fail(rc, NULL, st) : ok(st);

@@ -57,6 +57,12 @@ int ozm_fail(int rc, const char *msg, ozm_status *st);
  * Every present buffer must hold len bytes from its offset (offset >= 0, offset + len <= capacity). */
 int ozm_resolve(const ozm_buf *bufs, int n, int allow_absent, int64_t len, const uint8_t **out, ozm_status *st);
 
+/* ozm_encode / ozm_decode's validation alone (coder shape, counts, every present buffer's offset + len within its
+ * capacity) without reading any address: the JNI glue checks heap arrays with it before it copies their regions */
+int ozm_encode_check(ozec_coder *enc, const ozm_buf *in, int nin, const ozm_buf *out, int nout, int64_t len,
+                     ozm_status *st);
+int ozm_decode_check(ozec_coder *dec, const ozm_buf *in, int nin, const int *erased, int nerased, const ozm_buf *out,
+                     int nout, int64_t len, ozm_status *st);
 /* performEncodeImpl(inputs, inputOffsets, dataLen, outputs, outputOffsets): nin == k, nout == p */
 int ozm_encode(ozec_coder *enc, const ozm_buf *in, int nin, const ozm_buf *out, int nout, int64_t len,
                ozm_status *st);

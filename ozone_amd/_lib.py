@@ -146,6 +146,11 @@ _SIGS = {
     "ozec_stats_reset": (None, []),
     "ozec_set_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
     "ozec_tuning_variants": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "ozec_set_devices": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "ozec_get_devices": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "ozec_set_device_policy": (ctypes.c_int, [ctypes.c_int]),
+    "ozec_device_policy": (ctypes.c_int, []),
+    "ozec_coder_device": (ctypes.c_int, [ctypes.c_void_p]),
     "ozec_fill_splitmix64": (ctypes.c_int, [c_voidp, c_size, ctypes.c_uint64, ctypes.c_uint64, c_voidp]),
     "ozec_fill_splitmix64_cells": (ctypes.c_int, [c_voidp, c_i64, c_size, c_size, ctypes.c_uint64, ctypes.c_uint64,
                                                   c_voidp]),

@@ -15,10 +15,12 @@
 #include <mutex>
 #include <regex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ozec.h"
 #include "crc_host.hpp"
+#include "devices.hpp"
 #include "gf256.hpp"
 #include "copy_pool.hpp"
 #include "kernels.hpp"
@@ -265,6 +267,7 @@ thread_local bool g_stat_failed = false;
 // coder handle
 
 struct ozec_coder {
+  int device = -1;  // the GPU its host-buffer calls and stripe queues run on (devices.hpp: chosen at creation)
   int codec = OZEC_CODEC_RS;
   int k = 0, p = 0;
   bool decoder = false;
@@ -521,6 +524,26 @@ int ozec_set_device(int device) {
   return OZEC_OK;
 }
 
+int ozec_set_devices(const int *devices, int n) {
+  if (int rc = ozec::set_device_list(devices, n))
+    return fail(rc, rc == OZEC_EDEVICE ? "no such device in the list" : "invalid device list");
+  return OZEC_OK;
+}
+
+int ozec_get_devices(int *devices, int cap) {
+  const std::vector<int> l = ozec::device_list();
+  for (size_t i = 0; i < l.size() && static_cast<int>(i) < cap; ++i)
+    if (devices) devices[i] = l[i];
+  return static_cast<int>(l.size());
+}
+
+int ozec_set_device_policy(int policy) {
+  if (ozec::set_device_policy(policy)) return fail(OZEC_EINVAL, "unknown device policy " + std::to_string(policy));
+  return OZEC_OK;
+}
+
+int ozec_device_policy(void) { return ozec::device_policy(); }
+
 int ozec_synchronize(void) {
   OZEC_HIP(hipDeviceSynchronize());
   return OZEC_OK;
@@ -537,10 +560,15 @@ static int coder_create(int codec, int k, int p, bool decoder, ozec_coder **out)
   if (int rc = check_limits(k, codec == OZEC_CODEC_XOR ? 1 : p)) return rc;
   // a GPU coder must not be constructible without a device, so CodecUtil falls back to rs_java
   // (CodecUtil.createRawEncoderWithFallback, CodecUtil.java:62-78)
+  const int dev = ozec::pick_device();
+  if (dev < 0) return fail(OZEC_EDEVICE, "no HIP device available");
+  ozec::DeviceScope ds(dev);
+  if (!ds.ok()) return fail(OZEC_EDEVICE, "cannot select device " + std::to_string(dev));
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
   auto *c = new (std::nothrow) ozec_coder();
   if (!c) return fail(OZEC_ENOMEM, "out of memory");
+  c->device = dev;
   c->codec = codec;
   c->k = k;
   c->p = p;
@@ -567,14 +595,21 @@ void ozec_coder_free(ozec_coder *c) {
 }
 
 int ozec_release_staging(void) {
-  DevCtx *ctx;
-  if (int rc = get_ctx(&ctx)) return rc;
+  std::vector<DevCtx *> ctxs;
   {
-    std::lock_guard<std::mutex> lk(ctx->e2e.mu);
-    ctx->e2e.shrink();
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    for (auto &c : g_ctx)
+      if (c) ctxs.push_back(c.get());
   }
-  std::lock_guard<std::mutex> lk(ctx->pool_mu);
-  for (Slot *s : ctx->free_slots) s->shrink();  // leased slots keep theirs until their call returns
+  for (DevCtx *ctx : ctxs) {  // every GPU this process has used
+    ozec::DeviceScope ds(ctx->device);
+    {
+      std::lock_guard<std::mutex> lk(ctx->e2e.mu);
+      ctx->e2e.shrink();
+    }
+    std::lock_guard<std::mutex> lk(ctx->pool_mu);
+    for (Slot *s : ctx->free_slots) s->shrink();  // leased slots keep theirs until their call returns
+  }
   return OZEC_OK;
 }
 
@@ -585,6 +620,11 @@ int ozec_coder_retain(ozec_coder *c) {
 }
 
 int ozec_coder_is_closed(const ozec_coder *c) { return c && c->closed.load() ? 1 : 0; }
+
+int ozec_coder_device(const ozec_coder *c) {
+  if (!c) return fail(OZEC_EINVAL, "null coder");
+  return c->device;
+}
 
 int ozec_coder_info(const ozec_coder *c, int *codec, int *k, int *p, int *is_decoder) {
   if (!c) return fail(OZEC_EINVAL, "null coder");
@@ -608,6 +648,7 @@ int ozec_encode(ozec_coder *enc, const uint8_t *const *inputs, uint8_t *const *o
   for (int r = 0; r < rows; ++r)
     if (!outputs[r]) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
   if (len == 0) return OZEC_OK;  // RawErasureEncoder.java:73-75
+  ozec::DeviceScope ds(enc->device);  // the coder's GPU (devices.hpp)
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
   CodeArgs a{};
@@ -700,6 +741,7 @@ int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased
   if (int rc = plan_decode(dec, present, erased, n_erased, units, rows)) return rc;
   if (len == 0 || n_erased == 0) return OZEC_OK;
   const int nin = static_cast<int>(units.size());
+  ozec::DeviceScope ds(dec->device);  // the coder's GPU (devices.hpp)
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
   CodeArgs a{};
@@ -847,6 +889,7 @@ static int checksum_host(int checksum_type, const uint8_t *data, size_t len, siz
   if (bpc == 0) return fail(OZEC_EINVAL, "bytesPerChecksum must be positive");
   if (len == 0) return OZEC_OK;
   if (!data || !out) return fail(OZEC_EINVAL, "null buffer");
+  ozec::DeviceScope ds(ozec::thread_device());  // coder-less host call: this thread's GPU (devices.hpp)
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
   uint8_t *outs[1] = {reinterpret_cast<uint8_t *>(out)};
@@ -1027,11 +1070,11 @@ int ozec_encode_crc_block_groups(ozec_coder *enc, uint8_t *d_base, int64_t group
 
 // ---- end-to-end batch from host memory ----------------------------------------
 
-int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_stripe_stride,
-                               int64_t in_unit_stride, uint8_t *h_out, int64_t out_stripe_stride,
-                               int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
-                               size_t bpc, uint32_t *h_crcs, int big_endian, size_t stripes_per_chunk) {
-  ozec::StatScope stat_(OZEC_OP_HOST_BATCH, enc ? static_cast<uint64_t>(enc->k) * len * num_stripes : 0);
+// one device's share of a host batch, on the calling thread's current device (host_batch_split)
+static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64_t in_stripe_stride,
+                                     int64_t in_unit_stride, uint8_t *h_out, int64_t out_stripe_stride,
+                                     int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
+                                     size_t bpc, uint32_t *h_crcs, int big_endian, size_t stripes_per_chunk) {
   if (int rc = check_open(enc, "encode")) return rc;
   if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
   if (len == 0 || num_stripes == 0) return OZEC_OK;
@@ -1336,13 +1379,13 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
 // ozec_encode_crc_host_batch (ring of E2E::NB device chunk buffers, H2D / kernel / D2H on three streams, the host
 // waiting for a buffer's previous chunk before refilling it) around ozec_reconstruct_crc_batch.  Only the k units the
 // decoder reads cross PCIe, as one rectangular copy per run of consecutive unit indexes per chunk.
-int ozec_reconstruct_crc_host_batch(ozec_coder *dec, const uint8_t *h_in, int64_t in_stripe_stride,
-                                    int64_t in_unit_stride, const int *present_units, int num_present, const int *erased,
-                                    int n_erased, uint8_t *h_out, int64_t out_stripe_stride, int64_t out_unit_stride,
-                                    size_t num_stripes, size_t len, int checksum_type, size_t bpc,
-                                    const uint32_t *h_expected, int expected_big_endian, uint32_t *h_out_crcs,
-                                    int out_big_endian, int32_t *h_mismatch, size_t stripes_per_chunk) {
-  ozec::StatScope stat_(OZEC_OP_HOST_BATCH, dec ? static_cast<uint64_t>(dec->k) * len * num_stripes : 0);
+static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, int64_t in_stripe_stride,
+                                          int64_t in_unit_stride, const int *present_units, int num_present,
+                                          const int *erased, int n_erased, uint8_t *h_out, int64_t out_stripe_stride,
+                                          int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
+                                          size_t bpc, const uint32_t *h_expected, int expected_big_endian,
+                                          uint32_t *h_out_crcs, int out_big_endian, int32_t *h_mismatch,
+                                          size_t stripes_per_chunk) {
   if (int rc = check_open(dec, "decode")) return rc;
   if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
   const int n_all = dec->k + dec->p;
@@ -1538,6 +1581,111 @@ int ozec_reconstruct_crc_host_batch(ozec_coder *dec, const uint8_t *h_in, int64_
   if (!h_expected && h_mismatch)
     for (size_t s = 0; s < num_stripes; ++s) h_mismatch[s] = -1;
   return OZEC_OK;
+}
+
+// A host batch split over the device list (devices.hpp): contiguous stripe ranges, part i = stripe_range(S, i, n),
+// each run by the single-device pipeline on its own GPU, all at once (part 0 on the calling thread, the others on
+// threads of their own).  The coder's GPU takes part 0; a batch too small for one pipeline chunk per GPU stays on it.
+// No data crosses between GPUs (north_star: "a batch is partitioned across the 8 MI355X of one node as per-GPU
+// streams with no RCCL collectives").  fn(s0, s1) runs with its part's device current.
+}  // extern "C"
+
+template <class Fn>
+static int host_batch_split(const ozec_coder *c, size_t num_stripes, size_t chunk, Fn fn) {
+  std::vector<int> devs = ozec::device_list();
+  if (devs.empty()) return fail(OZEC_EDEVICE, "no HIP device available");
+  auto it = std::find(devs.begin(), devs.end(), c->device);
+  if (it != devs.end()) std::rotate(devs.begin(), it, devs.end());
+  else devs.insert(devs.begin(), c->device);  // a coder made before ozec_set_devices dropped its GPU
+  const size_t parts = std::min(devs.size(), std::max<size_t>(1, num_stripes / std::max<size_t>(1, chunk)));
+  auto range = [&](size_t i, size_t *s0, size_t *s1) {  // ozone_amd/shard.py stripe_range
+    const size_t per = (num_stripes + parts - 1) / parts;
+    *s0 = std::min(num_stripes, i * per);
+    *s1 = std::min(num_stripes, (i + 1) * per);
+  };
+  if (parts == 1) {
+    ozec::DeviceScope ds(devs[0]);
+    if (!ds.ok()) return fail(OZEC_EDEVICE, "cannot select device " + std::to_string(devs[0]));
+    return fn(size_t{0}, num_stripes);
+  }
+  std::vector<int> rcs(parts, OZEC_OK);
+  std::vector<std::string> msgs(parts);
+  auto run = [&](size_t i) {
+    size_t s0, s1;
+    range(i, &s0, &s1);
+    if (s0 >= s1) return;
+    ozec::DeviceScope ds(devs[i]);
+    if (!ds.ok()) {
+      rcs[i] = OZEC_EDEVICE;
+      msgs[i] = "cannot select device " + std::to_string(devs[i]);
+      return;
+    }
+    rcs[i] = fn(s0, s1);
+    if (rcs[i]) msgs[i] = g_error;
+  };
+  std::vector<std::thread> workers;
+  for (size_t i = 1; i < parts; ++i)
+    workers.emplace_back([&, i] {
+      ozec::g_stat_depth = 1;  // the caller's call is the one counted (stats.hpp)
+      run(i);
+    });
+  run(0);
+  for (auto &w : workers) w.join();
+  for (size_t i = 0; i < parts; ++i)
+    if (rcs[i]) return fail(rcs[i], "device " + std::to_string(devs[i]) + ": " + msgs[i]);
+  return OZEC_OK;
+}
+
+extern "C" {
+
+static size_t e2e_chunk_of(size_t stripes_per_chunk) {
+  return stripes_per_chunk ? stripes_per_chunk : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk.load()));
+}
+
+int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_stripe_stride,
+                               int64_t in_unit_stride, uint8_t *h_out, int64_t out_stripe_stride,
+                               int64_t out_unit_stride, size_t num_stripes, size_t len, int checksum_type,
+                               size_t bpc, uint32_t *h_crcs, int big_endian, size_t stripes_per_chunk) {
+  ozec::StatScope stat_(OZEC_OP_HOST_BATCH, enc ? static_cast<uint64_t>(enc->k) * len * num_stripes : 0);
+  if (int rc = check_open(enc, "encode")) return rc;
+  if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
+  if (len == 0 || num_stripes == 0) return OZEC_OK;
+  const bool with_crc = checksum_type != OZEC_CHECKSUM_NONE;
+  if (!h_in || !h_out || (with_crc && !h_crcs)) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
+  const size_t ncrc = with_crc && bpc ? static_cast<size_t>(enc->k + out_rows(enc)) * ((len + bpc - 1) / bpc) : 0;
+  return host_batch_split(enc, num_stripes, e2e_chunk_of(stripes_per_chunk), [&](size_t s0, size_t s1) {
+    return encode_crc_host_batch_dev(enc, h_in + s0 * in_stripe_stride, in_stripe_stride, in_unit_stride,
+                                     h_out + s0 * out_stripe_stride, out_stripe_stride, out_unit_stride, s1 - s0, len,
+                                     checksum_type, bpc, with_crc ? h_crcs + s0 * ncrc : nullptr, big_endian,
+                                     stripes_per_chunk);
+  });
+}
+
+int ozec_reconstruct_crc_host_batch(ozec_coder *dec, const uint8_t *h_in, int64_t in_stripe_stride,
+                                    int64_t in_unit_stride, const int *present_units, int num_present, const int *erased,
+                                    int n_erased, uint8_t *h_out, int64_t out_stripe_stride, int64_t out_unit_stride,
+                                    size_t num_stripes, size_t len, int checksum_type, size_t bpc,
+                                    const uint32_t *h_expected, int expected_big_endian, uint32_t *h_out_crcs,
+                                    int out_big_endian, int32_t *h_mismatch, size_t stripes_per_chunk) {
+  ozec::StatScope stat_(OZEC_OP_HOST_BATCH, dec ? static_cast<uint64_t>(dec->k) * len * num_stripes : 0);
+  if (int rc = check_open(dec, "decode")) return rc;
+  if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
+  // argument errors (reported in the single-device path's order) and empty batches: no split
+  if (num_stripes == 0 || len == 0 || bpc == 0 || n_erased < 0 || !h_in || (n_erased && (!h_out || !h_out_crcs)) ||
+      (h_expected && !h_mismatch))
+    return reconstruct_crc_host_batch_dev(dec, h_in, in_stripe_stride, in_unit_stride, present_units, num_present,
+                                          erased, n_erased, h_out, out_stripe_stride, out_unit_stride, num_stripes, len,
+                                          checksum_type, bpc, h_expected, expected_big_endian, h_out_crcs,
+                                          out_big_endian, h_mismatch, stripes_per_chunk);
+  const size_t nwin = (len + bpc - 1) / bpc, n_all = static_cast<size_t>(dec->k + dec->p);
+  return host_batch_split(dec, num_stripes, e2e_chunk_of(stripes_per_chunk), [&](size_t s0, size_t s1) {
+    return reconstruct_crc_host_batch_dev(
+        dec, h_in + s0 * in_stripe_stride, in_stripe_stride, in_unit_stride, present_units, num_present, erased,
+        n_erased, h_out ? h_out + s0 * out_stripe_stride : nullptr, out_stripe_stride, out_unit_stride, s1 - s0, len,
+        checksum_type, bpc, h_expected ? h_expected + s0 * n_all * nwin : nullptr, expected_big_endian,
+        h_out_crcs ? h_out_crcs + s0 * static_cast<size_t>(n_erased) * nwin : nullptr, out_big_endian,
+        h_mismatch ? h_mismatch + s0 : nullptr, stripes_per_chunk);
+  });
 }
 
 // ---- host-side math ----------------------------------------------------------------------------

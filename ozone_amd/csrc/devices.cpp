@@ -1,0 +1,169 @@
+#include "devices.hpp"
+
+#include <hip/hip_runtime.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/ozec.h"
+#include "numa.hpp"
+
+namespace ozec {
+namespace {
+
+std::mutex g_mu;
+bool g_init = false;
+std::vector<int> g_list;             // guarded by g_mu
+std::atomic<int> g_policy{-1};       // -1: read OZEC_DEVICE_POLICY on first use
+std::atomic<unsigned> g_next{0};     // round-robin cursor of pick_device
+std::atomic<unsigned> g_thread_next{0};
+std::atomic<unsigned> g_gen{1};          // bumped by set_device_list (threads re-pick their device)
+
+int visible() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+// OZEC_DEVICES: "all" / unset = every visible device, else a comma list of ordinals (invalid entries are skipped)
+std::vector<int> default_list(int n) {
+  std::vector<int> out;
+  const char *e = std::getenv("OZEC_DEVICES");
+  if (e && *e && std::strcmp(e, "all") != 0) {
+    std::string s(e);
+    size_t pos = 0;
+    while (pos <= s.size()) {
+      size_t c = s.find(',', pos);
+      if (c == std::string::npos) c = s.size();
+      const std::string tok = s.substr(pos, c - pos);
+      char *end = nullptr;
+      const long v = std::strtol(tok.c_str(), &end, 10);
+      if (!tok.empty() && end && *end == '\0' && v >= 0 && v < n) out.push_back(static_cast<int>(v));
+      pos = c + 1;
+    }
+  }
+  if (out.empty())
+    for (int d = 0; d < n; ++d) out.push_back(d);
+  return out;
+}
+
+void ensure_init() {  // caller holds g_mu
+  if (g_init) return;
+  g_list = default_list(visible());
+  g_init = true;
+}
+
+int caller_node() {
+  unsigned cpu = 0, node = 0;
+  if (syscall(SYS_getcpu, &cpu, &node, nullptr) != 0) return -1;
+  return static_cast<int>(node);
+}
+
+}  // namespace
+
+std::vector<int> device_list() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  ensure_init();
+  return g_list;
+}
+
+int set_device_list(const int *devs, int n) {
+  const int vis = visible();
+  if (n < 0 || (n > 0 && !devs)) return OZEC_EINVAL;
+  for (int i = 0; i < n; ++i)
+    if (devs[i] < 0 || devs[i] >= vis) return OZEC_EDEVICE;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_list = n > 0 ? std::vector<int>(devs, devs + n) : default_list(vis);
+  g_init = true;
+  g_gen.fetch_add(1, std::memory_order_release);
+  return OZEC_OK;
+}
+
+int device_policy() {
+  int p = g_policy.load(std::memory_order_relaxed);
+  if (p < 0) {
+    const char *e = std::getenv("OZEC_DEVICE_POLICY");
+    p = e && !std::strcmp(e, "numa") ? 1 : e && !std::strcmp(e, "current") ? 2 : 0;
+    g_policy.store(p, std::memory_order_relaxed);
+  }
+  return p;
+}
+
+int set_device_policy(int policy) {
+  if (policy < 0 || policy > 2) return OZEC_EINVAL;
+  g_policy.store(policy, std::memory_order_relaxed);
+  return OZEC_OK;
+}
+
+int pick_device() {
+  const int policy = device_policy();
+  if (policy == 2) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+      (void)hipGetLastError();
+      return -1;
+    }
+    return dev;
+  }
+  const std::vector<int> list = device_list();
+  if (list.empty()) return -1;
+  if (policy == 1) {  // the listed GPUs on the caller's NUMA node, round robin; all of them when none is
+    const int node = caller_node();
+    std::vector<int> near;
+    for (int d : list)
+      if (node >= 0 && device_numa_node(d) == node) near.push_back(d);
+    if (!near.empty()) return near[g_next.fetch_add(1, std::memory_order_relaxed) % near.size()];
+  }
+  return list[g_next.fetch_add(1, std::memory_order_relaxed) % list.size()];
+}
+
+int thread_device() {
+  if (device_policy() == 2) {  // follows the thread's current device, call by call
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) {
+      (void)hipGetLastError();
+      return -1;
+    }
+    return d;
+  }
+  thread_local int dev = -1;
+  thread_local unsigned gen = 0;
+  const unsigned now = g_gen.load(std::memory_order_acquire);
+  if (dev < 0 || gen != now) {  // first call, or the list changed since this thread was given its device
+    const std::vector<int> list = device_list();
+    if (list.empty()) return -1;
+    dev = list[g_thread_next.fetch_add(1, std::memory_order_relaxed) % list.size()];
+    gen = now;
+  }
+  return dev;
+}
+
+DeviceScope::DeviceScope(int dev) {
+  if (dev < 0) return;
+  if (hipGetDevice(&prev_) != hipSuccess) {
+    (void)hipGetLastError();
+    ok_ = false;
+    return;
+  }
+  if (prev_ == dev) return;
+  if (hipSetDevice(dev) != hipSuccess) {
+    (void)hipGetLastError();
+    ok_ = false;
+    return;
+  }
+  switched_ = true;
+}
+
+DeviceScope::~DeviceScope() {
+  if (switched_) (void)hipSetDevice(prev_);
+}
+
+}  // namespace ozec

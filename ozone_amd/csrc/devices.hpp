@@ -1,0 +1,46 @@
+// Which GPUs one drop-in process uses, and which one each coder and host call runs on.
+//
+// Ozone runs one JVM per datanode or client, not one process per GPU: every ECKeyOutputStream makes its own coder
+// (ECKeyOutputStream.java:117), every reconstruction its own decoder (ECBlockReconstructedStripeInputStream.java:232).
+// So the library, not the caller, spreads the work over the node's GPUs (SURVEY §7 "lazy singleton per GPU", §8(b)
+// process-global per-GPU context, north_star: "a batch is partitioned across the 8 MI355X of one node as per-GPU
+// streams"):
+//   * the device list: every visible GPU, or OZEC_DEVICES ("0,2,3", "all"), or ozec_set_devices;
+//   * a coder is bound to one device of the list when it is made (policy OZEC_DEVICE_POLICY: round_robin, the default;
+//     numa -- round robin over the listed GPUs closest to the creating thread's NUMA node; current -- the creating
+//     thread's current device, the one-process-per-GPU model); its host-buffer calls and stripe queues run there;
+//   * a host batch (ozec_encode_crc_host_batch / ozec_reconstruct_crc_host_batch) is split into contiguous stripe
+//     ranges over the whole list, one pipeline per GPU, run at once;
+//   * coder-less host calls (CRC of a host buffer) run on a device the calling thread is given on first use;
+//   * device-pointer entry points run on the caller's current device (the one its pointers and stream belong to).
+#pragma once
+#include <vector>
+
+namespace ozec {
+
+// the device list (never empty when a GPU exists; empty when none does)
+std::vector<int> device_list();
+// replace the list (ordinals must exist; duplicates allowed -- [0, 0] splits a batch in two on one GPU); n = 0
+// restores the default.  Returns 0 or a negative OZEC_* status.
+int set_device_list(const int *devs, int n);
+// the device a new coder is bound to, by the policy
+int pick_device();
+// the device of this thread's coder-less host calls
+int thread_device();
+// 0 round_robin, 1 numa, 2 current
+int device_policy();
+int set_device_policy(int policy);
+
+// switch the calling thread to `dev` for the scope (restored on exit); ok() false when the switch failed
+class DeviceScope {
+ public:
+  explicit DeviceScope(int dev);
+  ~DeviceScope();
+  bool ok() const { return ok_; }
+
+ private:
+  int prev_ = -1;
+  bool switched_ = false, ok_ = true;
+};
+
+}  // namespace ozec

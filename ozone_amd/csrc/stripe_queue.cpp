@@ -24,6 +24,7 @@
 
 #include "../../include/ozec.h"
 #include "copy_pool.hpp"
+#include "devices.hpp"
 #include "kernels.hpp"
 #include "numa.hpp"
 #include "stats.hpp"
@@ -238,8 +239,8 @@ int ozec_host_alloc_on(size_t bytes, int device, void **out) {
 }
 
 int ozec_host_alloc(size_t bytes, void **out) {
-  int dev = 0;
-  SQ_HIP(hipGetDevice(&dev));
+  const int dev = ozec::thread_device();  // this thread's GPU (devices.hpp; policy "current": its current device)
+  if (dev < 0) return set_error(OZEC_EDEVICE, "no HIP device available");
   return ozec_host_alloc_on(bytes, dev, out);
 }
 
@@ -306,9 +307,12 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
   // frees it first (the queue's launches then fail with OZEC_ECLOSED)
   (void)ozec_coder_retain(enc);
   q->enc = enc;
-  if (hipGetDevice(&q->device) != hipSuccess) {
+  q->device = ozec_coder_device(enc);  // the encoder's GPU (devices.hpp)
+  ozec::DeviceScope ds(q->device);
+  if (!ds.ok()) {
+    ozec_coder_free(enc);
     delete q;
-    return set_error(OZEC_EDEVICE, "no current device");
+    return set_error(OZEC_EDEVICE, "cannot select device " + std::to_string(q->device));
   }
   q->k = k;
   q->p = p;
@@ -355,6 +359,7 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
   if (len == 0 || len > q->cell_len)
     return set_error(OZEC_EINVAL, "stripe length must be in [1, cell_len] (" + std::to_string(q->cell_len) + ")");
   if (ozec_coder_is_closed(q->enc)) return set_error(OZEC_ECLOSED, "stripe queue submit failed: the encoder is closed");
+  ozec::DeviceScope ds(q->device);
   std::lock_guard<std::mutex> lk(q->mu);
   Batch *b = &q->batches[q->cur];
   // cur only ever points at a filling batch or, once the ring has wrapped, at the oldest in-flight one: that one
@@ -412,6 +417,7 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
 int ozec_stripe_queue_flush(ozec_stripe_queue *q) {
   ozec::StatScope stat_(OZEC_OP_QUEUE, 0);
   if (!q) return set_error(OZEC_EINVAL, "null queue");
+  ozec::DeviceScope ds(q->device);
   std::lock_guard<std::mutex> lk(q->mu);
   Batch &b = q->batches[q->cur];
   if (b.n > 0 && !b.in_flight) {
@@ -424,6 +430,7 @@ int ozec_stripe_queue_flush(ozec_stripe_queue *q) {
 int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket) {
   ozec::StatScope stat_(OZEC_OP_QUEUE, 0);
   if (!q) return set_error(OZEC_EINVAL, "null queue");
+  ozec::DeviceScope ds(q->device);
   std::lock_guard<std::mutex> lk(q->mu);
   if (ticket >= q->next_ticket) return set_error(OZEC_EINVAL, "unknown ticket " + std::to_string(ticket));
   // complete, oldest first, every batch holding a stripe <= ticket (launching the filling one if needed)
@@ -474,6 +481,7 @@ int ozec_stripe_queue_state(ozec_stripe_queue *q, size_t *in_flight, uint64_t *o
 
 int ozec_stripe_queue_free(ozec_stripe_queue *q) {
   if (!q) return OZEC_OK;
+  ozec::DeviceScope ds(q->device);
   int rc = OZEC_OK;
   // Stripes submitted but never waited for are completed here, oldest first: a filling batch is launched and
   // every batch's parity / CRCs land in the callers' buffers before they are released (ozec.h: the buffers

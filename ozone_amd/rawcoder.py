@@ -198,6 +198,11 @@ class _Coder:
         """Idempotent; later encode/decode raise IOException("... closed") (TestRawCoderBase.java:118-150)."""
         L.lib().ozec_coder_release(self._handle)
 
+    @property
+    def device(self):
+        """The GPU this coder's host-buffer calls and stripe queues run on (chosen at creation: set_devices)."""
+        return int(L.lib().ozec_coder_device(self._handle))
+
 
 # ---------------------------------------------------------------- encoder --------------------------------
 
@@ -654,6 +659,32 @@ def gf_mul(a, b):
 
 def device_count():
     return int(L.lib().ozec_device_count())
+
+
+DEVICE_POLICY = {"round_robin": 0, "numa": 1, "current": 2}
+
+
+def set_devices(devices=None):
+    """The GPUs this process's coders and host batches use (ozec_set_devices): None / [] restores every visible GPU
+    (or OZEC_DEVICES).  Coders created afterwards take them in turn; host batches split over all of them."""
+    devs = list(devices or [])
+    arr = (ctypes.c_int * max(1, len(devs)))(*devs)
+    rc = L.lib().ozec_set_devices(arr, len(devs))
+    if rc != L.OZEC_OK:
+        _raise_for(rc)
+
+
+def get_devices():
+    n = L.lib().ozec_get_devices(None, 0)
+    arr = (ctypes.c_int * max(1, n))()
+    L.lib().ozec_get_devices(arr, n)
+    return list(arr)[:n]
+
+
+def set_device_policy(policy):
+    rc = L.lib().ozec_set_device_policy(DEVICE_POLICY[policy] if isinstance(policy, str) else int(policy))
+    if rc != L.OZEC_OK:
+        _raise_for(rc)
 
 
 def fill_splitmix64_cells(d_base, cell_stride, num_cells, length, seed, first_stream, stream=None):

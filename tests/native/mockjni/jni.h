@@ -45,5 +45,9 @@ struct JNINativeInterface_ {
   jobject (*NewDirectByteBuffer)(JNIEnv *, void *, jlong);
   void *(*GetDirectBufferAddress)(JNIEnv *, jobject);
   jlong (*GetDirectBufferCapacity)(JNIEnv *, jobject);
+  void (*GetByteArrayRegion)(JNIEnv *, jbyteArray, jsize, jsize, jbyte *);
+  void (*SetByteArrayRegion)(JNIEnv *, jbyteArray, jsize, jsize, const jbyte *);
+  jintArray (*NewIntArray)(JNIEnv *, jsize);
+  void (*SetIntArrayRegion)(JNIEnv *, jintArray, jsize, jsize, const jint *);
 };
 #endif

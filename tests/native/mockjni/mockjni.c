@@ -18,6 +18,7 @@ struct mock_object {
   int64_t len;
   struct mock_object **elems;
   char name[96];
+  int owns;  /* data allocated by the mock (NewIntArray) */
 };
 
 static int g_pins, g_local_refs;
@@ -108,10 +109,53 @@ static jlong direct_capacity(JNIEnv *env, jobject o) {
   return o && o->kind == K_DIRECT ? o->len : -1;
 }
 
+/* Get/SetByteArrayRegion: the JVM's bounds check (ArrayIndexOutOfBoundsException pending, nothing copied) */
+static int region_ok(jarray a, jsize start, jsize n) {
+  if (a->kind == K_BYTES && start >= 0 && n >= 0 && (int64_t)start + n <= a->len) return 1;
+  snprintf(g_exc_class, sizeof g_exc_class, "java/lang/ArrayIndexOutOfBoundsException");
+  snprintf(g_exc_msg, sizeof g_exc_msg, "Array region %d..%lld out of bounds for length %lld", start,
+           (long long)start + n, (long long)a->len);
+  g_exc_pending = 1;
+  return 0;
+}
+
+static int g_region_copies;
+
+static void get_byte_region(JNIEnv *env, jbyteArray a, jsize start, jsize n, jbyte *buf) {
+  (void)env;
+  if (!region_ok(a, start, n)) return;
+  memcpy(buf, (jbyte *)a->data + start, (size_t)n);
+  ++g_region_copies;
+}
+
+static void set_byte_region(JNIEnv *env, jbyteArray a, jsize start, jsize n, const jbyte *buf) {
+  (void)env;
+  if (!region_ok(a, start, n)) return;
+  memcpy((jbyte *)a->data + start, buf, (size_t)n);
+  ++g_region_copies;
+}
+
+/* a new int[] owns its memory (freed with mock_free) */
+static jintArray new_int_array(JNIEnv *env, jsize n) {
+  (void)env;
+  struct mock_object *o = calloc(1, sizeof *o);
+  o->kind = K_INTS;
+  o->data = calloc((size_t)(n ? n : 1), sizeof(jint));
+  o->len = n;
+  o->owns = 1;  /* handed to the Java caller: not a local reference the glue must delete */
+  return o;
+}
+
+static void set_int_region(JNIEnv *env, jintArray a, jsize start, jsize n, const jint *buf) {
+  (void)env;
+  memcpy((jint *)a->data + start, buf, sizeof(jint) * (size_t)n);
+}
+
 static const struct JNINativeInterface_ g_table = {
     find_class,           throw_new,      exception_clear,       delete_local_ref, array_length,
     object_array_element, int_array_region, array_critical,      release_array_critical,
-    new_direct,           direct_address, direct_capacity,
+    new_direct,           direct_address, direct_capacity,       get_byte_region,  set_byte_region,
+    new_int_array,        set_int_region,
 };
 static JNIEnv g_env = &g_table;
 
@@ -145,10 +189,46 @@ int64_t mock_len(struct mock_object *o) { return o ? o->len : -1; }
 void mock_free(struct mock_object *o) {
   if (!o) return;
   free(o->elems);
+  if (o->owns) free(o->data);
   free(o);
 }
 
 int mock_pins(void) { return g_pins; }
+int mock_region_copies(void) { return g_region_copies; }
+
+/* libozec entry points that do device work, wrapped at link time (-Wl,--wrap=...): the most array pins outstanding
+ * when the glue called any of them -- VERDICT r3: heap arrays must not stay pinned across device work */
+static int g_pins_at_device_call = 0, g_device_calls = 0;
+static void at_device_call(void) {
+  ++g_device_calls;
+  if (g_pins > g_pins_at_device_call) g_pins_at_device_call = g_pins;
+}
+int mock_pins_at_device_call(void) { return g_pins_at_device_call; }
+int mock_device_calls(void) { return g_device_calls; }
+void mock_reset_device_calls(void) { g_pins_at_device_call = g_device_calls = 0; }
+
+#include "../../../include/ozec.h"
+int __real_ozec_encode(ozec_coder *, const uint8_t *const *, uint8_t *const *, size_t);
+int __wrap_ozec_encode(ozec_coder *c, const uint8_t *const *in, uint8_t *const *out, size_t len) {
+  at_device_call();
+  return __real_ozec_encode(c, in, out, len);
+}
+int __real_ozec_decode(ozec_coder *, const uint8_t *const *, const int *, int, uint8_t *const *, size_t);
+int __wrap_ozec_decode(ozec_coder *c, const uint8_t *const *in, const int *e, int ne, uint8_t *const *out,
+                       size_t len) {
+  at_device_call();
+  return __real_ozec_decode(c, in, e, ne, out, len);
+}
+int __real_ozec_crc_update(int, uint32_t *, const uint8_t *, size_t);
+int __wrap_ozec_crc_update(int t, uint32_t *s, const uint8_t *d, size_t len) {
+  at_device_call();
+  return __real_ozec_crc_update(t, s, d, len);
+}
+int __real_ozec_checksum_windows(int, const uint8_t *, size_t, size_t, uint32_t *, int);
+int __wrap_ozec_checksum_windows(int t, const uint8_t *d, size_t len, size_t bpc, uint32_t *out, int be) {
+  at_device_call();
+  return __real_ozec_checksum_windows(t, d, len, bpc, out, be);
+}
 int mock_local_refs(void) { return g_local_refs; }
 void mock_set_missing_class(const char *name) { snprintf(g_missing, sizeof g_missing, "%s", name ? name : ""); }
 

@@ -1,0 +1,36 @@
+"""The device list and device policies of one drop-in process (ozone_amd/csrc/devices.cpp) on the
+CPU: devices.cpp compiled against a fake HIP runtime of four devices on two NUMA nodes (tests/native/
+devices_policy.cpp) -- default list, OZEC_DEVICES, duplicates, bad ordinals, round robin, NUMA-first, "current",
+per-thread devices re-picked after a list change, DeviceScope restoring the caller's device."""
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def binary():
+    d = tempfile.mkdtemp(prefix="ozec_devices_")
+    exe = os.path.join(d, "devices_policy")
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                        "-I", ROOT, os.path.join(ROOT, "tests", "native", "devices_policy.cpp"),
+                        os.path.join(ROOT, "ozone_amd", "csrc", "devices.cpp"), "-o", exe, "-lpthread"],
+                       capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        pytest.fail(r.stderr[-2000:])
+    return exe
+
+
+@pytest.mark.parametrize("env", [None, "3,x,1,9"])
+def test_device_policies(binary, env):
+    e = dict(os.environ)
+    e.pop("OZEC_DEVICES", None)
+    e.pop("OZEC_DEVICE_POLICY", None)
+    if env:
+        e["OZEC_DEVICES"] = env
+    r = subprocess.run([binary], capture_output=True, text=True, timeout=60, env=e)
+    assert r.returncode == 0, r.stderr
+    assert "devices policy OK" in r.stdout

@@ -354,3 +354,77 @@ def test_per_call_counters_on_the_gpu_paths():
     # the e2e batch counts once, as a host batch, not again for the fused launches it makes
     assert st["host_batch"]["calls"] == 1 and st["host_batch"]["bytes"] == S * k * n
     assert st["fused"]["calls"] == 0
+
+
+# ------------------------------------------------------------------------------ several GPUs in one process (N2)
+
+
+@pytest.fixture
+def device_list():
+    """ozec_set_devices for the test, the default list restored afterwards."""
+    yield rc.set_devices
+    rc.set_devices(None)
+
+
+@pytest.mark.parametrize("devs", [[0, 0], [0, 0, 0]])
+def test_host_batches_split_over_the_device_list(device_list, devs):
+    """one process drives every GPU of its list.  On the one-GPU box the list [0, 0] ([0, 0, 0])
+    stands for two (three) GPUs: a host batch is cut into that many stripe ranges, each run by its own pipeline thread
+    on its listed device, and the union equals the oracle -- encode + CRC (pinned and pageable) and the fused
+    reconstruction with a corrupted window reported for its own stripe.  Coders take the listed devices in turn."""
+    device_list(devs)
+    assert rc.get_devices() == devs
+    e = rc.RawErasureEncoder(rc.ECReplicationConfig(6, 3))
+    assert e.device == 0
+    k, p, n, S, chunk, bpc = 6, 3, 1 << 16, 23, 4, 16384
+    for pinned in (True, False):
+        buf, v, us = _batch(S, k, p, n, 890000 + 100 * len(devs) + pinned)
+        crcs = np.zeros(S * (k + p) * (n // bpc), np.uint32)
+        keep = []
+        if pinned:
+            pb, pc = host_alloc(buf.nbytes), host_alloc(crcs.nbytes)
+            pb.array[:] = buf
+            keep += [pb, pc]
+            v, crcs = pb.array.reshape(S, k + p, us), pc.array.view(np.uint32)
+        base = v.ctypes.data
+        e.encode_crc_host_batch(base, (k + p) * us, us, base + k * us, (k + p) * us, us, S, n, ck.ChecksumType.CRC32C,
+                                bpc, crcs, False, chunk)
+        _check(v, crcs, "rs", k, p, n, S, ck.ChecksumType.CRC32C, bpc)
+    # reconstruction, split the same way
+    k, p, erased = 10, 4, [1, 4, 10, 13]
+    buf, v, us = _recon_batch("rs", k, p, n, S, 895000, 0)
+    nwin = n // bpc
+    stored = np.stack([np.stack([oracle.crc_windows(oracle.CRC32C, np.array(v[s, u, :n]), bpc) for u in range(k + p)])
+                       for s in range(S)]).astype(np.uint32).reshape(-1)
+    present = [u for u in range(k + p) if u not in erased]
+    orig = np.array(v[:, :, :n])
+    bad = S - 2  # a stripe of the last part
+    v[bad, present[0], 7] ^= 0x40
+    out = np.zeros(S * 4 * n, np.uint8)
+    ocrc = np.zeros(S * 4 * nwin, np.uint32)
+    mism = np.zeros(S, np.int32)
+    dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
+    dec.reconstruct_crc_host_batch(v.reshape(-1), (k + p) * us, us, present, erased, out, 4 * n, n, S, n,
+                                   ck.ChecksumType.CRC32C, bpc, ocrc, h_expected=stored, h_mismatch=mism,
+                                   stripes_per_chunk=chunk)
+    assert mism[bad] == present[0] * nwin and all(mism[s] == -1 for s in range(S) if s != bad), list(mism)
+    got, oc, st = out.reshape(S, 4, n), ocrc.reshape(S, 4, nwin), stored.reshape(S, k + p, nwin)
+    for s in range(S):
+        if s == bad:
+            continue
+        for i, u in enumerate(erased):
+            assert (got[s, i] == orig[s, u]).all() and (oc[s, i] == st[s, u]).all(), (s, u)
+
+
+def test_device_list_errors_and_default(device_list):
+    n = rc.device_count()
+    with pytest.raises(RuntimeError):  # no such device (OZEC_EDEVICE)
+        rc.set_devices([n])
+    device_list([0])
+    assert rc.get_devices() == [0]
+    rc.set_devices(None)
+    assert rc.get_devices() == list(range(n)) or os.environ.get("OZEC_DEVICES")
+    for name in ("round_robin", "numa", "current"):
+        rc.set_device_policy(name)
+        assert rc.RawErasureEncoder(rc.ECReplicationConfig(3, 2)).device in range(n)
+    rc.set_device_policy("round_robin")

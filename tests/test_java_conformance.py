@@ -321,7 +321,7 @@ def test_every_native_has_its_jni_entry():
     assert set(natives) == set(entries), (set(natives) ^ set(entries))
     jtype = {"int": "jint", "long": "jlong", "boolean": "jboolean", "byte[]": "jbyteArray", "int[]": "jintArray",
              "ByteBuffer": "jobject", "ByteBuffer[]": "jobjectArray", "byte[][]": "jobjectArray"}
-    jret = {"int": "jint", "long": "jlong", "void": "void", "ByteBuffer": "jobject"}
+    jret = {"int": "jint", "long": "jlong", "void": "void", "ByteBuffer": "jobject", "int[]": "jintArray"}
     for name, m in natives.items():
         params = entries[name]
         assert params[0].startswith("JNIEnv") and params[1].startswith("jclass"), name

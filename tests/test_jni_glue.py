@@ -29,6 +29,8 @@ def J():
                     "-I", os.path.join(ROOT, "tests", "native", "mockjni"), "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "jni", "ozec_jni.c"), os.path.join(ROOT, "jni", "ozec_marshal.c"),
                     os.path.join(ROOT, "tests", "native", "mockjni", "mockjni.c"), "-L", LIBDIR, "-lozec",
+                    # device-work entry points wrapped by the mock (pins outstanding at each call)
+                    "-Wl,--wrap=ozec_encode,--wrap=ozec_decode,--wrap=ozec_crc_update,--wrap=ozec_checksum_windows",
                     f"-Wl,-rpath,{LIBDIR}", "-o", so], check=True, capture_output=True, timeout=120)
     L = ctypes.CDLL(so)
     for name, res, args in [
@@ -36,9 +38,13 @@ def J():
         ("mock_bytes", vp, [vp, i64]), ("mock_ints", vp, [vp, i64]), ("mock_objects", vp, [i64]),
         ("mock_set", None, [vp, i64, vp]), ("mock_data", vp, [vp]), ("mock_len", i64, [vp]), ("mock_free", None, [vp]),
         ("mock_pins", ctypes.c_int, []), ("mock_local_refs", ctypes.c_int, []),
+        ("mock_pins_at_device_call", ctypes.c_int, []), ("mock_device_calls", ctypes.c_int, []),
+        ("mock_reset_device_calls", None, []), ("mock_region_copies", ctypes.c_int, []),
         ("mock_set_missing_class", None, [ctypes.c_char_p]),
         ("mock_take_exception", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
         (P + "deviceCount", i32, [vp, vp]),
+        (P + "setDevices", None, [vp, vp, vp]), (P + "getDevices", vp, [vp, vp]),
+        (P + "setDevicePolicy", None, [vp, vp, i32]), (P + "coderDevice", i32, [vp, vp, i64]),
         (P + "coderCreate", i64, [vp, vp, ctypes.c_uint8, i32, i32, i32]),
         (P + "coderRelease", None, [vp, vp, i64]),
         (P + "encodeDirect", None, [vp, vp, i64, vp, vp, i32, vp, vp]),
@@ -357,6 +363,83 @@ def test_checksums_and_streaming_update_vs_oracle(J, java):
         state = call(J, fn, 3, state, java.bytes(data) if lo == 0 else java.direct(data), lo, hi - lo)
     assert java.exception() is None
     assert (~state) & 0xFFFFFFFF == oracle.crc_windows(oracle.CRC32C, data, n + 5)[0]
+
+
+@pytest.mark.gpu
+def test_device_list_natives(J, java):
+    """OzecNative.setDevices / getDevices / setDevicePolicy / coderDevice (ozone.ec.hip.devices): a list of the one
+    GPU twice, coders bound to it, a bad ordinal refused with the device exception, the default restored."""
+    call(J, "setDevices", java.ints([0, 0]))
+    assert java.exception() is None
+    arr = call(J, "getDevices")
+    assert J.mock_len(arr) == 2 and list(np.ctypeslib.as_array(ctypes.cast(J.mock_data(arr), ctypes.POINTER(
+        ctypes.c_int32)), (2,))) == [0, 0]
+    J.mock_free(arr)
+    h = call(J, "coderCreate", 0, 0, 6, 3)
+    assert call(J, "coderDevice", h) == 0
+    call(J, "coderRelease", h)
+    call(J, "setDevices", java.ints([99]))
+    assert java.exception()[0] == "java/io/IOException"
+    call(J, "setDevicePolicy", 9)
+    assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"
+    call(J, "setDevices", java.ints([]))
+    assert java.exception() is None
+    call(J, "coderDevice", 0)
+    assert java.exception()[0] == "java/io/IOException"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1 << 16, (4 << 20) + 4096 + 3])  # one chunk; two chunks of the 4 MiB arena
+def test_heap_arrays_never_pinned_across_device_work(J, java, n):
+    """byte[] inputs and outputs are copied (Get/SetByteArrayRegion) into the thread's pinned arena, and
+    no array is pinned while libozec works -- the mock records the array pins outstanding at every wrapped ozec_encode
+    / ozec_decode / ozec_crc_update / ozec_checksum_windows call.  Results vs the oracle, calls longer than one arena
+    chunk included, inputs untouched and outputs written only inside their regions."""
+    k, p, pos = 3, 2, 7
+    h = call(J, "coderCreate", 0, 0, k, p)
+    hd = call(J, "coderCreate", 1, 0, k, p)
+    try:
+        J.mock_reset_device_calls()
+        copies0 = J.mock_region_copies()
+        d = cells(SEED, 742000 + n % 97, k, n)
+        ins = [np.zeros(n + 2 * pos, np.uint8) for _ in range(k)]
+        for w, x in zip(ins, d):
+            w[pos:pos + n] = x
+        keep = [w.copy() for w in ins]
+        outs = [np.full(n + 2 * pos, 0xA5, np.uint8) for _ in range(p)]
+        call(J, "encodeArrays", h, java.array([java.bytes(x) for x in ins]), java.ints([pos] * k), n,
+             java.array([java.bytes(x) for x in outs]), java.ints([pos] * p))
+        assert java.exception() is None
+        ref = oracle.rs_encode(k, p, d)
+        for o, r in zip(outs, ref):
+            assert (o[pos:pos + n] == r).all() and (o[:pos] == 0xA5).all() and (o[pos + n:] == 0xA5).all()
+        assert all((a == b).all() for a, b in zip(ins, keep))
+        units = d + ref
+        erased = [0, 4]
+        inputs = [None if u in erased else java.bytes(units[u]) for u in range(k + p)]
+        rec = [np.zeros(n, np.uint8) for _ in erased]
+        call(J, "decodeArrays", hd, java.array(inputs), java.ints([0] * (k + p)), n, java.ints(erased),
+             java.array([java.bytes(r) for r in rec]), java.ints([0, 0]))
+        assert java.exception() is None
+        assert all((r == units[e]).all() for r, e in zip(rec, erased))
+        bpc = 16384
+        nw = (n + bpc - 1) // bpc
+        out = np.zeros(4 * nw, np.uint8)
+        assert call(J, "checksumWindowsArray", 3, java.bytes(ins[0]), pos, n, bpc, java.bytes(out)) == 4 * nw
+        assert (out.view(">u4") == oracle.crc_windows(oracle.CRC32C, d[0], bpc)).all()
+        out[:] = 0
+        assert call(J, "checksumWindowsDirect", 2, java.direct(ins[1]), pos, n, bpc, java.bytes(out)) == 4 * nw
+        assert (out.view(">u4") == oracle.crc_windows(oracle.CRC32, d[1], bpc)).all()
+        state = call(J, "crcUpdateArray", 3, -1, java.bytes(ins[2]), pos, n)
+        assert java.exception() is None
+        assert (~state) & 0xFFFFFFFF == oracle.crc_windows(oracle.CRC32C, d[2], n)[0]
+        assert J.mock_device_calls() >= 5
+        assert J.mock_pins_at_device_call() == 0, "an array was pinned while libozec did device work"
+        assert J.mock_region_copies() > copies0
+        assert J.mock_pins() == 0
+    finally:
+        call(J, "coderRelease", h)
+        call(J, "coderRelease", hd)
 
 
 @pytest.mark.gpu

@@ -206,12 +206,6 @@ int get_ctx(DevCtx **out) {
     auto c = std::make_unique<DevCtx>();
     c->device = dev;
     c->numa = ozec::device_numa_node(dev);
-    // staging copies run where the first GPU's staging memory lives (one process per GPU is the multi-GPU model)
-    static bool copy_node_set = false;
-    if (!copy_node_set) {
-      ozec::set_copy_node(c->numa);
-      copy_node_set = true;
-    }
     for (int t = 0; t < 2; ++t)
       for (int b = 0; b < 3; ++b) {
         const auto &blob = CrcMath::get(static_cast<CrcType>(t)).device_tables(1 << b);
@@ -470,7 +464,7 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     const uint8_t *src = s->pinned + c * per_chunk + nin * cp;
     std::vector<ozec::CopyTask> tasks;
     for (int r = 0; r < nout; ++r) tasks.push_back({out[r] + out_pos(off), src + r * op, out_bytes(cl)});
-    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, shared);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, shared, ctx->numa);
     return OZEC_OK;
   };
   for (size_t c = 0; c < nch; ++c) {
@@ -478,7 +472,7 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     uint8_t *h = s->pinned + c * per_chunk, *d = s->dbuf + c * per_chunk;
     std::vector<ozec::CopyTask> tasks;
     for (int j = 0; j < nin; ++j) tasks.push_back({h + j * cp, in[j] + off, cl});
-    ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, shared);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, shared, ctx->numa);
     OZEC_HIP(hipMemcpyAsync(d, h, nin * cp, hipMemcpyHostToDevice, s->stream));
     OZEC_HIP(launch(d, static_cast<int64_t>(cp), d + nin * cp, static_cast<int64_t>(op), off, cl, s->stream));
     OZEC_HIP(hipMemcpyAsync(h + nin * cp, d + nin * cp, nout * op, hipMemcpyDeviceToHost, s->stream));
@@ -1159,7 +1153,7 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
                            P.hstage[b] + i * dstripe + static_cast<size_t>(k + r) * len, len});
     if (with_crc && !crc_pinned)
       tasks.push_back({h_crcs + s0 * ncrc, P.hstage[b] + dcrc_off, cs * ncrc * sizeof(uint32_t)});
-    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, true, ctx->numa);
     return OZEC_OK;
   };
   for (size_t c = 0; c < nch; ++c) {
@@ -1175,7 +1169,7 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
           for (int j = 0; j < k; ++j)
             tasks.push_back({P.hstage[b] + i * dstripe + static_cast<size_t>(j) * len,
                              h_in + (s0 + i) * in_stripe_stride + j * in_unit_stride, len});
-        ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging);
+        ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, true, ctx->numa);
       }
     }
     // H2D after the chunk that used this buffer NB chunks ago has left the device.  The host waits for it too
@@ -1497,7 +1491,7 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
     if (!ocrc_pinned)
       tasks.push_back({h_out_crcs + s0 * e * nwin, P.hstage[b] + docrc_off, cs * e * nwin * sizeof(uint32_t)});
     if (!mis_pinned) tasks.push_back({h_mismatch + s0, P.hstage[b] + dmis_off, cs * sizeof(int32_t)});
-    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, true, ctx->numa);
     return OZEC_OK;
   };
   for (size_t c = 0; c < nch; ++c) {
@@ -1516,7 +1510,7 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
                              h_in + (s0 + i) * in_stripe_stride + u * in_unit_stride, len});
       if (!exp_pinned)
         tasks.push_back({hs + dexp_off, h_expected + s0 * n_all * nwin, cs * n_all * nwin * sizeof(uint32_t)});
-      ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging);
+      ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, true, ctx->numa);
     }
     if (c >= static_cast<size_t>(E2E::NB)) {
       if (!staged) OZEC_HIP(hipEventSynchronize(P.d2h_done[b]));

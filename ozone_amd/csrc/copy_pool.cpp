@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -87,11 +88,20 @@ struct Job {
   }
 };
 
+// One pool per host NUMA node: a GPU's staging buffers live on its node (numa.hpp), and the copies into and out of
+// them run on that node's CPUs -- a process driving GPUs on both sockets (devices.hpp) keeps every staging copy local.
+int g_default_threads = -1;  // -1: min(8, hardware threads / 2) - 1, or OZEC_COPY_THREADS
+
 class Pool {
  public:
-  static Pool &get() {
-    static Pool p;
-    return p;
+  explicit Pool(int node) : node_(node) { start_workers(default_threads()); }
+  ~Pool() { stop_workers(); }
+
+  static int default_threads() {
+    if (g_default_threads >= 0) return g_default_threads;
+    int n = static_cast<int>(std::min(8u, std::max(1u, std::thread::hardware_concurrency() / 2)) - 1);
+    if (const char *e = std::getenv("OZEC_COPY_THREADS")) n = std::max(0, std::atoi(e));
+    return n;
   }
 
   void resize(int n) {
@@ -99,16 +109,6 @@ class Pool {
     const int keep = nthreads_;
     stop_workers();
     start_workers(n < 0 ? keep : n);
-  }
-
-  // restart the workers on the CPUs of `node` (the first GPU this process uses: its staging buffers live there)
-  void set_node(int node) {
-    std::lock_guard<std::mutex> lk(resize_mu_);
-    if (node == node_) return;
-    const int n = nthreads_;
-    stop_workers();
-    node_ = node;
-    start_workers(n);
   }
 
   int size() const { return nthreads_; }
@@ -125,13 +125,6 @@ class Pool {
   }
 
  private:
-  Pool() {
-    int n = static_cast<int>(std::min(8u, std::max(1u, std::thread::hardware_concurrency() / 2)) - 1);
-    if (const char *e = std::getenv("OZEC_COPY_THREADS")) n = std::max(0, std::atoi(e));
-    start_workers(n);
-  }
-  ~Pool() { stop_workers(); }
-
   void start_workers(int n) {
     stop_ = false;
     nthreads_ = n;
@@ -179,11 +172,23 @@ class Pool {
   int node_ = -1;
 };
 
+std::mutex g_pools_mu;
+std::map<int, std::unique_ptr<Pool>> g_pools;  // by NUMA node (-1: unknown / not NUMA); never destroyed before exit
+
+Pool &pool_for(int node) {
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  auto &p = g_pools[node];
+  if (!p) p.reset(new Pool(node));
+  return *p;
+}
+
 }  // namespace
 
-void set_copy_threads(int n) { Pool::get().resize(std::max(0, n)); }
-
-void set_copy_node(int node) { Pool::get().set_node(node); }
+void set_copy_threads(int n) {
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  g_default_threads = std::max(0, n);
+  for (auto &kv : g_pools) kv.second->resize(g_default_threads);
+}
 
 bool set_copy_stream(int mode) {
   if (mode < -1 || mode > 3) return false;
@@ -191,11 +196,11 @@ bool set_copy_stream(int mode) {
   return true;
 }
 
-void parallel_copy(const std::vector<CopyTask> &tasks, CopyDir dir, bool shared) {
+void parallel_copy(const std::vector<CopyTask> &tasks, CopyDir dir, bool shared, int node) {
   size_t total = 0;
   for (const CopyTask &t : tasks) total += t.n;
   const bool stream = use_stream(dir, shared);
-  Pool &pool = Pool::get();
+  Pool &pool = pool_for(node);
   if (pool.size() == 0 || total < 2 * kPiece) {
     for (const CopyTask &t : tasks) copy_bytes(t.dst, t.src, t.n, stream);
     return;

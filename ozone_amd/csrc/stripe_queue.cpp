@@ -118,7 +118,8 @@ struct Batch {
 
 struct ozec_stripe_queue {
   ozec_coder *enc = nullptr;
-  int device = 0;  // the queue's GPU (current device at creation); pinned staging lives on its NUMA node
+  int device = 0;  // the queue's GPU (its encoder's); pinned staging lives on its NUMA node
+  int node = -1;   // that node (its copy pool, copy_pool.hpp)
   int k = 0, p = 0, rows = 0, ctype = OZEC_CHECKSUM_NONE, big_endian = 0;
   size_t cell_len = 0, S = 0, bpc = 0, nwin_max = 0;
   std::vector<Batch> batches;
@@ -209,7 +210,7 @@ struct ozec_stripe_queue {
       if (pd.crcs && ctype != OZEC_CHECKSUM_NONE)
         tasks.push_back({pd.crcs, b.h_crcs + i * units() * nw, units() * nw * sizeof(uint32_t)});
     }
-    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging);
+    ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, true, node);
     b.in_flight = false;
     b.n = 0;
     return OZEC_OK;
@@ -308,6 +309,7 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
   (void)ozec_coder_retain(enc);
   q->enc = enc;
   q->device = ozec_coder_device(enc);  // the encoder's GPU (devices.hpp)
+  q->node = q->device >= 0 ? ozec::device_numa_node(q->device) : -1;
   ozec::DeviceScope ds(q->device);
   if (!ds.ok()) {
     ozec_coder_free(enc);
@@ -396,7 +398,7 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
     tasks.push_back({st, src[j], len});
     src[j] = st;
   }
-  ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging);
+  ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, true, q->node);
   for (int j = 0; j < q->k;) {
     const size_t off = i * q->stripe_bytes() + static_cast<size_t>(j) * q->cell_len;
     int run = 1;

@@ -26,6 +26,12 @@ e = d.get("e2e", {})
 print("e2e", e.get("value"), e.get("error"))
 PY
 fi
+# interleaved same-process A/Bs: AB="c3r:0,170,191 c5dev:0,171,189" (ROUNDS each)
+for spec in $AB; do
+  w=${spec%%:*}; v=${spec#*:}
+  timeout -k 10 300 python -u scripts/ab.py $w crc_variant $v ${ROUNDS:-5} > $O/ab_$w.log 2>&1 || { tail -20 $O/ab_$w.log; exit 1; }
+  grep median_ms $O/ab_$w.log
+done
 for w in $EXTRA; do
   timeout -k 10 300 python bench.py --workload $w --no-cpu > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
   python -c "import json,sys; d=json.loads(open('$O/bench_$w.json').read().strip().splitlines()[-1]); print('$w', d['value'], d['roofline']['frac'], d['roofline'].get('frac_rocprof_avg'), d['roofline'].get('traffic'))"

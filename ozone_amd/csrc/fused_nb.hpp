@@ -395,7 +395,7 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
 
 // whether variant v of the nibble kernel runs on the persistent WorkQueue grid (needs a leased counter slot)
 constexpr bool nb_variant_persistent(int v) { return v == 150 || v == 163 || v == 167 || v == 170 || v == 171 ||
-                                                     v == 172 || v == 176 || v == 177 || (v >= 186 && v <= 192); }
+                                                     v == 172 || v == 176 || v == 177 || (v >= 186 && v <= 196); }
 
 // variant (g_tune.crc_variant, kernels.hpp kCrcVariants): the measured alternates of the nibble-table kernel
 template <int K, int R>
@@ -438,6 +438,14 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     // per CU) in 10-wave workgroups: two per CU, 20 waves; 192: 172 (ring of 2) in 12-wave workgroups
     case 191: return launch_nb<K, R, 1, kNB, 10, 5, 2, true, 1, true, true>(e, st);
     case 192: return launch_nb<K, R, 2, 2, 12, 4, 2, true, 1, true, true>(e, st);
+    // 193: 171 in 14-wave workgroups held to 7 waves per SIMD (two per CU: 28 waves); 194: 171 with half the inputs'
+    // second distance set (36 + 12 KiB of tables: three 9-wave workgroups per CU, 27 waves); 195: 177 with a ring of 2 and
+    // dword fences (fewer VGPRs) in 10-wave workgroups at 5 waves per SIMD (20 waves per CU); 196: the same at 4 waves
+    // per SIMD in 16-wave workgroups
+    case 193: return launch_nb<K, R, 2, kNB, 14, 7, 2, true, 1, true, true>(e, st);
+    case 194: return launch_nb<K, R, 2, kNB, 9, 7, 2, true, 1, true, true, kHh>(e, st);
+    case 195: return launch_nb<K, R, 2, 2, 10, 5, 1, true, 1, true, true, kHh>(e, st);
+    case 196: return launch_nb<K, R, 2, 2, 16, 4, 1, true, 1, true, true, kHh>(e, st);
     default: break;
   }
   return hipErrorInvalidValue;

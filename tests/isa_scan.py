@@ -46,15 +46,30 @@ def _writes(mnemonic, ops):
     return set()
 
 
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
 def disassemble_shared_object(so_path):
-    """llvm-objdump text of the gfx950 code object bundled into a HIP shared library."""
+    """llvm-objdump text of every gfx950 code object bundled into a HIP shared library: the .hip_fatbin section holds
+    one offload bundle per translation unit (kernels, fused, each fused_nb_<K>_<R>), back to back at aligned offsets."""
     with tempfile.TemporaryDirectory() as d:
-        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "k.co")
+        fat = os.path.join(d, "fat.bin")
         subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fat}", so_path, os.path.join(d, "x")],
                        check=True, capture_output=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o", "--unbundle", f"--targets={TARGET}",
-                        f"--input={fat}", f"--output={co}"], check=True, capture_output=True)
-        return disassemble_code_object(co)
+        blob = open(fat, "rb").read()
+        starts = []
+        i = blob.find(BUNDLE_MAGIC)
+        while i >= 0:
+            starts.append(i)
+            i = blob.find(BUNDLE_MAGIC, i + 1)
+        out = []
+        for n, a in enumerate(starts):
+            part, co = os.path.join(d, f"b{n}.bin"), os.path.join(d, f"k{n}.co")
+            open(part, "wb").write(blob[a:starts[n + 1] if n + 1 < len(starts) else len(blob)])
+            subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o", "--unbundle", f"--targets={TARGET}",
+                            f"--input={part}", f"--output={co}"], check=True, capture_output=True)
+            out.append(disassemble_code_object(co))
+        return "\n".join(out)
 
 
 def disassemble_code_object(co_path):

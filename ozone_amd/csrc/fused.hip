@@ -282,15 +282,20 @@ WorkSlot *nb_work_lease(hipStream_t st) {
     delete w;
     return nullptr;
   }
+  // the zeroing is ordered before this launch by the stream, and before a launch on any other stream by the event
+  // (a launch that does not count on the slot hands it back without recording one)
   if (hipMemsetAsync(p, 0, kWqInts * sizeof(int32_t), st) != hipSuccess ||
-      hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(w->done, st) != hipSuccess) {
     (void)hipGetLastError();
     (void)hipStreamSynchronize(st);
+    if (w->done) (void)hipEventDestroy(w->done);
     (void)hipFree(p);
     delete w;
     return nullptr;
   }
   w->ctr = static_cast<int32_t *>(p);
+  w->recorded = true;
   w->leased = true;
   g_ws.push_back(w);
   return w;

@@ -395,7 +395,8 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
 
 // whether variant v of the nibble kernel runs on the persistent WorkQueue grid (needs a leased counter slot)
 constexpr bool nb_variant_persistent(int v) { return v == 150 || v == 163 || v == 167 || v == 170 || v == 171 ||
-                                                     v == 172 || v == 176 || v == 177 || (v >= 186 && v <= 196); }
+                                                     v == 172 || v == 176 || v == 177 || v == 187 || (v >= 189 && v <= 194) ||
+                                                     v == 196; }
 
 // variant (g_tune.crc_variant, kernels.hpp kCrcVariants): the measured alternates of the nibble-table kernel
 template <int K, int R>
@@ -425,13 +426,11 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 176: return launch_nb<K, R, 2, kNB, 8, 4, 2, true, 1, true, true, kHh>(e, st);
     case 177: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true, true, kHh>(e, st);
     // round 4, occupancy: the defaults are held to one 16-wave workgroup per CU by VGPRs (177: 119 -> 4 waves per SIMD;
-    // 171: 73 -> 6, but a second 16-wave workgroup needs 8).  186 / 188: 177 in 10-wave workgroups held to 5 waves per
-    // SIMD (two per CU, 20 waves), with lookups fenced per dword (186, 16 fewer results live) or per half (188); 187:
-    // 177 with the dword fences alone; 189: 171 in 12-wave workgroups (two per CU: 24 waves); 190: 171 held to 8 waves
-    // per SIMD (two 16-wave workgroups per CU)
-    case 186: return launch_nb<K, R, 2, kNB, 10, 5, 1, true, 1, true, true, kHh>(e, st);
+    // 171: 73 -> 6, but a second 16-wave workgroup needs 8).  187: 177 with lookups fenced per dword (16 fewer results
+    // live); 189: 171 in 12-wave workgroups (two per CU: 24 waves); 190: 171 held to 8 waves per SIMD (two 16-wave
+    // workgroups per CU).  177 held to 5 waves per SIMD in 10-wave workgroups spills (22 VGPRs to scratch) and ran 21 %
+    // slower (profiles/r04/a/ab_c3r.log, variants 186 / 188, since removed)
     case 187: return launch_nb<K, R, 2, kNB, 16, 4, 1, true, 1, true, true, kHh>(e, st);
-    case 188: return launch_nb<K, R, 2, kNB, 10, 5, 2, true, 1, true, true, kHh>(e, st);
     case 189: return launch_nb<K, R, 2, kNB, 12, 4, 2, true, 1, true, true>(e, st);
     case 190: return launch_nb<K, R, 2, kNB, 16, 8, 2, true, 1, true, true>(e, st);
     // 191: 170 (one-step groups, 87 VGPRs for rs-10-4: 5 waves per SIMD, but 8-wave workgroups fill only 16 wave slots
@@ -439,12 +438,10 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 191: return launch_nb<K, R, 1, kNB, 10, 5, 2, true, 1, true, true>(e, st);
     case 192: return launch_nb<K, R, 2, 2, 12, 4, 2, true, 1, true, true>(e, st);
     // 193: 171 in 14-wave workgroups held to 7 waves per SIMD (two per CU: 28 waves); 194: 171 with half the inputs'
-    // second distance set (36 + 12 KiB of tables: three 9-wave workgroups per CU, 27 waves); 195: 177 with a ring of 2 and
-    // dword fences (fewer VGPRs) in 10-wave workgroups at 5 waves per SIMD (20 waves per CU); 196: the same at 4 waves
-    // per SIMD in 16-wave workgroups
+    // second distance set (36 + 12 KiB of tables: three 9-wave workgroups per CU, 27 waves); 196: 177 with a ring of 2
+    // and dword fences (fewer VGPRs) in 16-wave workgroups
     case 193: return launch_nb<K, R, 2, kNB, 14, 7, 2, true, 1, true, true>(e, st);
     case 194: return launch_nb<K, R, 2, kNB, 9, 7, 2, true, 1, true, true, kHh>(e, st);
-    case 195: return launch_nb<K, R, 2, 2, 10, 5, 1, true, 1, true, true, kHh>(e, st);
     case 196: return launch_nb<K, R, 2, 2, 16, 4, 1, true, 1, true, true, kHh>(e, st);
     default: break;
   }

@@ -165,11 +165,11 @@ struct TuneKnobs {
 //     fused XOR codec (launch_enc_crc_kr, R = 1 all-ones): 2 no register shortcut, 3 D = 2, 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps
 //     fused RS (launch_encode_crc): 49 per-window kernel, 56 / 59 streamed-input kernel (fused.hip), 62 / 87 / 150 /
-//       163 / 167 / 170-174 / 176 / 177 / 186-196 nibble-table kernel (fused_nb.hpp launch_nb_kr)
+//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 nibble-table kernel (fused_nb.hpp launch_nb_kr)
 constexpr int kGfVariants[] = {1, 5, 11};
 constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  49,  56,  59,  62,  87,  150, 163, 167, 170,
-                                 171, 172, 173, 174, 176, 177, 186, 187, 188, 189, 190, 191, 192,
-                                 193, 194, 195, 196};
+                                 171, 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194,
+                                 196};
 
 extern TuneKnobs g_tune;
 

@@ -7,9 +7,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"
 O=gpurun_out/${OUT:-r4}; mkdir -p $O
 export TMPDIR=/tmp
 if [ -z "$NOTEST" ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
     || { tail -30 $O/pytest_gpu.log; exit 1; }
-  tail -2 $O/pytest_gpu.log
+  tail -1 $O/pytest_gpu.log
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
   tail -1 $O/smoke.log
 fi

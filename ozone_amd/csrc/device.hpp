@@ -228,6 +228,49 @@ __device__ __forceinline__ uint32_t g5_lane_tree(const uint32_t *T, uint32_t v, 
   return v;
 }
 
+// a wave-uniform 64-bit value, said explicitly (kept in SGPRs)
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32));
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// Dynamic work distribution of the persistent fused kernels (the nibble kernel and the XOR codec's per-window kernel
+// with DYN = 1).  The (stripe, window) units are cut into 8 contiguous ranges, one per XCD (the dispatcher deals workgroups round-robin over the 8 XCDs, so workgroup b starts
+// on range b % 8: each XCD streams one contiguous eighth of the batch), and a wave takes the next unit of its range
+// with one atomicAdd (a vector-memory atomic issued by lane 0 and broadcast with readfirstlane), one unit ahead of
+// the one it works on; a wave whose range is used up moves on to the next range, so every unit is taken exactly once
+// whatever the grid size or placement.  The counters are a slot leased for the launch (fused.hip work_lease):
+// the last wave of a launch to finish puts the slot back to zero, and the slot is reused only after an event recorded
+// behind the launch has completed.
+constexpr int kWqStride = 16;                 // ints between counters (64 B: one counter per cache line)
+constexpr int kWqDone = 8 * kWqStride;        // finished-wave counter
+constexpr int kWqInts = kWqDone + kWqStride;  // ints per slot
+struct WorkQueue {
+  int32_t *ctr;
+  int64_t units;
+  int q0, qi;
+  __device__ __forceinline__ int64_t next(int lane) {
+    while (qi < 8) {
+      const int q = (q0 + qi) & 7;
+      const int64_t lo = units * q / 8, hi = units * (q + 1) / 8;
+      int32_t t = 0;
+      if (lane == 0) t = atomicAdd(ctr + q * kWqStride, 1);
+      t = __builtin_amdgcn_readfirstlane(t);
+      if (lo + t < hi) return lo + t;
+      ++qi;
+    }
+    return units;
+  }
+  // every wave calls this once after its last unit: the last of `waves` resets the slot
+  __device__ __forceinline__ void finish(int lane, int32_t waves) {
+    if (lane == 0 && atomicAdd(ctr + kWqDone, 1) == waves - 1) {
+      for (int q = 0; q < 8; ++q) atomicExch(ctr + q * kWqStride, 0);
+      atomicExch(ctr + kWqDone, 0);
+    }
+  }
+};
+
 __device__ __forceinline__ void load_tables(uint32_t *s_t, const uint32_t *g, int words) {
   const uint4 *src = reinterpret_cast<const uint4 *>(g);
   uint4 *dst = reinterpret_cast<uint4 *>(s_t);

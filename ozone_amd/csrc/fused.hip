@@ -236,24 +236,21 @@ hipError_t launch_lv_kr(const EncCrcArgs &e, hipStream_t st, int v) {
   return hipErrorInvalidValue;
 }
 
-// Counter slots of the persistent nibble kernel's WorkQueue.  A launch leases a zeroed slot and hands it back behind an
-// event recorded after the kernel on the launch stream; the slot is leased again only once that event has completed,
+}  // namespace
+
+// Counter slots of the persistent kernels' WorkQueue (kernels.hpp work_lease).  A launch leases a zeroed slot and
+// hands it back behind an event recorded after the kernel on the launch stream; the slot is leased again only once
+// that event has completed,
 // i.e. once the kernel's last wave has put the counters back to zero.  Slots are not tied to a stream handle, so
 // concurrent launches never share one, whatever the stream (the null stream, hipStreamPerThread, several streams of
 // one caller).  A capturing stream gets no slot: its launches take the non-persistent form.
-struct WorkSlot {
-  int device = -1;
-  int32_t *ctr = nullptr;
-  hipEvent_t done = nullptr;
-  bool recorded = false;  // `done` marks the last launch that used the slot
-  bool leased = false;
-};
-
+namespace {
 std::mutex g_ws_mu;
 std::vector<WorkSlot *> g_ws;  // never freed: a handful per device and process
 constexpr size_t kMaxWorkSlots = 256;
+}  // namespace
 
-WorkSlot *nb_work_lease(hipStream_t st) {
+WorkSlot *work_lease(hipStream_t st) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
     (void)hipGetLastError();
@@ -302,7 +299,7 @@ WorkSlot *nb_work_lease(hipStream_t st) {
 }
 
 // give the slot back; `used`: a kernel that counts on it was enqueued on `st`
-void nb_work_return(WorkSlot *w, hipStream_t st, bool used) {
+void work_return(WorkSlot *w, hipStream_t st, bool used) {
   if (used) {
     if (hipEventRecord(w->done, st) == hipSuccess) {
       w->recorded = true;
@@ -314,8 +311,6 @@ void nb_work_return(WorkSlot *w, hipStream_t st, bool used) {
   std::lock_guard<std::mutex> lk(g_ws_mu);
   w->leased = false;
 }
-
-}  // namespace
 
 bool encode_crc_lv_supported(const EncCrcArgs &e) {
   const CodeArgs &a = e.code;
@@ -363,13 +358,13 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // compare (EM: 170 = 150, 171 = 167, 172 = 163 with it; C3r 5.711 -> 5.582 ms, C5dev 6.956 -> 6.911 ms,
   // profiles/r03/em/ab_*.log); rs-10-x takes two-step groups with the second distance set for half the inputs (177,
   // 0.5-1.3 % faster than 170 in three same-process A/Bs, profiles/r03/h/)
-  WorkSlot *ws = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) ? nb_work_lease(st) : nullptr;
+  WorkSlot *ws = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) ? work_lease(st) : nullptr;
   if (v == 0) v = k == 10 ? (ws ? 177 : 173) : !ws ? 174 : k == 6 ? 171 : 172;
   const bool used = ws && nb_variant_persistent(v);
   EncCrcArgs ed = e;
   ed.work = used ? ws->ctr : nullptr;
   const hipError_t err = launch_nb_shape(ed, st, v);
-  if (ws) nb_work_return(ws, st, used && err == hipSuccess);
+  if (ws) work_return(ws, st, used && err == hipSuccess);
   return err;
 }
 

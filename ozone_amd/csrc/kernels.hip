@@ -1025,13 +1025,17 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
   }
   if constexpr (R == 1) {
     if (e.code.all_ones && v != 2) {
-      // XOR codec: D = 4 with the next step's loads in flight (C4 77.9 % vs 75.8 % for D = 2, ab_c4.log)
-      if (v == 3) hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1>), grid, block, 0, st, e, tabs);
+      // XOR codec: groups of D = 2 steps, loads issued at the step (45 VGPRs for xor-2-1, 8 waves per SIMD).  Round 1
+      // chose D = 4 with the next step's loads in flight (67 VGPRs; variant 3 now): C4 77.9 % vs 75.8 % then
+      // (profiles/r01/session2/ab_c4.log); on the round-4 build D = 2 is 1.0-1.8 % faster in 4 same-process A/Bs on
+      // two boxes (profiles/r04/c4/ab_c4_*.log).  On a persistent WorkQueue grid either runs 10-12 % slower
+      // (ab_c4_persistent_*.log; not kept)
+      if (v == 3) hipLaunchKernelGGL((encode_crc_g26<K, R, 4, true, 1, 4, true>), grid, block, 0, st, e, tabs);
       else if (v == 4)  // free register shifts (XO)
         hipLaunchKernelGGL((encode_crc_g26<K, R, 4, true, 1, 4, true, false, true>), grid, block, 0, st, e, tabs);
       else if (v == 5)
         hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1, 4, true, false, true>), grid, block, 0, st, e, tabs);
-      else hipLaunchKernelGGL((encode_crc_g26<K, R, 4, true, 1, 4, true>), grid, block, 0, st, e, tabs);
+      else hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1>), grid, block, 0, st, e, tabs);
       return hipGetLastError();
     }
   }

@@ -72,7 +72,7 @@ struct EncCrcArgs {
   int32_t verify;
   int32_t exp_units;
   int32_t in_unit[OZEC_MAX_K];
-  int32_t *work;  // WorkQueue counter slot of the persistent nibble kernel (set by its launcher)
+  int32_t *work;  // WorkQueue counter slot of a persistent kernel (set by its launcher, work_lease)
 };
 
 // Device CRC "G5" table blob (uint32 entries), built on the host (crc_host.cpp), one per (CRC type, B) where
@@ -162,14 +162,14 @@ struct TuneKnobs {
 //   gf_variant (coding kernel gf_code_vec, kernels.hip launch_kr): 1, 5, 11
 //   crc_variant, by kernel family:
 //     streaming CRC (launch_crc_windows): 20, 22 -- D-step groups instead of the XO default
-//     fused XOR codec (launch_enc_crc_kr, R = 1 all-ones): 2 no register shortcut, 3 D = 2, 4 / 5 XO with D = 4 / 2,
+//     fused XOR codec (launch_enc_crc_kr, R = 1 all-ones): 2 no register shortcut, 3 D = 4 with loads one step ahead
+//       (the round-1 default), 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps
 //     fused RS (launch_encode_crc): 49 per-window kernel, 56 / 59 streamed-input kernel (fused.hip), 62 / 87 / 150 /
 //       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 nibble-table kernel (fused_nb.hpp launch_nb_kr)
 constexpr int kGfVariants[] = {1, 5, 11};
 constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  49,  56,  59,  62,  87,  150, 163, 167, 170,
-                                 171, 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194,
-                                 196};
+                                 171, 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196};
 
 extern TuneKnobs g_tune;
 
@@ -198,5 +198,19 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc);
 // the streamed-input fused kernel (fused.hip): RS shapes with full windows, bpc % 4096 == 0; `e` already rebased
 bool encode_crc_lv_supported(const EncCrcArgs &e);
 hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant);
+
+// WorkQueue counter slots of the persistent kernels (device.hpp WorkQueue; pool in fused.hip).  work_lease gives a
+// zeroed slot of the current device, not in use by any launch still running, or null (capturing stream, pool full,
+// allocation failure: the caller takes a non-persistent form); work_return hands it back, `used` when a kernel that
+// counts on it was enqueued on `st` (an event recorded behind it gates the next lease).
+struct WorkSlot {
+  int device = -1;
+  int32_t *ctr = nullptr;
+  hipEvent_t done = nullptr;
+  bool recorded = false;  // `done` marks the last launch that used the slot (or the slot's zeroing)
+  bool leased = false;
+};
+WorkSlot *work_lease(hipStream_t st);
+void work_return(WorkSlot *w, hipStream_t st, bool used);
 
 }  // namespace ozec

@@ -643,6 +643,7 @@ int ozec_encode(ozec_coder *enc, const uint8_t *const *inputs, uint8_t *const *o
     if (!outputs[r]) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
   if (len == 0) return OZEC_OK;  // RawErasureEncoder.java:73-75
   ozec::DeviceScope ds(enc->device);  // the coder's GPU (devices.hpp)
+  if (!ds.ok()) return fail(OZEC_EDEVICE, "cannot select device " + std::to_string(enc->device));
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
   CodeArgs a{};
@@ -736,6 +737,7 @@ int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased
   if (len == 0 || n_erased == 0) return OZEC_OK;
   const int nin = static_cast<int>(units.size());
   ozec::DeviceScope ds(dec->device);  // the coder's GPU (devices.hpp)
+  if (!ds.ok()) return fail(OZEC_EDEVICE, "cannot select device " + std::to_string(dec->device));
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
   CodeArgs a{};
@@ -884,6 +886,7 @@ static int checksum_host(int checksum_type, const uint8_t *data, size_t len, siz
   if (len == 0) return OZEC_OK;
   if (!data || !out) return fail(OZEC_EINVAL, "null buffer");
   ozec::DeviceScope ds(ozec::thread_device());  // coder-less host call: this thread's GPU (devices.hpp)
+  if (!ds.ok()) return fail(OZEC_EDEVICE, "cannot select this thread's device");
   DevCtx *ctx;
   if (int rc = get_ctx(&ctx)) return rc;
   uint8_t *outs[1] = {reinterpret_cast<uint8_t *>(out)};

@@ -67,6 +67,14 @@ int caller_node() {
   return static_cast<int>(node);
 }
 
+// the listed devices a NUMA-policy caller on `node` prefers: those on its node, or all when none is
+std::vector<int> near_or_all(const std::vector<int> &list, int node) {
+  std::vector<int> near;
+  for (int d : list)
+    if (node >= 0 && device_numa_node(d) == node) near.push_back(d);
+  return near.empty() ? list : near;
+}
+
 }  // namespace
 
 std::vector<int> device_list() {
@@ -115,15 +123,11 @@ int pick_device() {
   }
   const std::vector<int> list = device_list();
   if (list.empty()) return -1;
-  if (policy == 1) {  // the listed GPUs on the caller's NUMA node, round robin; all of them when none is
-    const int node = caller_node();
-    std::vector<int> near;
-    for (int d : list)
-      if (node >= 0 && device_numa_node(d) == node) near.push_back(d);
-    if (!near.empty()) return near[g_next.fetch_add(1, std::memory_order_relaxed) % near.size()];
-  }
-  return list[g_next.fetch_add(1, std::memory_order_relaxed) % list.size()];
+  // NUMA policy: the listed GPUs on the caller's NUMA node, round robin; all of them when none is
+  const std::vector<int> cand = policy == 1 ? near_or_all(list, caller_node()) : list;
+  return cand[g_next.fetch_add(1, std::memory_order_relaxed) % cand.size()];
 }
+
 
 int thread_device() {
   if (device_policy() == 2) {  // follows the thread's current device, call by call
@@ -140,7 +144,8 @@ int thread_device() {
   if (dev < 0 || gen != now) {  // first call, or the list changed since this thread was given its device
     const std::vector<int> list = device_list();
     if (list.empty()) return -1;
-    dev = list[g_thread_next.fetch_add(1, std::memory_order_relaxed) % list.size()];
+    const std::vector<int> cand = device_policy() == 1 ? near_or_all(list, caller_node()) : list;
+    dev = cand[g_thread_next.fetch_add(1, std::memory_order_relaxed) % cand.size()];
     gen = now;
   }
   return dev;

@@ -25,7 +25,8 @@ std::vector<int> device_list();
 int set_device_list(const int *devs, int n);
 // the device a new coder is bound to, by the policy
 int pick_device();
-// the device of this thread's coder-less host calls
+// the device of this thread's coder-less host calls: given on first use by the policy (round robin over the list, or
+// over the listed devices on the thread's NUMA node), re-picked when the list changes; "current": the current device
 int thread_device();
 // 0 round_robin, 1 numa, 2 current
 int device_policy();

@@ -362,6 +362,7 @@ int ozec_stripe_queue_submit(ozec_stripe_queue *q, const uint8_t *const *data, u
     return set_error(OZEC_EINVAL, "stripe length must be in [1, cell_len] (" + std::to_string(q->cell_len) + ")");
   if (ozec_coder_is_closed(q->enc)) return set_error(OZEC_ECLOSED, "stripe queue submit failed: the encoder is closed");
   ozec::DeviceScope ds(q->device);
+  if (!ds.ok()) return set_error(OZEC_EDEVICE, "cannot select device " + std::to_string(q->device));
   std::lock_guard<std::mutex> lk(q->mu);
   Batch *b = &q->batches[q->cur];
   // cur only ever points at a filling batch or, once the ring has wrapped, at the oldest in-flight one: that one
@@ -420,6 +421,7 @@ int ozec_stripe_queue_flush(ozec_stripe_queue *q) {
   ozec::StatScope stat_(OZEC_OP_QUEUE, 0);
   if (!q) return set_error(OZEC_EINVAL, "null queue");
   ozec::DeviceScope ds(q->device);
+  if (!ds.ok()) return set_error(OZEC_EDEVICE, "cannot select device " + std::to_string(q->device));
   std::lock_guard<std::mutex> lk(q->mu);
   Batch &b = q->batches[q->cur];
   if (b.n > 0 && !b.in_flight) {
@@ -433,6 +435,7 @@ int ozec_stripe_queue_wait(ozec_stripe_queue *q, uint64_t ticket) {
   ozec::StatScope stat_(OZEC_OP_QUEUE, 0);
   if (!q) return set_error(OZEC_EINVAL, "null queue");
   ozec::DeviceScope ds(q->device);
+  if (!ds.ok()) return set_error(OZEC_EDEVICE, "cannot select device " + std::to_string(q->device));
   std::lock_guard<std::mutex> lk(q->mu);
   if (ticket >= q->next_ticket) return set_error(OZEC_EINVAL, "unknown ticket " + std::to_string(ticket));
   // complete, oldest first, every batch holding a stripe <= ticket (launching the filling one if needed)

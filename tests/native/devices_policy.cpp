@@ -86,6 +86,13 @@ int main() {
   std::set<int> seen;
   for (int i = 0; i < 8; ++i) seen.insert(ozec::pick_device());
   CHECK((seen == std::set<int>{2, 3}));
+  {  // coder-less calls of NUMA-policy threads: a listed device on the thread's node
+    std::vector<int> nt(4, -1);
+    std::vector<std::thread> th;
+    for (int i = 0; i < 4; ++i) th.emplace_back([&, i] { nt[i] = ozec::thread_device(); });
+    for (auto &t : th) t.join();
+    for (int d : nt) CHECK(d == 2 || d == 3);
+  }
   const int far[] = {0, 1};
   CHECK(ozec::set_device_list(far, 2) == OZEC_OK);  // none near: every listed device
   seen.clear();

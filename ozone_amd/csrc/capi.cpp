@@ -1649,7 +1649,12 @@ int ozec_encode_crc_host_batch(ozec_coder *enc, const uint8_t *h_in, int64_t in_
   if (len == 0 || num_stripes == 0) return OZEC_OK;
   const bool with_crc = checksum_type != OZEC_CHECKSUM_NONE;
   if (!h_in || !h_out || (with_crc && !h_crcs)) return fail(OZEC_EINVAL, "Invalid buffer found, not allowing null");
-  const size_t ncrc = with_crc && bpc ? static_cast<size_t>(enc->k + out_rows(enc)) * ((len + bpc - 1) / bpc) : 0;
+  if (with_crc) {  // argument errors as the single-device path reports them, before any split
+    CrcType t;
+    if (int rc = crc_type_of(checksum_type, &t)) return rc;
+    if (bpc == 0) return fail(OZEC_EINVAL, "bytesPerChecksum must be positive");
+  }
+  const size_t ncrc = with_crc ? static_cast<size_t>(enc->k + out_rows(enc)) * ((len + bpc - 1) / bpc) : 0;
   return host_batch_split(enc, num_stripes, e2e_chunk_of(stripes_per_chunk), [&](size_t s0, size_t s1) {
     return encode_crc_host_batch_dev(enc, h_in + s0 * in_stripe_stride, in_stripe_stride, in_unit_stride,
                                      h_out + s0 * out_stripe_stride, out_stripe_stride, out_unit_stride, s1 - s0, len,

@@ -1,0 +1,206 @@
+"""Seeded random sweep of the HIP path against the oracle, bit-exact (GPU).
+
+The fixed-shape tests pin the configurations BASELINE names and the reference's own test shapes; this sweep draws
+shapes, lengths, alignments, erasure patterns, CRC types and window sizes at random (recorded seed per case) so the
+dispatch between kernels -- fused vs unfused, full vs short last windows, aligned vs misaligned cells, nibble vs
+per-window vs XOR kernels, first-k-valid decode -- is crossed in combinations no hand-written case lists.
+Reference semantics followed: RSRawEncoder / RSRawDecoder (EC/rawcoder/RSRawDecoder.java:79-176, first k valid
+inputs), XORRawEncoder / XORRawDecoder (XORRawEncoder.java:39-85), Checksum.computeChecksum window split
+(CM/Checksum.java:157-200, short last window), ECReconstructionCoordinator's verify + decode + re-checksum.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from ozone_amd import checksum as ck  # noqa: E402
+from ozone_amd import rawcoder as rc  # noqa: E402
+
+DEV = "cuda:0"
+N_CASES = 48
+
+
+def _rng(tag, i):
+    return np.random.default_rng([0x5EED, tag, i])
+
+
+def _codec(r):
+    """(codec, k, p): RS over the reference's schemas and odd ones, XOR with 1-3 parity slots."""
+    if r.random() < 0.2:
+        return "xor", int(r.integers(1, 9)), int(r.integers(1, 4))
+    k = int(r.choice([1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16]))
+    p = int(r.choice([1, 2, 3, 4])) if k < 16 else int(r.choice([2, 4]))
+    return "rs", k, p
+
+
+def _parity(codec, k, p, data):
+    return oracle.rs_encode(k, p, data) if codec == "rs" else [oracle.xor_encode(data)] + \
+        [np.zeros(len(data[0]), np.uint8) for _ in range(p - 1)]
+
+
+def _erasure(r, codec, k, p):
+    """(erased indexes in the reference's order, inputs present)."""
+    if codec == "xor":  # XORRawDecoder XORs every other slot (XORRawDecoder.java:40-86): all of them present
+        e = int(r.integers(0, k + p))
+        return [e], [u for u in range(k + p) if u != e]
+    ne = int(r.integers(1, p + 1))
+    erased = sorted(int(x) for x in r.choice(k + p, size=ne, replace=False))
+    present = [u for u in range(k + p) if u not in erased]
+    return erased, present
+
+
+def _cells(r, k, n):
+    return [r.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+
+
+@pytest.mark.parametrize("i", range(N_CASES))
+def test_random_host_encode_decode(i):
+    """Host-buffer entry points (the JNI drop-in's per-call path): cells at random offsets inside larger buffers,
+    outputs pre-filled with garbage, decode from the reference's input-slot convention."""
+    r = _rng(1, i)
+    codec, k, p = _codec(r)
+    n = int(r.integers(1, 300_000))
+    data = _cells(r, k, n)
+    pad = int(r.integers(0, 64))
+    bufs = [np.zeros(n + 2 * pad + 1, np.uint8) for _ in range(k)]
+    ins = [b[pad:pad + n] for b in bufs]
+    for a, d in zip(ins, data):
+        a[:] = d
+    outs = [np.full(n, 0xA5, np.uint8) for _ in range(p)]
+    rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec)).encode(ins, outs)
+    ref = _parity(codec, k, p, data)
+    assert all((o == x).all() for o, x in zip(outs, ref)), (codec, k, p, n)
+    units = data + ref  # XOR p > 1: the extra parity slots hold the zeros the encoder wrote
+    erased, present = _erasure(r, codec, k, p)
+    slots = [units[u] if u in present else None for u in range(k + p)]
+    got = [np.full(n, 0x5A, np.uint8) for _ in erased]
+    rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec)).decode(slots, erased, got)
+    assert all((g == units[e]).all() for g, e in zip(got, erased)), (codec, k, p, n, erased)
+
+
+@pytest.mark.parametrize("i", range(N_CASES))
+def test_random_device_encode_decode(i):
+    """Device-pointer entry points at random 0-15-byte misalignments, against the oracle."""
+    r = _rng(2, i)
+    codec, k, p = _codec(r)
+    n = int(r.integers(1, 200_000))
+    data = _cells(r, k, n)
+    off = [int(x) for x in r.integers(0, 16, k + p + 8)]
+    raw = [torch.zeros(n + 32, dtype=torch.uint8, device=DEV) for _ in range(k)]
+    for j in range(k):
+        raw[j][off[j]:off[j] + n] = torch.from_numpy(data[j]).to(DEV)
+    out = [torch.full((n + 32,), 0xA5, dtype=torch.uint8, device=DEV) for _ in range(p)]
+    rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec)).encode_device(
+        [raw[j][off[j]:] for j in range(k)], [out[q][off[k + q]:] for q in range(p)], n)
+    torch.cuda.synchronize()
+    ref = _parity(codec, k, p, data)
+    for q in range(p if codec == "rs" else 1):
+        o = out[q].cpu().numpy()
+        assert (o[off[k + q]:off[k + q] + n] == ref[q]).all(), (codec, k, p, n, q)
+        assert (o[:off[k + q]] == 0xA5).all() and (o[off[k + q] + n:] == 0xA5).all()  # nothing outside the cell
+    units = data + ref
+    erased, present = _erasure(r, codec, k, p)
+    d_in = [torch.from_numpy(units[u]).to(DEV) if u in present else None for u in range(k + p)]
+    d_out = [torch.zeros(n, dtype=torch.uint8, device=DEV) for _ in erased]
+    rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec)).decode_device(d_in, erased, d_out, n)
+    torch.cuda.synchronize()
+    assert all((x.cpu().numpy() == units[e]).all() for x, e in zip(d_out, erased)), (codec, k, p, n, erased)
+
+
+FUSED = [("rs", 6, 3), ("rs", 6, 2), ("rs", 6, 1), ("rs", 3, 2), ("rs", 3, 1), ("rs", 10, 4), ("rs", 10, 3),
+         ("rs", 10, 2), ("rs", 10, 1), ("xor", 2, 1), ("xor", 3, 1), ("rs", 5, 2), ("rs", 4, 4)]
+
+
+def _fused_case(r):
+    codec, k, p = FUSED[int(r.integers(0, len(FUSED)))]
+    bpc = int(r.choice([512, 1000, 4096, 8192, 16384, 65536]))
+    n = int(r.choice([bpc * int(r.integers(1, 5)), int(r.integers(1, 4 * bpc))]))  # full or short last windows
+    S = int(r.integers(1, 7))
+    ctype = (ck.ChecksumType.CRC32, ck.ChecksumType.CRC32C)[int(r.integers(0, 2))]
+    return codec, k, p, bpc, n, S, ctype
+
+
+def _otype(ctype):
+    return oracle.CRC32 if ctype == ck.ChecksumType.CRC32 else oracle.CRC32C
+
+
+@pytest.mark.parametrize("i", range(N_CASES))
+def test_random_fused_encode_crc(i):
+    """encode + window CRCs of every unit in one call, stripe-major batch, vs oracle parity and CRCs."""
+    r = _rng(3, i)
+    codec, k, p, bpc, n, S, ctype = _fused_case(r)
+    rows = p if codec == "rs" else 1
+    data = np.stack([np.stack(_cells(r, k, n)) for _ in range(S)])              # [S][k][n]
+    units = torch.full((S, k + p, n), 0xA5, dtype=torch.uint8, device=DEV)
+    units[:, :k] = torch.from_numpy(data).to(DEV)
+    nwin = -(-n // bpc)
+    crcs = torch.zeros((S, k + rows, nwin), dtype=torch.int32, device=DEV)
+    rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec)).encode_crc_batch(
+        units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n, ctype, bpc, crcs)
+    torch.cuda.synchronize()
+    got, c = units.cpu().numpy(), crcs.cpu().numpy().view(np.uint32)
+    for s in range(S):
+        ref = _parity(codec, k, p, list(data[s]))
+        for q in range(p):
+            assert (got[s, k + q] == ref[q]).all(), (codec, k, p, n, bpc, s, q)
+        for u, cell in enumerate(list(data[s]) + ref[:rows]):
+            assert (c[s, u] == oracle.crc_windows(_otype(ctype), cell, bpc)).all(), (codec, k, p, n, bpc, s, u)
+
+
+@pytest.mark.parametrize("i", range(N_CASES))
+def test_random_fused_reconstruction(i):
+    """Verify stored CRCs of the units read + decode + CRC of the rebuilt units, with a silent corruption planted
+    in a random stripe: that stripe reports the first failing (unit, window), the others rebuild exactly."""
+    r = _rng(4, i)
+    codec, k, p, bpc, n, S, ctype = _fused_case(r)
+    S = max(S, 2)
+    data = [list(_cells(r, k, n)) for _ in range(S)]
+    units = np.stack([np.stack(d + _parity(codec, k, p, d)) for d in data])      # [S][k+p][n]
+    nwin = -(-n // bpc)
+    ot = _otype(ctype)
+    stored = np.stack([np.stack([oracle.crc_windows(ot, units[s, u], bpc) for u in range(k + p)])
+                       for s in range(S)]).astype(np.uint32)
+    erased, present = _erasure(r, codec, k, p)
+    read = present[:k]
+    bad_s, bad_u = int(r.integers(0, S)), int(r.choice(read))
+    bad_w = int(r.integers(0, nwin))
+    pos = min(n - 1, bad_w * bpc + int(r.integers(0, bpc)))
+    corrupted = units.copy()
+    corrupted[:, erased] = 0xEE
+    corrupted[bad_s, bad_u, pos] ^= 0x41
+    d_out = torch.zeros((S, len(erased), n), dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, len(erased), nwin), dtype=torch.int32, device=DEV)
+    mism = torch.zeros(S, dtype=torch.int32, device=DEV)
+    dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec))
+    dec.reconstruct_crc_batch(torch.from_numpy(corrupted).to(DEV), (k + p) * n, n, present, erased, d_out,
+                              len(erased) * n, n, S, n, ctype, bpc, d_crc,
+                              d_expected=torch.from_numpy(stored.view(np.int32)).to(DEV), d_mismatch=mism)
+    torch.cuda.synchronize()
+    out, crcs, m = d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint32), mism.cpu().numpy()
+    for s in range(S):
+        if s == bad_s:
+            assert m[s] == bad_u * nwin + pos // bpc, (codec, k, p, n, bpc, erased, bad_u, pos)
+            for q in range(len(erased)):  # rebuilt CRCs describe what was written
+                assert (crcs[s, q] == oracle.crc_windows(ot, out[s, q], bpc)).all()
+            continue
+        assert m[s] == -1, (codec, k, p, n, bpc, s)
+        for q, e in enumerate(erased):
+            assert (out[s, q] == units[s, e]).all(), (codec, k, p, n, bpc, s, e)
+            assert (crcs[s, q] == stored[s, e]).all(), (codec, k, p, n, bpc, s, e)
+
+
+@pytest.mark.parametrize("i", range(N_CASES))
+def test_random_checksum_windows(i):
+    """Checksum.computeChecksum over random lengths, window sizes and offsets, host and device, both CRC types."""
+    r = _rng(5, i)
+    bpc = int(r.choice([1, 7, 16, 512, 1000, 4096, 16384, 65536, 1 << 20]))
+    n = int(r.integers(1, 400_000 if bpc >= 16 else 20_000))
+    ctype = (ck.ChecksumType.CRC32, ck.ChecksumType.CRC32C)[int(r.integers(0, 2))]
+    off = int(r.integers(0, 32))
+    buf = r.integers(0, 256, n + off, dtype=np.uint8)
+    want = [int(x) for x in oracle.crc_windows(_otype(ctype), buf[off:], bpc)]
+    cd = ck.Checksum(ctype, bpc).compute_checksum(buf[off:])
+    assert [int.from_bytes(b, "big") for b in cd.get_checksums()] == want, (n, bpc, off)

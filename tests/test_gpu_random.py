@@ -204,3 +204,82 @@ def test_random_checksum_windows(i):
     want = [int(x) for x in oracle.crc_windows(_otype(ctype), buf[off:], bpc)]
     cd = ck.Checksum(ctype, bpc).compute_checksum(buf[off:])
     assert [int.from_bytes(b, "big") for b in cd.get_checksums()] == want, (n, bpc, off)
+
+
+@pytest.fixture
+def device_list():
+    """ozec_set_devices for one test, the default list restored afterwards."""
+    yield rc.set_devices
+    rc.set_devices(None)
+
+
+@pytest.mark.parametrize("i", range(N_CASES // 2))
+def test_random_host_batches(device_list, i):
+    """C5's host-batch entry points (ozec_encode_crc_host_batch / ozec_reconstruct_crc_host_batch) over random
+    shapes, batch sizes, pipeline chunks, unit gaps, pinned or pageable batches and device lists ([0, 0, 0] stands
+    for three GPUs on the one-GPU box: the batch is cut into that many stripe ranges, each on its own pipeline)."""
+    from ozone_amd.stripe_queue import host_alloc
+    r = _rng(6, i)
+    codec, k, p, bpc, n, S, ctype = _fused_case(r)
+    S = int(r.integers(1, 40))
+    chunk = int(r.integers(0, 9))
+    gap = int(r.choice([0, 0, 16, 4096]))
+    devs = [0] * int(r.integers(1, 4))
+    pinned = bool(r.integers(0, 2))
+    device_list(devs)
+    rows = p if codec == "rs" else 1
+    us = n + gap
+    nwin = -(-n // bpc)
+    data = [_cells(r, k, n) for _ in range(S)]
+    units = [d + _parity(codec, k, p, d) for d in data]
+    keep = []
+
+    def host(nbytes, dtype=np.uint8):
+        if not pinned:
+            return np.zeros(nbytes // np.dtype(dtype).itemsize, dtype)
+        b = host_alloc(nbytes)
+        keep.append(b)
+        return b.array.view(dtype)
+
+    buf = host(S * (k + p) * us)
+    v = buf.reshape(S, k + p, us)
+    v[:] = 0xA5
+    for s in range(S):
+        for j in range(k):
+            v[s, j, :n] = data[s][j]
+    crcs = host(S * (k + rows) * nwin * 4, np.uint32)
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec))
+    enc.encode_crc_host_batch(buf.ctypes.data, (k + p) * us, us, buf.ctypes.data + k * us, (k + p) * us, us, S, n,
+                              ctype, bpc, crcs, False, chunk)
+    ot = _otype(ctype)
+    c = crcs.reshape(S, k + rows, nwin)
+    for s in range(S):
+        for q in range(p):
+            assert (v[s, k + q, :n] == units[s][k + q]).all(), (codec, k, p, n, S, chunk, devs, s, q)
+        for u in range(k + rows):
+            assert (c[s, u] == oracle.crc_windows(ot, units[s][u], bpc)).all(), (codec, k, p, n, S, s, u)
+    # the same stripes rebuilt from host memory, one planted corruption
+    erased, present = _erasure(r, codec, k, p)
+    for s in range(S):
+        for q in range(p):
+            v[s, k + q, :n] = units[s][k + q]
+    stored = np.stack([np.stack([oracle.crc_windows(ot, units[s][u], bpc) for u in range(k + p)])
+                       for s in range(S)]).astype(np.uint32)
+    bad_s, bad_u = int(r.integers(0, S)), int(present[int(r.integers(0, k))])
+    pos = int(r.integers(0, n))
+    v[bad_s, bad_u, pos] ^= 0x08
+    e = len(erased)
+    out = host(S * e * n)
+    ocrc = host(S * e * nwin * 4, np.uint32)
+    mism = np.zeros(S, np.int32)
+    dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec))
+    dec.reconstruct_crc_host_batch(buf, (k + p) * us, us, present, erased, out, e * n, n, S, n, ctype, bpc, ocrc,
+                                   h_expected=stored.reshape(-1), h_mismatch=mism, stripes_per_chunk=chunk)
+    got, oc = out.reshape(S, e, n), ocrc.reshape(S, e, nwin)
+    for s in range(S):
+        if s == bad_s:
+            assert mism[s] == bad_u * nwin + pos // bpc, (codec, k, p, n, S, erased, bad_u, pos)
+            continue
+        assert mism[s] == -1, (codec, k, p, n, S, chunk, devs, s)
+        for q, u in enumerate(erased):
+            assert (got[s, q] == units[s][u]).all() and (oc[s, q] == stored[s, u]).all(), (codec, k, p, s, u)

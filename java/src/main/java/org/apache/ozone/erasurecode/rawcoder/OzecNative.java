@@ -59,8 +59,8 @@ public final class OzecNative {
         setDevicePolicy("numa".equals(policy) ? DEVICE_POLICY_NUMA
             : "current".equals(policy) ? DEVICE_POLICY_CURRENT : DEVICE_POLICY_ROUND_ROBIN);
       }
-    } catch (RuntimeException e) {
-      // NumberFormatException or a device the node does not have: keep the default
+    } catch (IOException | RuntimeException e) {
+      // a device the node does not have (IOException) or a malformed value: keep the default
     }
   }
 
@@ -88,15 +88,18 @@ public final class OzecNative {
   public static final int DEVICE_POLICY_CURRENT = 2;
 
   // ---- the GPUs of this process (ozec_set_devices / ozec_get_devices / ozec_set_device_policy / ozec_coder_device)
-  /** The GPUs coders and host batches use from now on; an empty array restores every visible GPU. */
-  public static native void setDevices(int[] devices);
+  /**
+   * The GPUs coders and host batches use from now on; an empty array restores every visible GPU.
+   * @throws IOException a listed ordinal is not a GPU of this node (the list is left unchanged)
+   */
+  public static native void setDevices(int[] devices) throws IOException;
 
   public static native int[] getDevices();
 
   public static native void setDevicePolicy(int policy);
 
-  /** The GPU a coder handle's calls run on. */
-  static native int coderDevice(long handle);
+  /** The GPU a coder handle's calls run on; IOException for a null handle. */
+  static native int coderDevice(long handle) throws IOException;
 
   // ---- coders (ozec_encoder_create / ozec_decoder_create / ozec_coder_release + ozec_coder_free)
   static native long coderCreate(boolean decoder, int codec, int numData, int numParity);

@@ -67,11 +67,11 @@ def test_reconstruct_every_recoverable_set_with_crcs(k, p, bpc):
     d_exp = torch.from_numpy(stored.view(np.int32)).to(DEV)
     dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
     d_out = torch.empty((S, p, n), dtype=torch.uint8, device=DEV)
-    d_crc = torch.empty((S, p, nwin), dtype=torch.int32, device=DEV)
     mism = torch.empty(S, dtype=torch.int32, device=DEV)
     for erased in _sets(k, p):
         present = [u for u in range(k + p) if u not in erased]
         d_out.fill_(0xA5)
+        d_crc = torch.empty((S, len(erased), nwin), dtype=torch.int32, device=DEV)  # [stripe][rebuilt unit][window]
         dec.reconstruct_crc_batch(d_in, (k + p) * n, n, present, erased, d_out, p * n, n, S, n,
                                   ck.ChecksumType.CRC32C, bpc, d_crc, d_expected=d_exp, d_mismatch=mism)
         got, crcs, m = d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint32), mism.cpu().numpy()

@@ -283,3 +283,38 @@ def test_random_host_batches(device_list, i):
         assert mism[s] == -1, (codec, k, p, n, S, chunk, devs, s)
         for q, u in enumerate(erased):
             assert (got[s, q] == units[s][u]).all() and (oc[s, q] == stored[s, u]).all(), (codec, k, p, s, u)
+
+
+@pytest.mark.parametrize("i", range(N_CASES // 2))
+def test_random_stripe_queue(i):
+    """The writer-side stripe queue (ozec_stripe_queue_*): random codec, cell length, batch size,
+    stripe lengths up to the cell, CRC type (or none) and wait pattern; every stripe's parity and CRCs vs the oracle."""
+    from ozone_amd.stripe_queue import StripeQueue
+    r = _rng(7, i)
+    codec, k, p = _codec(r)
+    cell = int(r.choice([4096, 65536, 200_000, 1 << 20]))
+    batch = int(r.integers(1, 9))
+    with_crc = bool(r.integers(0, 2))
+    ctype = (ck.ChecksumType.CRC32, ck.ChecksumType.CRC32C)[int(r.integers(0, 2))] if with_crc \
+        else ck.ChecksumType.NONE
+    bpc = int(r.choice([512, 4096, 16384]))
+    rows = p if codec == "rs" else 1
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec))
+    jobs = []
+    with StripeQueue(enc, cell, batch, ctype, bpc) as q:
+        for s in range(int(r.integers(1, 3 * batch + 3))):
+            n = int(r.choice([cell, int(r.integers(1, cell + 1))]))
+            d = _cells(r, k, n)
+            par = [np.full(n, 0xA5, np.uint8) for _ in range(p)]
+            crcs = np.zeros((k + rows) * -(-n // bpc), np.uint32) if with_crc else None
+            jobs.append((q.submit(d, par, crcs=crcs), d, par, crcs, n))
+            if r.random() < 0.2:
+                q.wait(jobs[int(r.integers(0, len(jobs)))][0])
+        q.wait(jobs[-1][0])
+    for t, d, par, crcs, n in jobs:
+        ref = _parity(codec, k, p, d)
+        assert all((a == b).all() for a, b in zip(par, ref)), (codec, k, p, cell, batch, t, n)
+        if with_crc:
+            got = crcs.reshape(k + rows, -1)
+            for u, x in enumerate(d + ref[:rows]):
+                assert (got[u] == oracle.crc_windows(_otype(ctype), x, bpc)).all(), (codec, k, p, t, n, u)

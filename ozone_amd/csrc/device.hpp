@@ -243,9 +243,6 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 // whatever the grid size or placement.  The counters are a slot leased for the launch (fused.hip work_lease):
 // the last wave of a launch to finish puts the slot back to zero, and the slot is reused only after an event recorded
 // behind the launch has completed.
-constexpr int kWqStride = 16;                 // ints between counters (64 B: one counter per cache line)
-constexpr int kWqDone = 8 * kWqStride;        // finished-wave counter
-constexpr int kWqInts = kWqDone + kWqStride;  // ints per slot
 struct WorkQueue {
   int32_t *ctr;
   int64_t units;

@@ -199,10 +199,14 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc);
 bool encode_crc_lv_supported(const EncCrcArgs &e);
 hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant);
 
-// WorkQueue counter slots of the persistent kernels (device.hpp WorkQueue; pool in fused.hip).  work_lease gives a
+// WorkQueue counter slots of the persistent kernels (device.hpp WorkQueue; pool in work_slots.cpp).  work_lease gives a
 // zeroed slot of the current device, not in use by any launch still running, or null (capturing stream, pool full,
 // allocation failure: the caller takes a non-persistent form); work_return hands it back, `used` when a kernel that
 // counts on it was enqueued on `st` (an event recorded behind it gates the next lease).
+// counter slot layout (device.hpp WorkQueue)
+constexpr int kWqStride = 16;                 // ints between counters (64 B: one counter per cache line)
+constexpr int kWqDone = 8 * kWqStride;        // finished-wave counter
+constexpr int kWqInts = kWqDone + kWqStride;  // ints per slot
 struct WorkSlot {
   int device = -1;
   int32_t *ctr = nullptr;

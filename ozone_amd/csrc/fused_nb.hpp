@@ -331,16 +331,16 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
       // persistent: one resident set of workgroups (occupancy x CUs), each building its tables once; the caller has
       // leased the WorkQueue counter slot (e.work, fused.hip work_lease)
       if (e.work == nullptr || units > (int64_t{1} << 30)) return hipErrorInvalidValue;
-      static int resident = 0;  // per instantiation and process (one device type)
-      if (resident == 0) {
+      static std::atomic<int> resident{0};  // per instantiation and process (one device type)
+      if (resident.load(std::memory_order_relaxed) == 0) {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WPB * 64, 0) != hipSuccess)
           return hipErrorInvalidValue;
-        resident = std::max(1, cus * std::max(1, per_cu));
+        resident.store(std::max(1, cus * std::max(1, per_cu)), std::memory_order_relaxed);
       }
-      g = std::min<int64_t>(resident, blocks);
+      g = std::min<int64_t>(resident.load(std::memory_order_relaxed), blocks);
     }
     // non-persistent: one wave per (stripe, window) unit, no grid-stride: every workgroup builds its K*D*4 KiB of
     // tables, and the dispatcher's refill of finished workgroups balances the CUs.  Measured on MI355X against a

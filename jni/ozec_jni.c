@@ -10,7 +10,7 @@
  *   encodeDirect / decodeDirect   <- AbstractNativeRawEncoder.doEncode :49-73 / AbstractNativeRawDecoder.doDecode :49-75
  *                                    -> hadoop's performEncodeImpl / performDecodeImpl (HadoopNativeECAccessorUtil :32-58)
  *   encodeArrays / decodeArrays   <- doEncode(ByteArrayEncodingState) / doDecode(ByteArrayDecodingState); the reference
- *                                    copies heap arrays into direct buffers (:80-93), here into a per-thread pinned
+ *                                    copies heap arrays into direct buffers (:80-93), here into a pooled pinned
  *                                    arena (GetByteArrayRegion / SetByteArrayRegion, never a critical pin across
  *                                    device work: heap_* below)
  *   coderCreate / coderRelease    <- NativeRSRawEncoder ctor / release (EC/rawcoder/NativeRSRawEncoder.java:39-62)
@@ -107,62 +107,77 @@ static void refs_free(JNIEnv *env, array_set *as) {
 /* ---------------------------------------------------------------- heap arrays: copied, never pinned across the GPU
  * A byte[] pinned with GetPrimitiveArrayCritical for the whole call would hold the VM's GC locker through staging, H2D,
  * kernel and D2H (~0.3 ms per rs-6-3 stripe of 1 MiB cells; every ECKeyOutputStream writer passes heap buffers,
- * ECKeyOutputStream.java:701).  Instead each call copies the regions it reads with GetByteArrayRegion into this
- * thread's pinned arena (ozec_host_alloc: pinned, on the device's NUMA node), runs on the arena -- libozec DMAs pinned
- * memory in place, one rectangular copy each way for cells at one stride -- and copies the outputs back with
- * SetByteArrayRegion: the two host copies libozec's own staging would make, with no JNI pin while libozec works, as the
- * reference's bridge copies heap arrays into direct buffers (AbstractNativeRawEncoder.java:80-93).  Calls are cut in
- * column chunks of HEAP_CHUNK bytes per cell (coding is byte-position-wise), so the arena stays at (k + p) x 4 MiB. */
+ * ECKeyOutputStream.java:701).  Instead each call copies the regions it reads with GetByteArrayRegion into a pinned
+ * arena (ozec_host_alloc: pinned, on a listed GPU's NUMA node), runs on the arena -- libozec DMAs pinned memory in
+ * place, one rectangular copy each way for cells at one stride -- and copies the outputs back with SetByteArrayRegion:
+ * the two host copies libozec's own staging would make, with no JNI pin while libozec works, as the reference's bridge
+ * copies heap arrays into direct buffers (AbstractNativeRawEncoder.java:80-93).  Calls are cut in column chunks of
+ * HEAP_CHUNK bytes per cell (coding is byte-position-wise), so an arena holds at most (k + p) x 4 MiB.
+ * Arenas come from a process-wide pool of ARENA_POOL, leased for one call: pinned memory stays bounded however many
+ * Java threads call at once; a call that finds every arena leased gets a pageable one of its own (libozec then stages
+ * it through its pinned slots), so no call waits for another. */
 #define HEAP_CHUNK ((int64_t)4 << 20)
 #define ARENA_ALIGN 256
+#define ARENA_POOL 32
 
 typedef struct {
   uint8_t *p;
   size_t cap;
 } arena_t;
 
-static pthread_key_t g_arena_key;
-static pthread_once_t g_arena_once = PTHREAD_ONCE_INIT;
-static int g_arena_key_ok;
+typedef struct {
+  int slot;    /* index into g_arenas, or -1: `own` (pool exhausted) */
+  arena_t own; /* pageable, freed at release */
+} arena_lease;
 
-static void arena_destroy(void *v) {
-  arena_t *a = (arena_t *)v;
-  if (!a) return;
-  if (a->p) (void)ozec_host_free(a->p);
-  free(a);
+static pthread_mutex_t g_arena_mu = PTHREAD_MUTEX_INITIALIZER;
+static arena_t g_arenas[ARENA_POOL];
+static int g_arena_leased[ARENA_POOL];
+
+/* a free pooled arena (the largest, to spare reallocations), or a call-owned pageable one */
+static void arena_lease_begin(arena_lease *l) {
+  l->slot = -1;
+  l->own.p = NULL;
+  l->own.cap = 0;
+  pthread_mutex_lock(&g_arena_mu);
+  for (int i = 0; i < ARENA_POOL; ++i)
+    if (!g_arena_leased[i] && (l->slot < 0 || g_arenas[i].cap > g_arenas[l->slot].cap)) l->slot = i;
+  if (l->slot >= 0) g_arena_leased[l->slot] = 1;
+  pthread_mutex_unlock(&g_arena_mu);
 }
 
-static void arena_make_key(void) { g_arena_key_ok = pthread_key_create(&g_arena_key, arena_destroy) == 0; }
+static void arena_lease_end(arena_lease *l) {
+  if (l->slot < 0) {
+    free(l->own.p);
+    return;
+  }
+  pthread_mutex_lock(&g_arena_mu);
+  g_arena_leased[l->slot] = 0;
+  pthread_mutex_unlock(&g_arena_mu);
+}
 
-/* this thread's pinned arena of at least `bytes`, NULL (status set) when it cannot be had */
-static uint8_t *arena(size_t bytes, ozm_status *st) {
-  (void)pthread_once(&g_arena_once, arena_make_key);
-  if (!g_arena_key_ok) {
-    ozm_fail(OZEC_ENOMEM, "no thread-local arena", st);
+/* the leased arena, grown to at least `bytes`; NULL (status set) when it cannot be had */
+static uint8_t *arena(arena_lease *l, size_t bytes, ozm_status *st) {
+  arena_t *a = l->slot >= 0 ? &g_arenas[l->slot] : &l->own;
+  if (a->cap >= bytes) return a->p;
+  const size_t cap = (bytes + ((size_t)1 << 20) - 1) >> 20 << 20;
+  if (l->slot < 0) {
+    free(a->p);
+    a->p = (uint8_t *)aligned_alloc(ARENA_ALIGN, cap);
+    a->cap = a->p ? cap : 0;
+    if (!a->p) ozm_fail(OZEC_ENOMEM, "out of memory", st);
+    return a->p;
+  }
+  if (a->p) (void)ozec_host_free(a->p);
+  a->p = NULL;
+  a->cap = 0;
+  int rc = ozec_host_alloc(cap, (void **)&a->p);
+  if (rc) {
+    a->p = NULL;
+    ozm_fail(rc, NULL, st);
     return NULL;
   }
-  arena_t *a = (arena_t *)pthread_getspecific(g_arena_key);
-  if (!a) {
-    a = (arena_t *)calloc(1, sizeof *a);
-    if (!a || pthread_setspecific(g_arena_key, a) != 0) {
-      free(a);
-      ozm_fail(OZEC_ENOMEM, "no thread-local arena", st);
-      return NULL;
-    }
-  }
-  if (a->cap < bytes) {
-    if (a->p) (void)ozec_host_free(a->p);
-    a->p = NULL;
-    a->cap = 0;
-    const size_t cap = (bytes + ((size_t)1 << 20) - 1) >> 20 << 20;
-    int rc = ozec_host_alloc(cap, (void **)&a->p);
-    if (rc) {
-      a->p = NULL;
-      ozm_fail(rc, NULL, st);
-      return NULL;
-    }
-    a->cap = cap;
-  }
+  a->cap = cap;
   return a->p;
 }
 
@@ -212,19 +227,25 @@ static int heap_code(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_
                      const ozm_buf *ob, const int *erased, int ne, int64_t len, ozm_status *st) {
   ozm_buf si[MAX_BUFS], so[MAX_BUFS];
   const int nin = present_count(ai);
-  for (int64_t off = 0; off < len; off += HEAP_CHUNK) {
+  arena_lease l;
+  arena_lease_begin(&l);
+  int rc = 0;
+  for (int64_t off = 0; off < len && !rc; off += HEAP_CHUNK) {
     const int64_t cl = len - off < HEAP_CHUNK ? len - off : HEAP_CHUNK;
     const int64_t stride = round_up(cl, ARENA_ALIGN);
-    uint8_t *a = arena((size_t)((int64_t)(nin + ao->n) * stride), st);
-    if (!a) return st->code;
+    uint8_t *a = arena(&l, (size_t)((int64_t)(nin + ao->n) * stride), st);
+    if (!a) {
+      rc = st->code;
+      break;
+    }
     copy_in(env, ai, ib, off, cl, a, stride, 0, si);
     out_slots(ao, cl, a, stride, nin, so);
-    int rc = erased ? ozm_decode(h, si, ai->n, erased, ne, so, ao->n, cl, st)
-                    : ozm_encode(h, si, ai->n, so, ao->n, cl, st);
-    if (rc) return rc;
-    copy_out(env, ao, ob, off, cl, so);
+    rc = erased ? ozm_decode(h, si, ai->n, erased, ne, so, ao->n, cl, st)
+                : ozm_encode(h, si, ai->n, so, ao->n, cl, st);
+    if (!rc) copy_out(env, ao, ob, off, cl, so);
   }
-  return 0;
+  arena_lease_end(&l);
+  return rc;
 }
 
 static int int_array(JNIEnv *env, jintArray a, int *out, int max, int *n, ozm_status *st) {
@@ -411,9 +432,11 @@ JNIEXPORT jint JNICALL JNI_FN(crcUpdateArray)(JNIEnv *env, jclass cls, jint type
     b.base = (void *)arr; /* a placeholder address for the check: never read */
     const uint8_t *unused;
     rc = len == 0 ? 0 : ozm_resolve(&b, 1, 0, len, &unused, &st);
+    arena_lease l;
+    arena_lease_begin(&l);
     for (int64_t o = 0; !rc && o < len; o += HEAP_CHUNK) {
       const int64_t cl = len - o < HEAP_CHUNK ? len - o : HEAP_CHUNK;
-      uint8_t *a = arena((size_t)cl, &st);
+      uint8_t *a = arena(&l, (size_t)cl, &st);
       if (!a) {
         rc = st.code;
         break;
@@ -422,6 +445,7 @@ JNIEXPORT jint JNICALL JNI_FN(crcUpdateArray)(JNIEnv *env, jclass cls, jint type
       ozm_buf c = {a, 0, cl, 1};
       rc = ozm_crc_update(type, &s, &c, cl, &st);
     }
+    arena_lease_end(&l);
   }
   if (rc) throw_status(env, &st);
   return (jint)s;
@@ -458,10 +482,12 @@ static jint checksum_windows(JNIEnv *env, jint type, jobject direct, jbyteArray 
     rc = ozm_fail(OZEC_EINVAL, "checksum output too small", &st);
   /* whole windows per round trip (at least one): the arena holds the chunk's data (byte[] only) and its CRCs */
   const int64_t chunk = bpc <= 0 ? 1 : HEAP_CHUNK < bpc ? bpc : HEAP_CHUNK / bpc * bpc;
+  arena_lease l;
+  arena_lease_begin(&l);
   for (int64_t o = 0; !rc && o < len; o += chunk) {
     const int64_t cl = len - o < chunk ? len - o : chunk;
     const int64_t nw = (cl + bpc - 1) / bpc, dbytes = direct ? 0 : round_up(cl, ARENA_ALIGN);
-    uint8_t *a = arena((size_t)(dbytes + 4 * nw), &st);
+    uint8_t *a = arena(&l, (size_t)(dbytes + 4 * nw), &st);
     if (!a) {
       rc = st.code;
       break;
@@ -482,6 +508,7 @@ static jint checksum_windows(JNIEnv *env, jint type, jobject direct, jbyteArray 
       total += written;
     }
   }
+  arena_lease_end(&l);
   if (rc) throw_status(env, &st);
   return (jint)total;
 }

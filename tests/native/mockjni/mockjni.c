@@ -229,6 +229,24 @@ int __wrap_ozec_checksum_windows(int t, const uint8_t *d, size_t len, size_t bpc
   at_device_call();
   return __real_ozec_checksum_windows(t, d, len, bpc, out, be);
 }
+/* pinned allocations of the glue's arenas (ozec_host_alloc / ozec_host_free, wrapped): calls and live count */
+static int g_host_allocs = 0, g_host_live = 0;
+int __real_ozec_host_alloc(size_t, void **);
+int __wrap_ozec_host_alloc(size_t bytes, void **out) {
+  int rc = __real_ozec_host_alloc(bytes, out);
+  if (rc == 0) {
+    __atomic_add_fetch(&g_host_allocs, 1, __ATOMIC_RELAXED);
+    __atomic_add_fetch(&g_host_live, 1, __ATOMIC_RELAXED);
+  }
+  return rc;
+}
+int __real_ozec_host_free(void *);
+int __wrap_ozec_host_free(void *p) {
+  if (p) __atomic_sub_fetch(&g_host_live, 1, __ATOMIC_RELAXED);
+  return __real_ozec_host_free(p);
+}
+int mock_host_allocs(void) { return __atomic_load_n(&g_host_allocs, __ATOMIC_RELAXED); }
+int mock_host_live(void) { return __atomic_load_n(&g_host_live, __ATOMIC_RELAXED); }
 int mock_local_refs(void) { return g_local_refs; }
 void mock_set_missing_class(const char *name) { snprintf(g_missing, sizeof g_missing, "%s", name ? name : ""); }
 

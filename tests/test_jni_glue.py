@@ -30,7 +30,8 @@ def J():
                     os.path.join(ROOT, "jni", "ozec_jni.c"), os.path.join(ROOT, "jni", "ozec_marshal.c"),
                     os.path.join(ROOT, "tests", "native", "mockjni", "mockjni.c"), "-L", LIBDIR, "-lozec",
                     # device-work entry points wrapped by the mock (pins outstanding at each call)
-                    "-Wl,--wrap=ozec_encode,--wrap=ozec_decode,--wrap=ozec_crc_update,--wrap=ozec_checksum_windows",
+                    "-Wl,--wrap=ozec_encode,--wrap=ozec_decode,--wrap=ozec_crc_update,--wrap=ozec_checksum_windows,"
+                    "--wrap=ozec_host_alloc,--wrap=ozec_host_free",
                     f"-Wl,-rpath,{LIBDIR}", "-o", so], check=True, capture_output=True, timeout=120)
     L = ctypes.CDLL(so)
     for name, res, args in [
@@ -40,7 +41,8 @@ def J():
         ("mock_pins", ctypes.c_int, []), ("mock_local_refs", ctypes.c_int, []),
         ("mock_pins_at_device_call", ctypes.c_int, []), ("mock_device_calls", ctypes.c_int, []),
         ("mock_reset_device_calls", None, []), ("mock_region_copies", ctypes.c_int, []),
-        ("mock_set_missing_class", None, [ctypes.c_char_p]),
+        ("mock_set_missing_class", None, [ctypes.c_char_p]), ("mock_host_allocs", ctypes.c_int, []),
+        ("mock_host_live", ctypes.c_int, []),
         ("mock_take_exception", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
         (P + "deviceCount", i32, [vp, vp]),
         (P + "setDevices", None, [vp, vp, vp]), (P + "getDevices", vp, [vp, vp]),
@@ -391,7 +393,7 @@ def test_device_list_natives(J, java):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [1 << 16, (4 << 20) + 4096 + 3])  # one chunk; two chunks of the 4 MiB arena
 def test_heap_arrays_never_pinned_across_device_work(J, java, n):
-    """byte[] inputs and outputs are copied (Get/SetByteArrayRegion) into the thread's pinned arena, and
+    """byte[] inputs and outputs are copied (Get/SetByteArrayRegion) into a pooled pinned arena, and
     no array is pinned while libozec works -- the mock records the array pins outstanding at every wrapped ozec_encode
     / ozec_decode / ozec_crc_update / ozec_checksum_windows call.  Results vs the oracle, calls longer than one arena
     chunk included, inputs untouched and outputs written only inside their regions."""
@@ -440,6 +442,36 @@ def test_heap_arrays_never_pinned_across_device_work(J, java, n):
     finally:
         call(J, "coderRelease", h)
         call(J, "coderRelease", hd)
+
+
+@pytest.mark.gpu
+def test_heap_arenas_are_pooled_across_threads(J, java):
+    """The pinned arenas heap-array calls copy through come from a bounded pool, not one per Java thread: 24 threads
+    calling one after another reuse one arena (no new pinned allocation after the first), and the results stay exact."""
+    import threading
+    k, p, n = 6, 3, 50_000
+    h = call(J, "coderCreate", 0, 0, k, p)
+    try:
+        d = cells(SEED, 748000, k, n)
+        ref = oracle.rs_encode(k, p, d)
+
+        def one():
+            outs = [np.zeros(n, np.uint8) for _ in range(p)]
+            call(J, "encodeArrays", h, java.array([java.bytes(x) for x in d]), java.ints([0] * k), n,
+                 java.array([java.bytes(x) for x in outs]), java.ints([0] * p))
+            assert java.exception() is None
+            assert all((o == r).all() for o, r in zip(outs, ref))
+
+        one()  # the first call sizes an arena
+        allocs0, live0 = J.mock_host_allocs(), J.mock_host_live()
+        for _ in range(24):
+            t = threading.Thread(target=one)
+            t.start()
+            t.join()
+        assert J.mock_host_allocs() == allocs0, "a thread got a pinned arena of its own"
+        assert J.mock_host_live() == live0
+    finally:
+        call(J, "coderRelease", h)
 
 
 @pytest.mark.gpu

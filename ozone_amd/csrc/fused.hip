@@ -234,12 +234,22 @@ hipError_t launch_lv_kr(const EncCrcArgs &e, hipStream_t st, int v) {
 
 }  // namespace
 
-bool encode_crc_lv_supported(const EncCrcArgs &e) {
-  const CodeArgs &a = e.code;
+namespace {
+bool fused_shape(const CodeArgs &a) {
   if (a.all_ones && a.rows == 1) return false;  // the XOR codec has its own register shortcut (encode_crc_g26 XORC)
-  const bool shape = (a.k == 6 && (a.rows == 3 || a.rows == 2)) || (a.k == 10 && a.rows >= 1 && a.rows <= 4) ||
-                     (a.k == 3 && a.rows == 2);
-  return shape && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && a.len % e.crc.bpc == 0;
+  return (a.k == 6 && (a.rows == 3 || a.rows == 2)) || (a.k == 10 && a.rows >= 1 && a.rows <= 4) ||
+         (a.k == 3 && a.rows == 2);
+}
+}  // namespace
+
+bool encode_crc_lv_supported(const EncCrcArgs &e) {
+  return fused_shape(e.code) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc == 0;
+}
+
+// the nibble kernel also takes a short last window, when it is a whole number of two-step groups (2 KiB): cells of
+// rs-3-2-1524k with 16 KiB windows end in a 4 KiB window (ECBlockChecksumComputer.java:160-166)
+bool encode_crc_nb_supported(const EncCrcArgs &e) {
+  return fused_shape(e.code) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc % 2048 == 0;
 }
 
 namespace {

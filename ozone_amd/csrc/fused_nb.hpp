@@ -171,7 +171,6 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   const int64_t nwin = cr.nwin;
   const int64_t units = a.nstripes * nwin;
   const int32_t T = static_cast<int32_t>(cr.bpc >> 10);  // steps per window
-  const int32_t G = T / D;                                // step groups per window
   const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
   uint32_t v4, vf0;  // index-op operands in VGPRs (VOP2/SDWA with no SGPR or literal operand issue fastest)
   asm volatile("v_mov_b32 %0, 4" : "=v"(v4));
@@ -192,7 +191,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     const int64_t w = uniform64(u - s * nwin);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
     const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
-    auto vstep = [&](int32_t t) { return voff + (t < T ? static_cast<uint32_t>(t) * 1024u : 0x80000000u); };
+    // steps of this window: a cell's last window may be short (a whole number of D-KiB steps, nb_supported in
+    // fused.hip); loads past it are addressed outside the input descriptor (zeros, no memory access)
+    const int32_t Tu = w == nwin - 1 ? static_cast<int32_t>((a.len - w * cr.bpc) >> 10) : T;
+    const int32_t Gu = Tu / D;
+    auto vstep = [&](int32_t t) { return voff + (t < Tu ? static_cast<uint32_t>(t) * 1024u : 0x80000000u); };
     auto load = [&](uint32_t vo, int j) {
       const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, vo, static_cast<int>(a.in_off[j]), 2);
       return make_uint4(d[0], d[1], d[2], d[3]);
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     uint4 ring[NB];
 #pragma unroll
     for (int i = 0; i + 1 < NB; ++i) ring[i] = load(vstep(i / K), i % K);
-    for (int32_t g = 0; g < G; ++g) {
+    for (int32_t g = 0; g < Gu; ++g) {
 #pragma unroll
       for (int rr = 0; rr < D; ++rr) {
         const int32_t t = g * D + rr;
@@ -279,7 +282,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
           }
         }
       }
-      if (g + 1 < G) {
+      if (g + 1 < Gu) {
 #pragma unroll
         for (int q = 0; q < (XO ? K : K + R); ++q)
           S[q] = g5_shift(s_t + (q < H ? kShIn : q < K ? kSh1 : g26_gshift(D)), S[q]);

@@ -1065,10 +1065,13 @@ hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   if (e0.code.nstripes * e0.crc.nwin <= 0) return hipSuccess;
   EncCrcArgs e = e0;
   if (!rebase32(e.code)) return hipErrorInvalidValue;
-  // full windows of the RS shapes: the nibble-table kernel (fused.hip; 50-59 the streamed-input kernel); variant 49
-  // pins the per-window kernel
+  // the RS shapes with whole windows (or a short last window of whole 2 KiB groups): the nibble-table kernel
+  // (fused_nb.hpp); 56 / 59 the streamed-input kernel (full windows only); variant 49 pins the per-window kernel
   const int v = g_tune.crc_variant.load(std::memory_order_relaxed);
-  if ((v == 0 || (v >= 50 && v < 300)) && encode_crc_lv_supported(e)) return launch_encode_crc_lv(e, st, v);
+  if (v == 0 || (v >= 50 && v < 300)) {
+    const bool lv = v == 56 || v == 59;
+    if (lv ? encode_crc_lv_supported(e) : encode_crc_nb_supported(e)) return launch_encode_crc_lv(e, st, v);
+  }
   const int k = e.code.k, r = e.code.rows;
 #define OZEC_SHAPE_LAUNCH(KK, RR) \
   if (k == KK && r == RR) return launch_enc_crc_kr<KK, RR>(e, st);

@@ -410,14 +410,17 @@ def test_encode_crc_xor_free_shift_vs_oracle(variant, k, n, bpc, S, ctype, otype
 
 @pytest.mark.parametrize("variant", [v for v in variants.RS_FUSED if v >= 62])
 @pytest.mark.parametrize("k,p,n,bpc,S", [(6, 3, 1 << 17, 16384, 3), (10, 4, 1 << 16, 4096, 2), (3, 2, 1 << 17, 8192, 3),
-                                         (6, 2, 1 << 15, 32768, 2), (10, 1, 1 << 16, 16384, 2)])
+                                         (6, 2, 1 << 15, 32768, 2), (10, 1, 1 << 16, 16384, 2),
+                                         # short last windows of whole 2 KiB groups (rs-3-2-1524k: a 4 KiB last window)
+                                         (6, 3, 3 * 16384 + 4096, 16384, 2), (10, 4, 5 * 4096 + 2048, 4096, 2),
+                                         (3, 2, 1524 * 1024, 16384, 2)])
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
 def test_encode_crc_nibble_kernel_vs_oracle(variant, k, p, n, bpc, S, ctype, otype):
     """The nibble-table fused kernel (fused_nb.hpp encode_crc_nb, every alternate the library holds) for both CRC types
-    and every RS shape it takes, bit-exact vs the oracle."""
+    and every RS shape it takes, whole windows and a short last window, bit-exact vs the oracle."""
     lib = L.lib()
     data = np.stack([np.stack(cells(SEED, 54000 + s * k, k, n)) for s in range(S)])
-    nwin = n // bpc
+    nwin = -(-n // bpc)
     d_out = torch.full((S, p, n), 0xA5, dtype=torch.uint8, device=DEV)
     d_crc = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
     e = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))

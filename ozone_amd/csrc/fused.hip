@@ -235,21 +235,23 @@ hipError_t launch_lv_kr(const EncCrcArgs &e, hipStream_t st, int v) {
 }  // namespace
 
 namespace {
-bool fused_shape(const CodeArgs &a) {
+// nb: the nibble kernel's shapes (also rs-6-x / rs-3-x with one output: single-unit reconstruction); else the
+// streamed-input kernel's
+bool fused_shape(const CodeArgs &a, bool nb) {
   if (a.all_ones && a.rows == 1) return false;  // the XOR codec has its own register shortcut (encode_crc_g26 XORC)
-  return (a.k == 6 && (a.rows == 3 || a.rows == 2)) || (a.k == 10 && a.rows >= 1 && a.rows <= 4) ||
-         (a.k == 3 && a.rows == 2);
+  return (a.k == 6 && (a.rows == 3 || a.rows == 2 || (nb && a.rows == 1))) ||
+         (a.k == 10 && a.rows >= 1 && a.rows <= 4) || (a.k == 3 && (a.rows == 2 || (nb && a.rows == 1)));
 }
 }  // namespace
 
 bool encode_crc_lv_supported(const EncCrcArgs &e) {
-  return fused_shape(e.code) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc == 0;
+  return fused_shape(e.code, false) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc == 0;
 }
 
 // the nibble kernel also takes a short last window, when it is a whole number of two-step groups (2 KiB): cells of
 // rs-3-2-1524k with 16 KiB windows end in a 4 KiB window (ECBlockChecksumComputer.java:160-166)
 bool encode_crc_nb_supported(const EncCrcArgs &e) {
-  return fused_shape(e.code) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc % 2048 == 0;
+  return fused_shape(e.code, true) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc % 2048 == 0;
 }
 
 namespace {
@@ -258,7 +260,9 @@ hipError_t launch_nb_shape(const EncCrcArgs &e, hipStream_t st, int v) {
   const int k = e.code.k, r = e.code.rows;
   if (k == 6 && r == 3) return launch_nb_6_3(e, st, v);
   if (k == 6 && r == 2) return launch_nb_6_2(e, st, v);
+  if (k == 6 && r == 1) return launch_nb_6_1(e, st, v);
   if (k == 3 && r == 2) return launch_nb_3_2(e, st, v);
+  if (k == 3 && r == 1) return launch_nb_3_1(e, st, v);
   if (k == 10 && r == 4) return launch_nb_10_4(e, st, v);
   if (k == 10 && r == 3) return launch_nb_10_3(e, st, v);
   if (k == 10 && r == 2) return launch_nb_10_2(e, st, v);

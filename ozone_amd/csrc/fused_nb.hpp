@@ -1,5 +1,5 @@
 // Nibble-table fused kernel (encode_crc_nb) and its launcher, instantiated per (K, R) shape in its own translation
-// unit (fused_nb_<K>_<R>.hip) so the variants of the seven shapes compile in parallel; fused.hip dispatches.
+// unit (fused_nb_<K>_<R>.hip) so the variants of the nine shapes compile in parallel; fused.hip dispatches.
 #pragma once
 #include <algorithm>
 
@@ -8,7 +8,7 @@
 namespace ozec {
 
 
-#define OZEC_NB_SHAPES(X) X(6, 3) X(6, 2) X(3, 2) X(10, 4) X(10, 3) X(10, 2) X(10, 1)
+#define OZEC_NB_SHAPES(X) X(6, 3) X(6, 2) X(6, 1) X(3, 2) X(3, 1) X(10, 4) X(10, 3) X(10, 2) X(10, 1)
 #define OZEC_NB_DECL(K, R) hipError_t launch_nb_##K##_##R(const EncCrcArgs &e, hipStream_t st, int v);
 OZEC_NB_SHAPES(OZEC_NB_DECL)
 

@@ -1,0 +1,6 @@
+// encode_crc_nb variants of the rs-6-1 shape (fused_nb.hpp): single-unit reconstruction of rs-6-x
+#include "fused_nb.hpp"
+
+namespace ozec {
+hipError_t launch_nb_6_1(const EncCrcArgs &e, hipStream_t st, int v) { return launch_nb_kr<6, 1>(e, st, v); }
+}  // namespace ozec

@@ -67,6 +67,7 @@ def _stripe_units(codec, k, p, n, S, first):
     ("rs", 6, 3, [0, 2, 7], 50000, 1000),         # unfused fallback (bpc not a multiple of 16)
     ("rs", 10, 4, [1, 4, 10, 13], 8 * 16384 + 2048, 16384),  # nibble kernel, short last window (2 KiB)
     ("rs", 3, 2, [0, 4], 1524 * 1024, 16384),     # rs-3-2-1524k: a 4 KiB last window
+    ("rs", 3, 2, [4], 1 << 16, 16384),            # fused shape (3,1): single-unit reconstruction
 ])
 @pytest.mark.parametrize("variant", [0] + variants.RS_FUSED + [4, 5])
 def test_reconstruct_crc_batch(codec, k, p, erased, n, bpc, variant):

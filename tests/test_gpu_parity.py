@@ -413,7 +413,9 @@ def test_encode_crc_xor_free_shift_vs_oracle(variant, k, n, bpc, S, ctype, otype
                                          (6, 2, 1 << 15, 32768, 2), (10, 1, 1 << 16, 16384, 2),
                                          # short last windows of whole 2 KiB groups (rs-3-2-1524k: a 4 KiB last window)
                                          (6, 3, 3 * 16384 + 4096, 16384, 2), (10, 4, 5 * 4096 + 2048, 4096, 2),
-                                         (3, 2, 1524 * 1024, 16384, 2)])
+                                         (3, 2, 1524 * 1024, 16384, 2),
+                                         # one output: single-unit reconstruction of rs-6-x / rs-3-x
+                                         (6, 1, 1 << 16, 16384, 2), (3, 1, 1 << 16, 8192, 2)])
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
 def test_encode_crc_nibble_kernel_vs_oracle(variant, k, p, n, bpc, S, ctype, otype):
     """The nibble-table fused kernel (fused_nb.hpp encode_crc_nb, every alternate the library holds) for both CRC types

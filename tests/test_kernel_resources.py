@@ -26,12 +26,12 @@ def _nb(K, R, D, NB, WPB, DYN, H):
 
 
 def _defaults():
-    """fused.hip: rs-10-x 177 (queue) / 173, rs-6-x 171 / 174, rs-3-x 172 / 174 (fused_nb.hpp launch_nb_kr)."""
+    """fused.hip: rs-10-x 177 (queue) / 173, rs-6-x 171 / 174, rs-3-x 172 / 174 (fused_nb.hpp launch_nb_kr), x = 1-4."""
     out = [_nb(10, R, 2, 5, 16, 1, 5) for R in (1, 2, 3, 4)]     # 177
     out += [_nb(10, R, 1, 5, 8, 0, 10) for R in (1, 2, 3, 4)]    # 173
-    out += [_nb(6, R, 2, 3, 16, 1, 6) for R in (2, 3)]   # 171
-    out += [_nb(6, R, 2, 2, 12, 0, 6) for R in (2, 3)]   # 174 (kD2 = 2 for K = 6)
-    out += [_nb(3, 2, 2, 2, 16, 1, 3), _nb(3, 2, 2, 2, 12, 0, 3)]  # 172, 174
+    out += [_nb(6, R, 2, 3, 16, 1, 6) for R in (1, 2, 3)]   # 171
+    out += [_nb(6, R, 2, 2, 12, 0, 6) for R in (1, 2, 3)]   # 174 (kD2 = 2 for K = 6)
+    out += [_nb(3, R, 2, 2, 16, 1, 3) for R in (1, 2)] + [_nb(3, R, 2, 2, 12, 0, 3) for R in (1, 2)]  # 172, 174
     return out
 
 

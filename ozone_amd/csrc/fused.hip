@@ -248,10 +248,11 @@ bool encode_crc_lv_supported(const EncCrcArgs &e) {
   return fused_shape(e.code, false) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc == 0;
 }
 
-// the nibble kernel also takes a short last window, when it is a whole number of two-step groups (2 KiB): cells of
-// rs-3-2-1524k with 16 KiB windows end in a 4 KiB window (ECBlockChecksumComputer.java:160-166)
+// the nibble kernel also takes a short last window of any whole number of 16-B blocks, front-padded with virtual zero
+// blocks to whole step groups (fused_nb.hpp): cells of rs-3-2-1524k with 16 KiB windows end in a 4 KiB window
+// (ECBlockChecksumComputer.java:160-166), the last stripe of a block group in a cell of any length
 bool encode_crc_nb_supported(const EncCrcArgs &e) {
-  return fused_shape(e.code, true) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc % 2048 == 0;
+  return fused_shape(e.code, true) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len > 0 && e.code.len % 16 == 0;
 }
 
 namespace {

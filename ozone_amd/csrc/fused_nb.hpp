@@ -31,7 +31,8 @@ namespace {
 // with the tables of p and p ^ 1 interleaved (+0 / +8): under ds_read_b64 banking ((a/4) mod 64) the 16 entries
 // of a table cover 32 distinct banks, so random nibbles never conflict.  K*D*4 KiB of LDS (40 KiB for rs-10-4 at
 // D = 1), built once per workgroup; the grid is persistent (one resident set of workgroups).
-// Windows must be full and a whole number of D-step groups, as for encode_crc_lv.
+// Windows are a whole number of D-step groups (bpc a multiple of 4 KiB); a cell's short last window is front-padded
+// with virtual zero blocks to whole groups (below).
 __device__ __forceinline__ uint32_t nib_lo_idx(uint32_t w, int q, uint32_t v4) {  // ((byte_q << 4) & 0xf0)
   uint32_t d;
   switch (q) {
@@ -178,7 +179,13 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   int64_t off_max = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
-  const uint32_t in_extent = static_cast<uint32_t>(off_max + cr.bpc);
+  // descriptor ranges end with the last unit's window (rebase32: offset + cell length < 2^31)
+  const int64_t wmax = cr.bpc < a.len ? cr.bpc : a.len;
+  const uint32_t in_extent = static_cast<uint32_t>(off_max + wmax);
+  int64_t out_max = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) out_max = a.out_off[r] > out_max ? a.out_off[r] : out_max;
+  const uint32_t out_extent = static_cast<uint32_t>(out_max + wmax);
   const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   WorkQueue wq{e.work, units, static_cast<int>(blockIdx.x & 7), 0};
   int64_t u = DYN == 1 ? wq.next(lane) : bid * WPB + wave;
@@ -190,12 +197,24 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     const int64_t s = uniform64(u / nwin);
     const int64_t w = uniform64(u - s * nwin);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
-    // steps of this window: a cell's last window may be short (a whole number of D-KiB steps, nb_supported in
-    // fused.hip); loads past it are addressed outside the input descriptor (zeros, no memory access)
-    const int32_t Tu = w == nwin - 1 ? static_cast<int32_t>((a.len - w * cr.bpc) >> 10) : T;
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(a.out + out_off(a, s) + w * cr.bpc, out_extent);
+    // steps of this window: a cell's last window may be short (any whole number of 16-B blocks, nb_supported in
+    // fused.hip).  It is run as whole D-step groups with Pb virtual zero blocks in front, as the per-window kernel
+    // does: a zero block leaves a zero CRC register at zero and has zero GF products, and the blocks after it keep
+    // their distance to the window end.  Virtual blocks and the look-ahead past the window are addressed outside
+    // both descriptors: their loads return zeros without a memory access and their stores are dropped.
+    int32_t Tu = T, Pb = 0;
+    if (w == nwin - 1) {
+      const int32_t mb = static_cast<int32_t>((a.len - w * cr.bpc) >> 4);
+      Tu = (mb + 64 * D - 1) / (64 * D) * D;
+      Pb = Tu * 64 - mb;
+    }
     const int32_t Gu = Tu / D;
-    auto vstep = [&](int32_t t) { return voff + (t < Tu ? static_cast<uint32_t>(t) * 1024u : 0x80000000u); };
+    const int32_t vbase = static_cast<int32_t>(voff) - Pb * 16;  // lane's byte offset at step 0 (< 0: virtual)
+    auto vstep = [&](int32_t t) {
+      const int32_t o = vbase + t * 1024;
+      return t < Tu && o >= 0 ? static_cast<uint32_t>(o) : 0x80000000u;
+    };
     auto load = [&](uint32_t vo, int j) {
       const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, vo, static_cast<int>(a.in_off[j]), 2);
       return make_uint4(d[0], d[1], d[2], d[3]);

@@ -1065,7 +1065,7 @@ hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   if (e0.code.nstripes * e0.crc.nwin <= 0) return hipSuccess;
   EncCrcArgs e = e0;
   if (!rebase32(e.code)) return hipErrorInvalidValue;
-  // the RS shapes with whole windows (or a short last window of whole 2 KiB groups): the nibble-table kernel
+  // the RS shapes with whole windows and a short last window of any whole number of blocks: the nibble-table kernel
   // (fused_nb.hpp); 56 / 59 the streamed-input kernel (full windows only); variant 49 pins the per-window kernel
   const int v = g_tune.crc_variant.load(std::memory_order_relaxed);
   if (v == 0 || (v >= 50 && v < 300)) {

@@ -197,7 +197,7 @@ hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t nc
 bool encode_crc_supported(const CodeArgs &a, int64_t bpc);
 // the streamed-input fused kernel (fused.hip): RS shapes with full windows, bpc % 4096 == 0; `e` already rebased
 bool encode_crc_lv_supported(const EncCrcArgs &e);
-// the nibble-table kernel (fused_nb.hpp): the same shapes, and a short last window of whole 2 KiB groups
+// the nibble-table kernel (fused_nb.hpp): the same shapes, and a short last window of any whole number of 16-B blocks
 bool encode_crc_nb_supported(const EncCrcArgs &e);
 hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant);
 

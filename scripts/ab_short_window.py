@@ -2,7 +2,9 @@
 16 KiB windows, a 4 KiB last window; ECBlockChecksumComputer.java:160-166) and rs-6-3-1524k, device-resident.
 Variant 0 (the nibble kernel, which takes short last windows since round 4) against 49 (the per-window kernel that
 took them before), interleaved rounds, HIP events on the launch stream; prints one JSON line per (shape, variant).
-usage: python scripts/ab_short_window.py [ROUNDS]"""
+CELL (bytes, a multiple of 16) replaces 1524 KiB, e.g. 700000: 42 windows and an 11,872-B last window (a cell of the
+last, partial stripe of a block group; cells that are not whole 2 KiB groups take the nibble kernel since round 4).
+usage: python scripts/ab_short_window.py [ROUNDS [CELL]]"""
 import json
 import os
 import sys
@@ -16,7 +18,7 @@ from ozone_amd import checksum as ck  # noqa: E402
 from ozone_amd import rawcoder as rc  # noqa: E402
 
 ROUNDS = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-N, BPC = 1524 * 1024, 16384
+N, BPC = (int(sys.argv[2]) if len(sys.argv) > 2 else 1524 * 1024), 16384
 lib = L.lib()
 for k, p, S in ((3, 2, 4096), (6, 3, 2048)):
     nwin = -(-N // BPC)
@@ -50,7 +52,7 @@ for k, p, S in ((3, 2, 4096), (6, 3, 2048)):
         lib.ozec_set_tuning(b"crc_variant", 0)
     for v, ts in times.items():
         med = sorted(ts)[len(ts) // 2]
-        print(json.dumps({"shape": f"rs-{k}-{p}-1524k", "stripes": S, "crc_variant": v, "median_ms": round(med, 3),
+        print(json.dumps({"shape": f"rs-{k}-{p} cells of {N} B", "stripes": S, "crc_variant": v, "median_ms": round(med, 3),
                           "frac": round(alg / (med * 1e-3) / 8e12, 4)}), flush=True)
     del units, crcs
     torch.cuda.empty_cache()

@@ -68,6 +68,8 @@ def _stripe_units(codec, k, p, n, S, first):
     ("rs", 10, 4, [1, 4, 10, 13], 8 * 16384 + 2048, 16384),  # nibble kernel, short last window (2 KiB)
     ("rs", 3, 2, [0, 4], 1524 * 1024, 16384),     # rs-3-2-1524k: a 4 KiB last window
     ("rs", 3, 2, [4], 1 << 16, 16384),            # fused shape (3,1): single-unit reconstruction
+    ("rs", 6, 3, [2], 4 * 16384 + 3008, 16384),   # nibble kernel, a 3008-B last window (virtual zero blocks in front)
+    ("rs", 10, 4, [0, 5, 11], 3 * 16384 + 16, 16384),  # ... and a one-block last window
 ])
 @pytest.mark.parametrize("variant", [0] + variants.RS_FUSED + [4, 5])
 def test_reconstruct_crc_batch(codec, k, p, erased, n, bpc, variant):

@@ -414,6 +414,11 @@ def test_encode_crc_xor_free_shift_vs_oracle(variant, k, n, bpc, S, ctype, otype
                                          # short last windows of whole 2 KiB groups (rs-3-2-1524k: a 4 KiB last window)
                                          (6, 3, 3 * 16384 + 4096, 16384, 2), (10, 4, 5 * 4096 + 2048, 4096, 2),
                                          (3, 2, 1524 * 1024, 16384, 2),
+                                         # short last windows of any whole number of 16-B blocks (front-padded with
+                                         # virtual zero blocks), a cell of one short window, a cell of one block
+                                         (6, 3, 3 * 16384 + 1008, 16384, 2), (10, 4, 2 * 4096 + 16, 4096, 3),
+                                         (3, 2, 50000, 16384, 2), (10, 2, (1 << 16) + 2048 + 16, 16384, 2),
+                                         (6, 3, 4992, 16384, 2), (3, 1, 16, 4096, 2),
                                          # one output: single-unit reconstruction of rs-6-x / rs-3-x
                                          (6, 1, 1 << 16, 16384, 2), (3, 1, 1 << 16, 8192, 2)])
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])

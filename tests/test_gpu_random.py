@@ -8,6 +8,8 @@ Reference semantics followed: RSRawEncoder / RSRawDecoder (EC/rawcoder/RSRawDeco
 inputs), XORRawEncoder / XORRawDecoder (XORRawEncoder.java:39-85), Checksum.computeChecksum window split
 (CM/Checksum.java:157-200, short last window), ECReconstructionCoordinator's verify + decode + re-checksum.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -20,7 +22,7 @@ from ozone_amd import checksum as ck  # noqa: E402
 from ozone_amd import rawcoder as rc  # noqa: E402
 
 DEV = "cuda:0"
-N_CASES = 48
+N_CASES = int(os.environ.get("OZEC_RANDOM_CASES", "48"))  # draws per entry family (a wider sweep: e.g. 480)
 
 
 def _rng(tag, i):

@@ -172,6 +172,17 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   return b < (q << 3) ? (b & 7) * q + (b >> 3) : b;
 }
 
+// byte range of a stripe-side descriptor over n units at offsets off[0..n), each reached for `span` bytes: an access
+// past it returns zeros or is dropped instead of reaching other memory.  Every kernel bounds its indices itself; this
+// is the second fence (rebase32 keeps offset + span < 2^31).
+template <int N>
+__device__ __forceinline__ uint32_t unit_extent(const int64_t *off, int64_t span) {
+  int64_t mx = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) mx = off[i] > mx ? off[i] : mx;
+  return static_cast<uint32_t>(mx + span);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
   // raw buffer (stride 0), full 4 GiB range; bounds are checked explicitly by the kernels
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0xffffffff, 0x00020000);

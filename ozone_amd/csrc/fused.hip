@@ -79,6 +79,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
   for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
   const uint32_t in_extent = static_cast<uint32_t>(off_max + cr.bpc);
+  const uint32_t out_extent = unit_extent<R>(a.out_off, cr.bpc);
   const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   for (int64_t u = bid * WPB + wave; u < units; u += static_cast<int64_t>(gridDim.x) * WPB) {
     const int64_t s = u / nwin;
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     // loads past the window's last step get voffset + 2^31, outside the range: they return zeros and cost no
     // memory traffic (no 32-bit wrap: 2^31 + 1008 + in_off < 2^32)
     const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(a.out + out_off(a, s) + w * cr.bpc, out_extent);
     // step part of the address in a VGPR (one add per step), unit offset in soffset: K SGPRs in all, instead of
     // one SGPR per (step, unit) slot of the unrolled group
     auto vstep = [&](int32_t t) { return voff + (t < T ? static_cast<uint32_t>(t) * 1024u : 0x80000000u); };

@@ -66,13 +66,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
   const uint32_t cpc = (nvec + kChunk - 1) / kChunk;  // units per cell
   const uint32_t units = static_cast<uint32_t>(a.nstripes) * cpc;
   const uint32_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t in_extent = unit_extent<K>(a.in_off, a.len), out_extent = unit_extent<R>(a.out_off, a.len);
   for (uint32_t u = bid; u < units; u += gridDim.x) {
     if constexpr (!SREG) asm volatile("" ::: "memory");  // keep the LDS table reads inside the loop
     const uint32_t s = u / cpc;
     const uint32_t c = u - s * cpc;
     const uint32_t v0 = c * kChunk + threadIdx.x;
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, s));
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s));
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s), in_extent);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(a.out + out_off(a, s), out_extent);
     uint4 x[VPT][K];
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
@@ -487,6 +488,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
   const int64_t nwin = cr.nwin;
   const int64_t units = a.nstripes * nwin;
   const int64_t bid = a.unit_map == 1 ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t wmax = cr.bpc < a.len ? cr.bpc : a.len;  // bytes of a window
+  const uint32_t in_extent = unit_extent<K>(a.in_off, wmax), out_extent = unit_extent<R>(a.out_off, wmax);
   for (int64_t u = bid * (kBlock / 64) + wave; u < units; u += static_cast<int64_t>(gridDim.x) * (kBlock / 64)) {
     const int64_t s = u / nwin;
     const int64_t w = u - s * nwin;
@@ -495,8 +498,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     const int64_t m = N >> 4;
     const int32_t G = static_cast<int32_t>((m + 64 * D - 1) / (64 * D));
     const int32_t P = G * 64 * D - static_cast<int32_t>(m);  // window <= 2 GiB: 32-bit block indices
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, s) + w * cr.bpc);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, s) + w * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(a.out + out_off(a, s) + w * cr.bpc, out_extent);
     uint32_t S[K + R];
 #pragma unroll
     for (int q = 0; q < K + R; ++q) S[q] = 0;

@@ -662,7 +662,8 @@ __global__ __launch_bounds__(kBlock) void encode_xor_crc_g26s(const EncCrcArgs e
   // load cursor (wave-uniform): unit lu = (stripe ls, window lw), step lt
   int64_t lu = u0, ls = u0 / nwin, lw = u0 - ls * nwin;
   int32_t lt = 0;
-  __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, ls) + lw * cr.bpc);
+  const uint32_t in_extent = unit_extent<K>(a.in_off, cr.bpc), out_extent = unit_extent<1>(a.out_off, cr.bpc);
+  __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, ls) + lw * cr.bpc, in_extent);
   auto load_next = [&](uint4 (&dst)[K]) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -678,7 +679,7 @@ __global__ __launch_bounds__(kBlock) void encode_xor_crc_g26s(const EncCrcArgs e
         lw = 0;
         ++ls;
       }
-      rin = make_rsrc(a.in + in_off(a, ls) + lw * cr.bpc);
+      rin = make_rsrc_n(a.in + in_off(a, ls) + lw * cr.bpc, in_extent);
     }
   };
   uint4 x[NS][K];
@@ -686,7 +687,7 @@ __global__ __launch_bounds__(kBlock) void encode_xor_crc_g26s(const EncCrcArgs e
   for (int i = 0; i + 1 < NS; ++i) load_next(x[i]);
   int64_t cs = u0 / nwin, cw = u0 - cs * nwin;  // compute cursor
   for (int64_t u = u0; u < u1; ++u) {
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc(a.out + out_off(a, cs) + cw * cr.bpc);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(a.out + out_off(a, cs) + cw * cr.bpc, out_extent);
     uint32_t S[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) S[j] = 0;

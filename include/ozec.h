@@ -357,7 +357,8 @@ void ozec_stats_reset(void);
  * "unit_map"; 0 = default) and host-buffer staging ("host_chunk" bytes per unit per chunk, "host_chunk_shared" the
  * same while other host-buffer calls are in flight (0: always host_chunk), "host_slots", "copy_threads" = helper
  * threads for pageable <-> pinned copies, 0 = copy on the calling thread, "copy_stream" -1..3, "queue_batches",
- * "e2e_chunk", "e2e_rect").  OZEC_EINVAL for an unknown key, a value out of range, or a kernel variant the library
+ * "e2e_chunk", "e2e_rect", "host_graph" = bytes per unit up to which a one-chunk staged encode / decode replays a
+ * cached hipGraph of its H2D + kernel + D2H, default 256 KiB, 0 = off).  OZEC_EINVAL for an unknown key, a value out of range, or a kernel variant the library
  * does not hold. */
 int ozec_set_tuning(const char *key, int64_t value);
 /* the kernel variants "gf_variant" / "crc_variant" accept besides 0: writes up to cap ids, returns how many exist */

@@ -64,10 +64,40 @@ struct Slot {
   uint8_t *dbuf = nullptr;
   size_t dbuf_cap = 0;
   std::vector<hipEvent_t> events;
+  // host_graph: instantiated graphs of one-chunk staged calls (H2D + kernel + D2H on this slot's buffers), keyed by
+  // the bytes their launch depends on; dropped whenever the buffers move
+  struct Graph {
+    std::vector<uint8_t> key;
+    hipGraphExec_t exec;
+  };
+  std::vector<Graph> graphs;
+  size_t graph_next = 0;  // round-robin replacement once kMaxGraphs are held
+  static constexpr size_t kMaxGraphs = 8;
+
+  void drop_graphs() {
+    for (auto &g : graphs) (void)hipGraphExecDestroy(g.exec);
+    graphs.clear();
+    graph_next = 0;
+  }
+  hipGraphExec_t find_graph(const std::vector<uint8_t> &key) const {
+    for (const auto &g : graphs)
+      if (g.key == key) return g.exec;
+    return nullptr;
+  }
+  void keep_graph(std::vector<uint8_t> key, hipGraphExec_t exec) {
+    if (graphs.size() < kMaxGraphs) {
+      graphs.push_back({std::move(key), exec});
+      return;
+    }
+    Graph &g = graphs[graph_next++ % kMaxGraphs];
+    (void)hipGraphExecDestroy(g.exec);
+    g = {std::move(key), exec};
+  }
 
   // device buffer only (calls whose caller buffers are pinned need no staging)
   int reserve_device(size_t bytes) {
     if (bytes > dbuf_cap) {
+      drop_graphs();
       if (dbuf) (void)hipFree(dbuf);
       dbuf = nullptr;
       dbuf_cap = 0;
@@ -79,6 +109,7 @@ struct Slot {
   }
 
   int reserve(size_t bytes, size_t nevents) {
+    if (bytes > pinned_cap || bytes > dbuf_cap) drop_graphs();
     if (bytes > pinned_cap) {
       if (pinned) (void)ozec::pinned_free(pinned);
       pinned = nullptr;
@@ -107,6 +138,7 @@ struct Slot {
   // give the staging buffers back (an idle slot: its stream has drained)
   void shrink() {
     if (stream) (void)hipStreamSynchronize(stream);
+    drop_graphs();
     if (pinned) (void)ozec::pinned_free(pinned);
     if (dbuf) (void)hipFree(dbuf);
     pinned = dbuf = nullptr;
@@ -382,9 +414,13 @@ bool range_pinned(const void *p, size_t n) {
 // Chunk-major staging layout, chunk c at c * per_chunk: [nin inputs x Cp][nout outputs x Op].
 //   launch(d_in, in_stride, d_out, out_stride, off, cl, stream) enqueues the kernel for bytes [off, off+cl)
 //   out_bytes(cl) / out_pos(off) give the output bytes a chunk produces and where they go in each output
+//   gkey (optional): the bytes the launch depends on besides the slot's buffers and the chunk geometry; with it, a
+//   call of one staged chunk up to host_graph bytes per unit replays a cached graph of its three stream operations
+//   (one graph launch instead of three operations: 45 -> 34 us for a 64 KiB-cell rs-6-3 stripe)
 template <class Launch, class OutBytes, class OutPos>
 int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, size_t gran, int nout,
-                    uint8_t *const *out, OutBytes out_bytes, OutPos out_pos, Launch launch) {
+                    uint8_t *const *out, OutBytes out_bytes, OutPos out_pos, Launch launch,
+                    const std::vector<uint8_t> *gkey = nullptr) {
   constexpr size_t kMaxChunks = 64;
   SlotLease lease(ctx);
   if (int rc = ctx->acquire(&lease.slot)) return rc;
@@ -467,6 +503,40 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, shared, ctx->numa);
     return OZEC_OK;
   };
+  const int64_t graph_max = ozec::g_tune.host_graph.load(std::memory_order_relaxed);
+  if (gkey && nch == 1 && graph_max > 0 && len <= static_cast<size_t>(graph_max)) {
+    std::vector<uint8_t> key = *gkey;
+    const size_t geo[5] = {len, static_cast<size_t>(nin), static_cast<size_t>(nout), cp, op};
+    key.insert(key.end(), reinterpret_cast<const uint8_t *>(geo), reinterpret_cast<const uint8_t *>(geo + 5));
+    hipGraphExec_t ex = s->find_graph(key);
+    uint8_t *h = s->pinned, *d = s->dbuf;
+    if (!ex) {  // capture the chunk's three operations once; any failure falls back to the plain operations
+      hipGraph_t g = nullptr;
+      bool ok = hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+      if (ok) {
+        ok = hipMemcpyAsync(d, h, nin * cp, hipMemcpyHostToDevice, s->stream) == hipSuccess &&
+             launch(d, static_cast<int64_t>(cp), d + nin * cp, static_cast<int64_t>(op), 0, len, s->stream) == hipSuccess &&
+             hipMemcpyAsync(h + nin * cp, d + nin * cp, nout * op, hipMemcpyDeviceToHost, s->stream) == hipSuccess;
+        ok = hipStreamEndCapture(s->stream, &g) == hipSuccess && ok && g != nullptr;
+      }
+      if (ok) ok = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) == hipSuccess;
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+      if (ok) {
+        s->keep_graph(std::move(key), ex);
+      } else {
+        ex = nullptr;
+      }
+    }
+    if (ex) {
+      std::vector<ozec::CopyTask> tasks;
+      for (int j = 0; j < nin; ++j) tasks.push_back({h + j * cp, in[j], len});
+      ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, shared, ctx->numa);
+      OZEC_HIP(hipGraphLaunch(ex, s->stream));
+      OZEC_HIP(hipEventRecord(s->events[0], s->stream));
+      return unstage(0);
+    }
+  }
   for (size_t c = 0; c < nch; ++c) {
     const size_t off = c * chunk, cl = std::min(chunk, len - off);
     uint8_t *h = s->pinned + c * per_chunk, *d = s->dbuf + c * per_chunk;
@@ -485,6 +555,17 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
 
 // host-buffer coding job (encode / decode): rows outputs from nin inputs
 int staged_code(DevCtx *ctx, const CodeArgs &tmpl, const uint8_t *const *in, uint8_t *const *out, size_t len) {
+  // graph key: the coding parameters the kernel launch reads (the pointers and offsets are the slot's, set below)
+  std::vector<uint8_t> key;
+  auto put = [&key](const void *p, size_t n) {
+    key.insert(key.end(), static_cast<const uint8_t *>(p), static_cast<const uint8_t *>(p) + n);
+  };
+  const int32_t hdr[5] = {tmpl.k, tmpl.rows, tmpl.all_ones, tmpl.unit_map,
+                          ozec::g_tune.gf_variant.load(std::memory_order_relaxed)};
+  put(hdr, sizeof(hdr));
+  put(tmpl.coef, static_cast<size_t>(tmpl.k) * tmpl.rows * sizeof(tmpl.coef[0]));
+  const int64_t tail[2] = {ozec::g_tune.grid.load(std::memory_order_relaxed), tmpl.grp_stripes};
+  put(tail, sizeof(tail));
   return staged_pipeline(
       ctx, tmpl.k, in, len, 4096, tmpl.rows, out, [](size_t cl) { return cl; }, [](size_t off) { return off; },
       [&](uint8_t *d_in, int64_t in_stride, uint8_t *d_out, int64_t out_stride, size_t, size_t cl, hipStream_t st) {
@@ -496,7 +577,8 @@ int staged_code(DevCtx *ctx, const CodeArgs &tmpl, const uint8_t *const *in, uin
         for (int j = 0; j < a.k; ++j) a.in_off[j] = j * in_stride;
         for (int r = 0; r < a.rows; ++r) a.out_off[r] = r * out_stride;
         return ozec::launch_code(a, st);
-      });
+      },
+      &key);
 }
 
 }  // namespace
@@ -1800,6 +1882,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "e2e_rect") {
     if (value != 0 && value != 1) return bad();
     t.e2e_rect.store(static_cast<int>(value));
+  } else if (k == "host_graph") {
+    if (value < 0) return bad();
+    t.host_graph.store(value);
   } else {
     return fail(OZEC_EINVAL, "unknown tuning key " + k);
   }

@@ -154,6 +154,9 @@ struct TuneKnobs {
   std::atomic<int64_t> queue_batches{0};     // stripe queue: batches in the ring (0 = default), read at queue creation
   std::atomic<int64_t> e2e_chunk{32};        // host batches: stripes per pipelined chunk when the caller passes 0
   std::atomic<int> e2e_rect{1};              // host batches: one rectangular copy per chunk (0: one per stripe)
+  std::atomic<int64_t> host_graph{256 << 10};  // host-buffer coding calls of one staged chunk up to this many bytes
+                                               // per unit replay a cached hipGraph of H2D + kernel + D2H (0: off;
+                                               // 64 KiB-cell rs-6-3 stripe from pageable cells 74 -> 64 us)
 };
 
 // Kernel alternates the library holds besides the defaults, selectable with ozec_set_tuning for A/B (0 = default).

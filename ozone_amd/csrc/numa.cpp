@@ -18,6 +18,7 @@
 #include <sstream>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 namespace ozec {
 namespace {
@@ -32,6 +33,19 @@ constexpr size_t kHuge = 2u << 20;
 
 std::mutex g_mu;
 std::unordered_map<void *, size_t> g_allocs;  // pinned_alloc'ed regions -> mapped length
+// Freed pinned blocks are kept registered and mapped, and handed out again, instead of being unregistered and
+// unmapped: a host address range that was registered, unregistered and unmapped can come back from the kernel for an
+// unrelated pageable buffer, and HIP's pageable-copy path is suspected of faulting on such ranges ("GPU
+// faults").  Per NUMA node of the placement; bounded, past the bound a block is really freed.
+struct Cached {
+  void *p;
+  size_t len;
+  int node;
+};
+std::vector<Cached> g_cache;
+std::unordered_map<void *, int> g_nodes;  // pinned_alloc'ed regions -> NUMA node of their placement
+size_t g_cached = 0;
+constexpr size_t kCacheCap = size_t{4} << 30;
 
 size_t page_size() {
   static const size_t ps = static_cast<size_t>(sysconf(_SC_PAGESIZE));
@@ -123,11 +137,34 @@ int pinned_alloc(size_t bytes, int device, void **out) {
   *out = nullptr;
   if (bytes == 0) return 0;
   const size_t len = (bytes + kHuge - 1) / kHuge * kHuge;
+  const int node = device >= 0 ? device_numa_node(device) : -1;
+  void *hit = nullptr;
+  {  // the smallest cached block of this placement that fits, if it wastes at most half of itself
+    std::lock_guard<std::mutex> lk(g_mu);
+    size_t best = g_cache.size();
+    for (size_t i = 0; i < g_cache.size(); ++i)
+      if (g_cache[i].node == node && g_cache[i].len >= len && g_cache[i].len <= 2 * len &&
+          (best == g_cache.size() || g_cache[i].len < g_cache[best].len))
+        best = i;
+    if (best < g_cache.size()) {
+      const Cached c = g_cache[best];
+      g_cache.erase(g_cache.begin() + static_cast<std::ptrdiff_t>(best));
+      g_cached -= c.len;
+      g_allocs[c.p] = c.len;
+      g_nodes[c.p] = node;
+      hit = c.p;
+    }
+  }
+  if (hit) {
+    std::memset(hit, 0, bytes);  // as a fresh mapping
+    *out = hit;
+    return 0;
+  }
   void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
   if (p == MAP_FAILED) return -ENOMEM;
   (void)madvise(p, len, MADV_HUGEPAGE);  // fewer translations per DMA; best effort
   // placement first (pages are allocated on the first touch, which hipHostRegister does while pinning)
-  (void)bind_to_node(p, len, device >= 0 ? device_numa_node(device) : -1, false, false);
+  (void)bind_to_node(p, len, node, false, false);
   if (hipHostRegister(p, len, hipHostRegisterPortable) != hipSuccess) {
     (void)hipGetLastError();
     munmap(p, len);
@@ -136,6 +173,7 @@ int pinned_alloc(size_t bytes, int device, void **out) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     g_allocs[p] = len;
+    g_nodes[p] = node;
   }
   *out = p;
   return 0;
@@ -150,6 +188,13 @@ int pinned_free(void *p) {
     if (it == g_allocs.end()) return -EINVAL;
     len = it->second;
     g_allocs.erase(it);
+    const int node = g_nodes[p];
+    g_nodes.erase(p);
+    if (g_cached + len <= kCacheCap) {
+      g_cache.push_back({p, len, node});
+      g_cached += len;
+      return 0;
+    }
   }
   (void)hipHostUnregister(p);
   munmap(p, len);

@@ -242,6 +242,9 @@ def test_reconstruct_host_batch_errors():
                                        4 * 4096, 4096, 1, 4096, ck.ChecksumType.CRC32C, 4096, np.zeros(4, np.uint32))
 
 
+_KEEP_REGISTERED = []  # host ranges this process registered and unregistered, kept mapped until exit
+
+
 def test_pinned_memory_is_numa_local():
     """ozec_host_alloc places its pages on the GPU's NUMA node (mbind before the pinning touch)."""
     node = device_numa_node(0)
@@ -259,8 +262,7 @@ def test_pinned_memory_is_numa_local():
     host_register(addr, 16 << 20, 0)
     assert page_node(addr) == node and page_node(addr + (16 << 20) - 1) == node
     host_unregister(addr)
-    del anchor
-    mm.close()
+    _KEEP_REGISTERED.append((mm, anchor))  # not unmapped before exit (test_gpu_parity.py _KEEP_REGISTERED)
 
 
 def _free_port():

@@ -81,7 +81,10 @@ int ozec_device_policy(void);
 int ozec_synchronize(void);
 /* give back the host-batch pipeline's chunk buffers (4 device + 4 pinned buffers of one chunk each: about 1.1 GiB
  * of HBM and, for pageable callers, of pinned memory with rs-6-3 1 MiB cells and 32-stripe chunks) and the staging
- * buffers of the idle host-call slots, on every GPU the process has used; the next call allocates again */
+ * buffers of the idle host-call slots, on every GPU the process has used; the next call allocates again.  Device
+ * memory goes back to HIP; pinned blocks up to 4 GiB in all stay registered in libozec's own cache for the next
+ * allocation (ozec_host_free likewise), so a registered host range is not handed back to the kernel in normal
+ * operation ("GPU faults") */
 int ozec_release_staging(void);
 
 /* ---- coder lifecycle: RawErasureCoderFactory.createEncoder/createDecoder

@@ -47,10 +47,13 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED = 0x00EC5EED
 METRIC = "EC encode GB/s (data bytes) rs-6-3-1024k @1/8 GPUs + % HBM roofline"
 WORKLOADS = ["c1", "c2", "c3", "c3r", "c3r_host", "c4", "c4s", "c5", "c5dev", "crc", "verify", "host", "queue", "queue_pageable",
-             "stream", "fused"]
-# the fused legs of the default line (the kernels C5 and the reconstruction coordinator run, under the
-# driver's clock): (workload, erased units) -- C5dev rs-6-3 encode + CRC32C, C3r with both erasure sets of BASELINE.md
-FUSED_LEGS = [("c5dev", (0, 1, 2, 3)), ("c3r", (0, 1, 2, 3)), ("c3r", (1, 4, 10, 13))]
+             "stream", "legs", "jni", "tail"]
+# the device-resident legs of the default line, each timed like the headline (every kernel north_star
+# names under the driver's clock): (workload, erased units) -- C5dev rs-6-3 encode + CRC32C, C3r with both erasure sets
+# of BASELINE.md, C3 rs-10-4 decode with both sets (RSRawDecoder.java:87-101), CRC32C compute and verify per 16 KiB
+# window (Checksum.java:157-200, :272-297), C4 xor-2-1 + CRC32C over block groups (XORRawEncoder.java:39-85)
+LEGS = [("c5dev", None), ("c3r", (0, 1, 2, 3)), ("c3r", (1, 4, 10, 13)), ("c3", (0, 1, 2, 3)), ("c3", (1, 4, 10, 13)),
+        ("crc", None), ("verify", None), ("c4", None)]
 
 
 def parse(argv=None):
@@ -68,7 +71,10 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the C5 end-to-end leg of the default line")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC traffic passes")
-    ap.add_argument("--no-fused", action="store_true", help="skip the fused-kernel legs (C5dev, C3r) of the default line")
+    ap.add_argument("--no-legs", action="store_true", help="skip the device-resident legs (LEGS) of the default line")
+    ap.add_argument("--no-inproc", action="store_true",
+                    help="skip the in-process multi-GPU C5 leg (one process, libozec's device list over all N GPUs)")
+    ap.add_argument("--no-jni", action="store_true", help="skip the JNI per-call rows of the default line")
     ap.add_argument("--e2e-stripes", type=int, default=8192, help="C5 batch size (all GPUs together)")
     ap.add_argument("--e2e-steps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0, help="C5: stripes per pipelined chunk (0 = library default)")
@@ -561,9 +567,11 @@ class HostBatch:
             dist.barrier()
 
 
-def e2e_leg(args, rank, world, dist, dev, backend):
+def e2e_leg(args, rank, world, dist, dev, backend, cpu_group=None):
     """BASELINE configs[4] (C5): rs-6-3-1024k encode + CRC32C of one 8192-stripe batch in pinned host memory,
-    sharded across the GPUs by contiguous stripe ranges, end to end (H2D + fused kernel + D2H)."""
+    sharded across the GPUs by contiguous stripe ranges, end to end (H2D + fused kernel + D2H): one process per GPU.
+    Then (unless --no-inproc) the same batch through ONE process driving all N GPUs (in_process_leg).  Returns
+    (multi-process result, in-process result or None)."""
     from ozone_amd import checksum as ck
     from ozone_amd import rawcoder as rc
     from ozone_amd.shard import max_over_ranks
@@ -624,9 +632,110 @@ def e2e_leg(args, rank, world, dist, dev, backend):
         pc = pcie_ceiling(64 * 6 * MIB, 64 * 3 * MIB)
         res["pcie_per_gpu"] = pc
         res["frac_of_duplex_h2d_link"] = round(res["value"] / world / pc["duplex_h2d_GBps"], 4)
-        return res
+        inproc = None
+        if not args.no_inproc:
+            log("C5 end-to-end leg, one process over all GPUs")
+            try:
+                inproc = in_process_leg(args, hb, rank, world, dist, cpu_group, pc)
+            except Exception as e:  # the multi-process figure stands on its own
+                inproc = {"error": f"{type(e).__name__}: {e}"}
+        return res, inproc
     finally:
         hb.close(dist)
+
+
+def in_process_leg(args, hb, rank, world, dist, cpu_group, pc):
+    """north_star: "a batch is partitioned across the 8 MI355X of one node as per-GPU streams" -- inside the drop-in
+    process, as Ozone runs it (one JVM per datanode or client making a coder per stream, ECKeyOutputStream.java:117,
+    ECReconstructionCoordinator.java:240-352).  Rank 0 alone sets libozec's device list to the node's N GPUs
+    (ozec_set_devices) and runs the whole C5 batch through ONE ozec_encode_crc_host_batch call per step, which cuts it
+    into N contiguous stripe ranges run by per-GPU pipelines on threads of their own (capi.cpp host_batch_split); the
+    other ranks wait on a CPU barrier and leave their GPUs idle.  The batch is the one the ranks just encoded (each
+    range's pages already on its GPU's NUMA node); rank 0 registers the other ranks' ranges in its own process."""
+    from ozone_amd import _lib
+    from ozone_amd import checksum as ck
+    from ozone_amd import rawcoder as rc
+    from ozone_amd.shard import stripe_range
+    from ozone_amd.stripe_queue import device_numa_node, host_alloc, host_register, host_unregister, page_node
+
+    def cpu_barrier():
+        if dist is not None:
+            dist.barrier(group=cpu_group)
+    if world > 1 and not hb.shared:
+        cpu_barrier()
+        return {"error": "the batch is not in shared memory (/dev/shm too small): rank 0 cannot see every range"}
+    if rank != 0:
+        cpu_barrier()
+        return None
+    try:
+        S, sb, n, k = hb.S, hb.stripe_bytes, hb.n, hb.k
+        same = os.environ.get("OZEC_BENCH_SAME_DEVICE") == "1"
+        devs = [0] * world if same else list(range(world))
+        nwin = hb.nwin
+        base = hb.base  # the shared mapping: stripe s at base + s * sb in every rank
+        extra = []
+        t0 = time.perf_counter()
+        for r in range(1, world):  # the other ranks' ranges, one registration each (= libozec's part r)
+            lo, hi = stripe_range(S, r, world)
+            if hi > lo:
+                host_register(base + lo * sb, (hi - lo) * sb, -1)  # pages already on GPU r's node: no move
+                extra.append(base + lo * sb)
+        reg_s = time.perf_counter() - t0
+        crc = host_alloc(S * hb.units * nwin * 4, devs[0])
+        saved_aff = os.sched_getaffinity(0)
+        if ORIG_AFFINITY:
+            os.sched_setaffinity(0, ORIG_AFFINITY)  # the per-GPU pipeline threads of both sockets
+        L = _lib.lib()
+        prev_policy = L.ozec_device_policy()
+        try:
+            rc.set_devices(devs)
+            rc.set_device_policy("current")  # the coder on device 0, so part r (= rank r's range) runs on GPU r
+            enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, hb.p))
+            rc.set_device_policy(prev_policy)
+
+            def step():
+                enc.encode_crc_host_batch(base, sb, n, base + k * n, sb, n, S, n, ck.ChecksumType.CRC32C, 16384,
+                                          crc.array.ctypes.data, False, args.chunk)
+            step()  # warm-up: every GPU's pipeline buffers
+            t0 = time.perf_counter()
+            for _ in range(args.e2e_steps):
+                step()
+            el = time.perf_counter() - t0
+            # spot check: the last stripe of every part against the device coder on GPU 0
+            ok = True
+            parts = []
+            for i, d in enumerate(devs):
+                lo, hi = stripe_range(S, i, len(devs))
+                parts.append({"device": d, "stripes": hi - lo, "gpu_node": device_numa_node(d),
+                              "data_page_nodes": [page_node(base + lo * sb), page_node(base + hi * sb - 1)]
+                              if hi > lo else []})
+                if hi > lo:
+                    last = np.frombuffer((ctypes.c_uint8 * sb).from_address(base + (hi - 1) * sb), np.uint8).reshape(
+                        hb.units, n)
+                    cells = torch.from_numpy(last[:k].copy()).cuda().unsqueeze(0)
+                    par = enc.encode_stripes(cells)
+                    torch.cuda.synchronize()
+                    ok = ok and bool((par[0].cpu().numpy() == last[k:]).all())
+        finally:
+            rc.set_devices([devs[0]])
+            L.ozec_set_device_policy(prev_policy)
+            os.sched_setaffinity(0, saved_aff)
+            for a in extra:
+                host_unregister(a)
+            crc.free()
+        ndev = len(set(devs))
+        value = S * k * n * args.e2e_steps / el / 1e9
+        return {"workload": "rs-6-3-1024k encode + CRC32C/16 KiB, the same %d-stripe batch through ONE process: "
+                            "ozec_set_devices(%s), one ozec_encode_crc_host_batch call per step split into contiguous "
+                            "stripe ranges on per-GPU pipeline threads" % (S, devs),
+                "value": round(value, 2), "unit": "GB/s (data bytes)",
+                "ms_per_step": round(el / args.e2e_steps * 1e3, 2), "steps": args.e2e_steps, "n_gpus": ndev,
+                "devices": devs, "parts": parts, "register_other_ranges_s": round(reg_s, 2),
+                "parity_spot_check": ok,
+                "frac_of_duplex_h2d_link": round(value / ndev / pc["duplex_h2d_GBps"], 4),
+                "note": "per-GPU pipelines run concurrently inside one call; per-part times are not separated"}
+    finally:
+        cpu_barrier()
 
 
 def pcie_ceiling(h2d_bytes, d2h_bytes, reps=5):
@@ -721,6 +830,7 @@ def cpu_baseline(workload, budget_s):
 # ------------------------------------------------------------------------------------------ live PMC traffic
 
 HOST_PINNED = False  # --host-pinned (host workload)
+ORIG_AFFINITY = None  # the CPUs the process was started with, before each rank binds itself to its GPU's node
 
 KERNEL_PAT = {"c1": "gf_code_vec<3, 2", "c2": "gf_code_vec<6, 3", "c3": "gf_code_vec<10, 4",
               "c3r": ("encode_crc_nb<10, 4", "encode_crc_lv<10, 4", "encode_crc_g26<10, 4"), "c4": "encode_crc_g26<2, 1",
@@ -762,22 +872,35 @@ def _rocprof_passes(child, tag_opts, timeout=300):
 _PMC_PASSES = (("FETCH_SIZE", ["--pmc", "FETCH_SIZE"]), ("WRITE_SIZE", ["--pmc", "WRITE_SIZE"]), ("stats", []))
 
 
-def _leg_stats(files, pat, group, ngroups, steps, alg_bytes):
-    """One workload's numbers from the three passes: the kernel's dispatches matching `pat` come in `ngroups`
-    consecutive groups of equal size (one per leg of the child that launches that kernel), this leg is group `group`,
-    and its timed dispatches are the group's last `steps`."""
+def _runs(rows, name_key, order_key):
+    """The dispatches in launch order cut into maximal runs of one kernel name.  A leg's warm-up and timed steps are one
+    such run: its set-up launches other kernels (the synthetic-data fill) before them."""
+    rows = sorted(rows, key=lambda r: int(r[order_key]))
+    runs = []
+    for r in rows:
+        if runs and runs[-1][0] == r[name_key]:
+            runs[-1][1].append(r)
+        else:
+            runs.append((r[name_key], [r]))
+    return runs
+
+
+def _leg_rows(rows, name_key, order_key, pat, occurrence, warmup, steps):
+    """The timed dispatches of a leg: the last `steps` of the `occurrence`-th run of at least warmup + steps dispatches
+    of a kernel matching `pat` (set-up launches of the same kernel -- the encode before a decode leg -- are shorter)."""
+    runs = [rs for nm, rs in _runs(rows, name_key, order_key) if _kernel_match(pat, nm) and len(rs) >= warmup + steps]
+    return runs[occurrence][-steps:]
+
+
+def _leg_stats(files, pat, occurrence, warmup, steps, alg_bytes):
+    """One leg's numbers from the three passes (the child runs the legs in order; `occurrence` counts the legs before
+    this one whose kernel matches the same pattern)."""
     import csv
     out = {}
-
-    def mine(rows, name_key, order_key):
-        rows = [r for r in rows if _kernel_match(pat, r[name_key])]
-        rows.sort(key=lambda r: int(r[order_key]))
-        per = len(rows) // ngroups
-        return rows[group * per:(group + 1) * per]
     st = [f for f in files["stats"] if f.endswith("kernel_stats.csv")]
     tr = [f for f in files["stats"] if f.endswith("kernel_trace.csv")]
-    disp = mine(list(csv.DictReader(open(tr[0]))), "Kernel_Name", "Start_Timestamp")
-    timed = disp[-steps:]
+    timed = _leg_rows(list(csv.DictReader(open(tr[0]))), "Kernel_Name", "Start_Timestamp", pat, occurrence, warmup,
+                      steps)
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
     out["rocprof_kernel"] = timed[-1]["Kernel_Name"]
     out["rocprof_avg_ms"] = round(float(np.mean(dur)), 4)
@@ -786,13 +909,14 @@ def _leg_stats(files, pat, group, ngroups, steps, alg_bytes):
     out["kernel_vgpr"] = int(timed[-1].get("VGPR_Count") or 0)
     out["kernel_lds_bytes"] = int(timed[-1].get("LDS_Block_Size") or 0)
     out["kernel_scratch_bytes"] = int(timed[-1].get("Scratch_Size") or 0)
-    rows = [row for row in csv.DictReader(open(st[0])) if _kernel_match(pat, row["Name"])]
+    rows = [row for row in csv.DictReader(open(st[0])) if row["Name"] == out["rocprof_kernel"]]
     if rows:
         out["rocprof_stats_avg_all_calls_ms"] = round(float(rows[0]["AverageNs"]) / 1e6, 4)
     for tag in ("FETCH_SIZE", "WRITE_SIZE"):
         cc = [f for f in files[tag] if f.endswith("counter_collection.csv")]
-        vals = [float(r["Counter_Value"]) for r in mine([r for r in csv.DictReader(open(cc[0]))
-                                                         if r["Counter_Name"] == tag], "Kernel_Name", "Dispatch_Id")]
+        vals = [float(r["Counter_Value"]) for r in _leg_rows([r for r in csv.DictReader(open(cc[0]))
+                                                              if r["Counter_Name"] == tag], "Kernel_Name", "Dispatch_Id",
+                                                             pat, occurrence, warmup, steps)]
         if not vals:
             raise KeyError(f"no {tag} rows for kernel {pat}")
         out[tag + "_KiB"] = sum(vals) / len(vals)
@@ -807,7 +931,8 @@ def _leg_stats(files, pat, group, ngroups, steps, alg_bytes):
 
 def _child_base(args, workload):
     base = [sys.executable, os.path.abspath(__file__), "--workload", workload, "--steps", str(args.steps),
-            "--warmup", str(args.warmup), "--no-cpu", "--no-e2e", "--no-pmc", "--erased", args.erased] + \
+            "--warmup", str(args.warmup), "--no-cpu", "--no-e2e", "--no-pmc", "--no-legs", "--no-inproc", "--no-jni",
+            "--erased", args.erased] + \
         (["--stripes", str(args.stripes)] if args.stripes else [])
     for kv in args.tune:
         base += ["--tune", kv]
@@ -827,7 +952,7 @@ def pmc_traffic(args, alg_bytes):
     files = {}
     try:
         files = _rocprof_passes(_child_base(args, args.workload), _PMC_PASSES)
-        return _leg_stats(files, pat, 0, 1, args.steps, alg_bytes)
+        return _leg_stats(files, pat, 0, args.warmup, args.steps, alg_bytes)
     except (OSError, subprocess.SubprocessError, IndexError, KeyError, ValueError) as e:
         return None, {"error": f"{type(e).__name__}: {e}"}
     finally:
@@ -858,20 +983,22 @@ def time_workload(wl, steps, warmup, dist):
     return elapsed, float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
 
-def fused_legs(args, rank, world, dist, red_dev):
-    """The fused kernels of C5 (rs-6-3 encode + CRC32C) and of reconstruction (rs-10-4 verify + decode + CRC32C,
-    both erasure sets), device-resident, timed like the headline and reduced max over ranks: the kernel's roofline
-    fraction from HIP events, and at N = 1 the rocprofv3 average and PMC traffic of the same timed dispatches from
-    one child run of all legs (3 passes)."""
+def device_legs(args, rank, world, dist, red_dev):
+    """The device-resident legs (LEGS): the fused kernels of C5 (rs-6-3 encode + CRC32C) and of reconstruction (rs-10-4
+    verify + decode + CRC32C, both erasure sets), the rs-10-4 decode (both sets), CRC32C compute and verify, and C4,
+    each timed like the headline and reduced max over ranks: the kernel's roofline fraction from HIP events, and at
+    N = 1 the rocprofv3 average and PMC traffic of the same timed dispatches from one child run of all legs (3
+    passes)."""
     from ozone_amd.shard import max_over_ranks
     legs = []
-    for name, erased in FUSED_LEGS:
-        log(f"fused leg {name} {erased}")
-        wl = Workload(name, rank, world, args.stripes, erased=list(erased))
+    for name, erased in LEGS:
+        log(f"leg {name} {erased or ''}")
+        wl = Workload(name, rank, world, args.stripes, erased=list(erased or (0, 1, 2, 3)))
         elapsed, kern_ms = time_workload(wl, args.steps, args.warmup, dist)
         elapsed = max_over_ranks(elapsed, dist, device=red_dev)
         kern_ms = max_over_ranks(kern_ms, dist, device=red_dev)
-        leg = {"workload": wl.config["workload"], "kernel": wl.kernel, "stripes_per_gpu": wl.S,
+        leg = {"leg": name + (f" {{{','.join(map(str, erased))}}}" if erased else ""),
+               "workload": wl.config["workload"], "kernel": wl.kernel, "stripes_per_gpu": wl.S,
                "value": round(wl.data_bytes * world * args.steps / elapsed / 1e9, 2), "unit": "GB/s (data bytes)",
                "ms_per_step": round(elapsed / args.steps * 1e3, 4), "kernel_ms": round(kern_ms, 4),
                "alg_bytes_per_launch": wl.alg_bytes,
@@ -884,10 +1011,11 @@ def fused_legs(args, rank, world, dist, red_dev):
     if rank == 0 and world == 1 and not args.no_pmc:
         files = {}
         try:
-            files = _rocprof_passes(_child_base(args, "fused"), _PMC_PASSES, timeout=400)
-            for i, (name, _) in enumerate(FUSED_LEGS):
-                same = [j for j, (nm, _) in enumerate(FUSED_LEGS) if nm == name]
-                traffic, detail = _leg_stats(files, KERNEL_PAT[name], same.index(i), len(same), args.steps,
+            files = _rocprof_passes(_child_base(args, "legs"), _PMC_PASSES, timeout=600)
+            for i, (name, _) in enumerate(LEGS):
+                pat = KERNEL_PAT[name]
+                occurrence = sum(1 for nm, _ in LEGS[:i] if KERNEL_PAT[nm] == pat)
+                traffic, detail = _leg_stats(files, pat, occurrence, args.warmup, args.steps,
                                              legs[i]["alg_bytes_per_launch"])
                 legs[i]["traffic"] = traffic
                 legs[i]["pmc"] = detail
@@ -1009,6 +1137,139 @@ def stream_latency(args):
     return rows
 
 
+# ------------------------------------------------------------------------------------------ JNI per-call path
+
+_JNI_BIN = None
+
+
+def _jni_percall_bin():
+    """tests/native/jni_percall.c + jni/ozec_jni.c + jni/ozec_marshal.c against the JNI test double, linked to the
+    in-tree libozec.so (built here at run time, as the CPU baseline is)."""
+    global _JNI_BIN
+    if _JNI_BIN:
+        return _JNI_BIN
+    lib = os.path.join(ROOT, "ozone_amd", "lib")
+    out = os.path.join(tempfile.mkdtemp(prefix="ozec_jni_"), "jni_percall")
+    mock = os.path.join(ROOT, "tests", "native", "mockjni")
+    subprocess.run(["gcc", "-O2", "-I", mock, "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "jni", "ozec_jni.c"),
+                    os.path.join(ROOT, "jni", "ozec_marshal.c"), os.path.join(mock, "mockjni.c"),
+                    os.path.join(ROOT, "tests", "native", "jni_percall.c"), "-L", lib, "-lozec", "-lpthread",
+                    "-Wl,--wrap=ozec_encode,--wrap=ozec_decode,--wrap=ozec_crc_update,--wrap=ozec_checksum_windows,"
+                    "--wrap=ozec_host_alloc,--wrap=ozec_host_free", f"-Wl,-rpath,{lib}", "-o", out],
+                   check=True, capture_output=True, timeout=120)
+    _JNI_BIN = out
+    return out
+
+
+def jni_percall(specs, seconds, dev=0):
+    """Run the JNI harness over `specs` ("encode:6:3:65536:4", ...) in one child process pinned to GPU `dev`
+    (OZEC_DEVICES), one JSON row per spec."""
+    env = dict(os.environ, OZEC_DEVICES=str(dev))
+    r = subprocess.run([_jni_percall_bin(), str(seconds)] + list(specs), capture_output=True, text=True,
+                       timeout=120 + 4 * seconds * len(specs), env=env)
+    if r.returncode != 0:
+        raise RuntimeError(f"jni_percall rc={r.returncode}: {r.stderr.strip()[-400:]}")
+    return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+
+
+def _cpu_percall_encode(nbytes, seconds=0.3):
+    exe, flags = _cpu_baseline_bin()
+    out = subprocess.run([exe, "percall_encode", str(nbytes), str(seconds)], capture_output=True, text=True, timeout=60)
+    return json.loads(out.stdout)["us_per_call"], flags
+
+
+def jni_rows(args, threads=(1, 4, 16), cells=(64 << 10, MIB), seconds=0.5):
+    """The Java drop-in's per-call production path: OzecNative.encodeArrays / decodeArrays on heap
+    byte[] -- what ECKeyOutputStream (one stripe per call, ECKeyOutputStream.java:304, heap buffers :701) and the
+    reconstruction coordinator (ECReconstructionCoordinator.java:283) call -- through jni/ozec_jni.c compiled
+    against the JNI test double: GetByteArrayRegion into a pooled pinned arena, in-place DMA + kernel,
+    SetByteArrayRegion back.  rs-6-3, T threads sharing one coder (RawErasureCoderBenchmark.java:201-206), beside
+    the CPU doing one stripe per call on one thread (oracle/cpu_baseline.c percall_encode: the RSUtil table loop)."""
+    specs = [f"{mode}:6:3:{c}:{t}" for mode in ("encode", "decode") for c in cells for t in threads]
+    rows = jni_percall(specs, seconds)
+    cpu = {}
+    for c in cells:
+        cpu[c], flags = _cpu_percall_encode(c)
+    for r in rows:
+        if r["mode"] == "encode":
+            r["cpu_1thread_us_per_stripe"] = round(cpu[r["cell_bytes"]], 1)
+    return {"path": "jni/ozec_jni.c encodeArrays / decodeArrays (heap byte[]) via the JNI test double, rs-6-3, decode "
+                    "of 3 erased {0,1,2}", "rows": rows,
+            "cpu": f"oracle/cpu_baseline.c percall_encode (1 thread, one stripe per call), {flags}"}
+
+
+def tail_rows(args, lens=(1007, 1008, 50000, 50001, 700000, 700001), seconds=0.4):
+    """The last, partial stripe of every key (parityCellSize = dataBuffers[0].position(), ECKeyOutputStream.java:276):
+    cells of any length.  (a) one stripe per call through the JNI path (encodeArrays, 1 and 16
+    threads); (b) the fused encode + CRC32C of one stripe per call from pinned host memory
+    (ozec_encode_crc_host_batch); (c) device-resident fused encode + CRC32C batches of such cells (unit stride
+    padded to 4 KiB), kernel time per launch -- a length that is not a multiple of 16 B takes the unfused path (encode,
+    then one CRC pass per unit)."""
+    from ozone_amd import checksum as ck
+    from ozone_amd import rawcoder as rc
+    from ozone_amd.stripe_queue import host_alloc
+    k, p, bpc = 6, 3, 16384
+    out = {"lens": list(lens)}
+    specs = [f"encode:{k}:{p}:{n}:{t}" for n in lens for t in (1, 16)]
+    out["jni_encode"] = jni_percall(specs, seconds)
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    dev = torch.device("cuda", torch.cuda.current_device())
+    host, dev_rows, cpu = [], [], {}
+    for n in lens:
+        cpu[n], flags = _cpu_percall_encode(n, 0.2)
+        nwin = -(-n // bpc)
+        pb = host_alloc((k + p) * n + (k + p) * nwin * 4)
+        a = pb.array
+        a[:k * n] = np.random.default_rng(n).integers(0, 256, k * n, dtype=np.uint8)
+        crc_addr = a.ctypes.data + (k + p) * n
+
+        def one():
+            enc.encode_crc_host_batch(a.ctypes.data, (k + p) * n, n, a.ctypes.data + k * n, (k + p) * n, n, 1, n,
+                                      ck.ChecksumType.CRC32C, bpc, crc_addr)
+        one()
+        calls, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            one()
+            calls += 1
+        us = (time.perf_counter() - t0) / calls * 1e6
+        host.append({"cell_bytes": n, "us_per_stripe": round(us, 1), "GBps": round(k * n / us / 1e3, 3),
+                     "cpu_1thread_encode_only_us": round(cpu[n], 1)})
+        pb.free()
+        # device-resident batch of such stripes: about 2 GiB of data cells
+        S = max(64, min(65536, (2 << 30) // (k * n)))
+        us_ = -(-n // 4096) * 4096
+        units = torch.zeros((S, k + p, us_), dtype=torch.uint8, device=dev)
+        for u in range(k):
+            rc.fill_splitmix64_cells(units[:, u], (k + p) * us_, S, n, SEED, u * S)
+        crcs = torch.empty((S, k + p, nwin), dtype=torch.int32, device=dev)
+
+        def launch():
+            enc.encode_crc_batch(units, (k + p) * us_, us_, units[:, k:], (k + p) * us_, us_, S, n,
+                                 ck.ChecksumType.CRC32C, bpc, crcs)
+        for _ in range(3):
+            launch()
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        e0.record(st)
+        for _ in range(reps):
+            launch()
+        e1.record(st)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        alg = S * (k + p) * n + S * (k + p) * nwin * 4
+        dev_rows.append({"cell_bytes": n, "stripes": S, "ms_per_launch": round(ms, 4),
+                         "GBps_data": round(S * k * n / ms / 1e6, 1),
+                         "frac_hbm": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                         "path": "fused (nibble kernel)" if n % 16 == 0 else "unfused (encode + 9 CRC passes)"})
+        del units, crcs
+        torch.cuda.empty_cache()
+    out["fused_host_one_stripe_per_call"] = host
+    out["fused_device_batch"] = dev_rows
+    out["cpu"] = f"oracle/cpu_baseline.c percall_encode (1 thread, encode only), {flags}"
+    return out
+
+
 # ------------------------------------------------------------------------------------------ main
 
 
@@ -1060,13 +1321,19 @@ def main():
     # would spread one process's coders over every visible GPU, ozec_set_devices)
     from ozone_amd import rawcoder as _rc
     _rc.set_devices([dev_idx])
+    global ORIG_AFFINITY
+    ORIG_AFFINITY = os.sched_getaffinity(0)
     numa_node = bind_process_to_gpu_node(dev_idx)
     backend = os.environ.get("OZEC_DIST_BACKEND", "nccl")
     dist = None
+    cpu_group = None
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+            # waits that must not occupy a GPU (an RCCL barrier spins a kernel on each waiting rank's GPU, which the
+            # in-process leg is using): a gloo group over the same ranks
+            cpu_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(backend)
     if args.tune:
@@ -1090,7 +1357,7 @@ def main():
     n_gpus = len(set(devices))
 
     if args.workload == "c5":
-        res = e2e_leg(args, rank, world, dist, dev_idx, backend)
+        res, inproc = e2e_leg(args, rank, world, dist, dev_idx, backend, cpu_group)
         result = {"metric": "C5 e2e: rs-6-3-1024k encode + CRC32C GB/s (data bytes) from pinned host memory",
                   "value": res["value"], "unit": "GB/s", "n_gpus": n_gpus, "n_ranks": world,
                   "steps": args.e2e_steps, "warmup": 1, "ms_per_step": res["ms_per_step"], "higher_is_better": True,
@@ -1098,7 +1365,7 @@ def main():
                   "data": "synthetic (splitmix64 bytes generated on the GPU, copied into the host batch)",
                   "config": {"workload": res["workload"], "stripes": args.e2e_stripes,
                              "parallelism": f"stripe-range sharded x{world} (one shared batch, no collective)"},
-                  "e2e": res}
+                  "e2e": res, "e2e_in_process": inproc}
         if rank == 0 and world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline("c5", args.cpu_seconds)
         if rank == 0:
@@ -1107,12 +1374,19 @@ def main():
             dist.destroy_process_group()
         return 0
 
-    if args.workload == "fused":  # the fused legs alone (the rocprofv3 child of the default line)
-        legs = fused_legs(args, rank, world, dist, red_dev)
+    if args.workload == "legs":  # the device-resident legs alone (the rocprofv3 child of the default line)
+        legs = device_legs(args, rank, world, dist, red_dev)
         if rank == 0:
-            emit({"metric": "fused legs", "value": None, "legs": legs})
+            emit({"metric": "device-resident legs", "value": None, "legs": legs})
         if dist is not None:
             dist.destroy_process_group()
+        return 0
+
+    if args.workload in ("jni", "tail"):
+        if rank == 0:
+            rows = jni_rows(args) if args.workload == "jni" else tail_rows(args)
+            emit({"metric": f"{args.workload}: per-call rows", "value": None, "n_gpus": n_gpus, "dtype": "u8",
+                  "config": {"workload": args.workload}, "rows": rows})
         return 0
 
     if args.workload == "stream":
@@ -1167,15 +1441,15 @@ def main():
         result["verified"] = wl._check()
     wl.free()
     del wl
-    if args.workload == "c2" and not args.no_fused:
+    if args.workload == "c2" and not args.no_legs:
         try:
-            result["fused"] = fused_legs(args, rank, world, dist, red_dev)
+            result["legs"] = device_legs(args, rank, world, dist, red_dev)
         except Exception as e:  # the headline stands on its own
-            result["fused"] = [{"error": f"{type(e).__name__}: {e}"}]
+            result["legs"] = [{"error": f"{type(e).__name__}: {e}"}]
     if args.workload == "c2" and not args.no_e2e:
         log("C5 end-to-end leg")
         try:
-            result["e2e"] = e2e_leg(args, rank, world, dist, dev_idx, backend)
+            result["e2e"], result["e2e_in_process"] = e2e_leg(args, rank, world, dist, dev_idx, backend, cpu_group)
         except Exception as e:  # the device-resident line stands on its own
             result["e2e"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1:
@@ -1194,6 +1468,12 @@ def main():
                 rf["clocks"] = ("kernel_ms: HIP events around each timed step on the launch stream (mean of the timed "
                                 "steps); rocprof_avg_ms: rocprofv3 durations of the same kernel's timed dispatches in a "
                                 "child run with the same warm-up and steps; frac uses kernel_ms")
+        if args.workload == "c2" and not args.no_jni:
+            log("JNI per-call rows")
+            try:
+                result["jni_percall"] = jni_rows(args)
+            except Exception as e:  # the device-resident line stands on its own
+                result["jni_percall"] = {"error": f"{type(e).__name__}: {e}"}
         if not args.no_cpu:
             log("CPU baseline")
             result["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)

@@ -20,6 +20,9 @@
  */
 #include <jni.h>
 #include <pthread.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -119,31 +122,73 @@ static void refs_free(JNIEnv *env, array_set *as) {
 #define HEAP_CHUNK ((int64_t)4 << 20)
 #define ARENA_ALIGN 256
 #define ARENA_POOL 32
+/* Pinned arena memory is bounded: at most ARENA_BYTES_MAX bytes over the whole pool (env
+ * OZEC_JNI_ARENA_MB, default 1024), a lease that would pass it runs on a pageable arena instead; an arena left unleased
+ * for ARENA_IDLE_S seconds is given back at the next lease.  Each arena remembers the NUMA node its pages were placed
+ * on, and a lease prefers a free arena on the calling thread's node, so a datanode's threads on both sockets DMA from
+ * local memory.  Worst case pinned by the JNI layer: ARENA_BYTES_MAX ("Pinned memory"). */
+#define ARENA_IDLE_S 30
 
 typedef struct {
   uint8_t *p;
   size_t cap;
+  int node;          /* NUMA node of the arena's pages, -1 unknown */
+  struct timespec t; /* when it was last handed back */
 } arena_t;
 
 typedef struct {
-  int slot;    /* index into g_arenas, or -1: `own` (pool exhausted) */
+  int slot;    /* index into g_arenas, or -1: `own` (pool exhausted, or the pinned bound reached) */
   arena_t own; /* pageable, freed at release */
 } arena_lease;
 
 static pthread_mutex_t g_arena_mu = PTHREAD_MUTEX_INITIALIZER;
 static arena_t g_arenas[ARENA_POOL];
 static int g_arena_leased[ARENA_POOL];
+static size_t g_arena_bytes; /* pinned bytes held by the pool, guarded by g_arena_mu */
 
-/* a free pooled arena (the largest, to spare reallocations), or a call-owned pageable one */
+static size_t arena_bytes_max(void) {
+  static size_t v;
+  if (!v) {
+    const char *e = getenv("OZEC_JNI_ARENA_MB");
+    const long mb = e && *e ? atol(e) : 1024;
+    v = (size_t)(mb > 0 ? mb : 1024) << 20;
+  }
+  return v;
+}
+
+static int caller_node(void) {
+  unsigned cpu = 0, node = 0;
+  return syscall(SYS_getcpu, &cpu, &node, NULL) == 0 ? (int)node : -1;
+}
+
+/* a free pooled arena -- on the caller's NUMA node if one is free, the largest among the candidates (to spare
+ * reallocations) -- or a call-owned pageable one; pooled arenas idle for ARENA_IDLE_S are freed on the way */
 static void arena_lease_begin(arena_lease *l) {
   l->slot = -1;
-  l->own.p = NULL;
-  l->own.cap = 0;
+  memset(&l->own, 0, sizeof(l->own));
+  const int node = caller_node();
+  struct timespec now;
+  clock_gettime(CLOCK_MONOTONIC, &now);
+  uint8_t *idle[ARENA_POOL];
+  int nidle = 0;
   pthread_mutex_lock(&g_arena_mu);
-  for (int i = 0; i < ARENA_POOL; ++i)
-    if (!g_arena_leased[i] && (l->slot < 0 || g_arenas[i].cap > g_arenas[l->slot].cap)) l->slot = i;
+  int near = -1, any = -1;
+  for (int i = 0; i < ARENA_POOL; ++i) {
+    if (g_arena_leased[i]) continue;
+    arena_t *a = &g_arenas[i];
+    if (a->p && now.tv_sec - a->t.tv_sec > ARENA_IDLE_S) {
+      idle[nidle++] = a->p;
+      g_arena_bytes -= a->cap;
+      a->p = NULL;
+      a->cap = 0;
+    }
+    if (any < 0 || a->cap > g_arenas[any].cap) any = i;
+    if (a->p && a->node == node && (near < 0 || a->cap > g_arenas[near].cap)) near = i;
+  }
+  l->slot = near >= 0 ? near : any;
   if (l->slot >= 0) g_arena_leased[l->slot] = 1;
   pthread_mutex_unlock(&g_arena_mu);
+  for (int i = 0; i < nidle; ++i) (void)ozec_host_free(idle[i]);
 }
 
 static void arena_lease_end(arena_lease *l) {
@@ -152,6 +197,7 @@ static void arena_lease_end(arena_lease *l) {
     return;
   }
   pthread_mutex_lock(&g_arena_mu);
+  clock_gettime(CLOCK_MONOTONIC, &g_arenas[l->slot].t);
   g_arena_leased[l->slot] = 0;
   pthread_mutex_unlock(&g_arena_mu);
 }
@@ -161,23 +207,40 @@ static uint8_t *arena(arena_lease *l, size_t bytes, ozm_status *st) {
   arena_t *a = l->slot >= 0 ? &g_arenas[l->slot] : &l->own;
   if (a->cap >= bytes) return a->p;
   const size_t cap = (bytes + ((size_t)1 << 20) - 1) >> 20 << 20;
-  if (l->slot < 0) {
-    free(a->p);
-    a->p = (uint8_t *)aligned_alloc(ARENA_ALIGN, cap);
-    a->cap = a->p ? cap : 0;
-    if (!a->p) ozm_fail(OZEC_ENOMEM, "out of memory", st);
-    return a->p;
-  }
-  if (a->p) (void)ozec_host_free(a->p);
-  a->p = NULL;
-  a->cap = 0;
-  int rc = ozec_host_alloc(cap, (void **)&a->p);
-  if (rc) {
+  if (l->slot >= 0) {
+    uint8_t *old = a->p;
+    pthread_mutex_lock(&g_arena_mu);
+    const int fits = g_arena_bytes - a->cap + cap <= arena_bytes_max();
+    g_arena_bytes -= a->cap;
     a->p = NULL;
-    ozm_fail(rc, NULL, st);
-    return NULL;
+    a->cap = 0;
+    if (fits) g_arena_bytes += cap; /* reserved before the allocation, so concurrent growths stay under the bound */
+    else g_arena_leased[l->slot] = 0; /* over the bound: this call goes pageable (libozec stages it) */
+    pthread_mutex_unlock(&g_arena_mu);
+    if (old) (void)ozec_host_free(old);
+    if (!fits) {
+      l->slot = -1;
+      a = &l->own;
+    } else {
+      int rc = ozec_host_alloc(cap, (void **)&a->p);
+      if (rc) {
+        a->p = NULL;
+        pthread_mutex_lock(&g_arena_mu);
+        g_arena_bytes -= cap;
+        pthread_mutex_unlock(&g_arena_mu);
+        ozm_fail(rc, NULL, st);
+        return NULL;
+      }
+      a->cap = cap;
+      a->node = -1;
+      (void)ozec_host_page_node(a->p, &a->node);
+      return a->p;
+    }
   }
-  a->cap = cap;
+  free(a->p);
+  a->p = (uint8_t *)aligned_alloc(ARENA_ALIGN, cap);
+  a->cap = a->p ? cap : 0;
+  if (!a->p) ozm_fail(OZEC_ENOMEM, "out of memory", st);
   return a->p;
 }
 

@@ -597,6 +597,7 @@ int ozec_device_count(void) {
 
 int ozec_set_device(int device) {
   OZEC_HIP(hipSetDevice(device));
+  (void)ozec::note_set_device();
   return OZEC_OK;
 }
 
@@ -1676,12 +1677,8 @@ static int host_batch_split(const ozec_coder *c, size_t num_stripes, size_t chun
   auto it = std::find(devs.begin(), devs.end(), c->device);
   if (it != devs.end()) std::rotate(devs.begin(), it, devs.end());
   else devs.insert(devs.begin(), c->device);  // a coder made before ozec_set_devices dropped its GPU
-  const size_t parts = std::min(devs.size(), std::max<size_t>(1, num_stripes / std::max<size_t>(1, chunk)));
-  auto range = [&](size_t i, size_t *s0, size_t *s1) {  // ozone_amd/shard.py stripe_range
-    const size_t per = (num_stripes + parts - 1) / parts;
-    *s0 = std::min(num_stripes, i * per);
-    *s1 = std::min(num_stripes, (i + 1) * per);
-  };
+  const size_t parts = ozec::split_parts(num_stripes, chunk, devs.size());
+  auto range = [&](size_t i, size_t *s0, size_t *s1) { ozec::part_range(num_stripes, parts, i, s0, s1); };
   if (parts == 1) {
     ozec::DeviceScope ds(devs[0]);
     if (!ds.ok()) return fail(OZEC_EDEVICE, "cannot select device " + std::to_string(devs[0]));
@@ -1702,13 +1699,21 @@ static int host_batch_split(const ozec_coder *c, size_t num_stripes, size_t chun
     rcs[i] = fn(s0, s1);
     if (rcs[i]) msgs[i] = g_error;
   };
+  // a part no thread can be started for (std::system_error: the process's thread limit, or memory) runs on the calling
+  // thread after part 0 -- nothing may escape through the C ABI into the JVM
   std::vector<std::thread> workers;
-  for (size_t i = 1; i < parts; ++i)
-    workers.emplace_back([&, i] {
-      ozec::g_stat_depth = 1;  // the caller's call is the one counted (stats.hpp)
-      run(i);
-    });
+  size_t threaded = 1;  // parts 1 .. threaded-1 have a thread
+  try {
+    workers.reserve(parts - 1);
+    for (size_t i = 1; i < parts; ++i, ++threaded)
+      workers.emplace_back([&, i] {
+        ozec::g_stat_depth = 1;  // the caller's call is the one counted (stats.hpp)
+        run(i);
+      });
+  } catch (const std::exception &) {
+  }
   run(0);
+  for (size_t i = threaded; i < parts; ++i) run(i);
   for (auto &w : workers) w.join();
   for (size_t i = 0; i < parts; ++i)
     if (rcs[i]) return fail(rcs[i], "device " + std::to_string(devs[i]) + ": " + msgs[i]);

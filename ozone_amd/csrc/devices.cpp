@@ -23,6 +23,9 @@ std::atomic<int> g_policy{-1};       // -1: read OZEC_DEVICE_POLICY on first use
 std::atomic<unsigned> g_next{0};     // round-robin cursor of pick_device
 std::atomic<unsigned> g_thread_next{0};
 std::atomic<unsigned> g_gen{1};          // bumped by set_device_list (threads re-pick their device)
+// whether the process chose its devices itself (ozec_set_devices, ozec_set_device_policy, OZEC_DEVICES,
+// OZEC_DEVICE_POLICY): only a process that did not gets "current" from note_set_device
+std::atomic<bool> g_configured{false};
 
 int visible() {
   int n = 0;
@@ -61,6 +64,11 @@ void ensure_init() {  // caller holds g_mu
   g_init = true;
 }
 
+bool env_set(const char *name) {
+  const char *e = std::getenv(name);
+  return e && *e;
+}
+
 int caller_node() {
   unsigned cpu = 0, node = 0;
   if (syscall(SYS_getcpu, &cpu, &node, nullptr) != 0) return -1;
@@ -91,6 +99,7 @@ int set_device_list(const int *devs, int n) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_list = n > 0 ? std::vector<int>(devs, devs + n) : default_list(vis);
   g_init = true;
+  g_configured.store(true, std::memory_order_relaxed);
   g_gen.fetch_add(1, std::memory_order_release);
   return OZEC_OK;
 }
@@ -108,7 +117,15 @@ int device_policy() {
 int set_device_policy(int policy) {
   if (policy < 0 || policy > 2) return OZEC_EINVAL;
   g_policy.store(policy, std::memory_order_relaxed);
+  g_configured.store(true, std::memory_order_relaxed);
   return OZEC_OK;
+}
+
+bool note_set_device() {
+  if (g_configured.load(std::memory_order_relaxed) || env_set("OZEC_DEVICES") || env_set("OZEC_DEVICE_POLICY"))
+    return false;
+  g_policy.store(2, std::memory_order_relaxed);
+  return true;
 }
 
 int pick_device() {
@@ -149,6 +166,18 @@ int thread_device() {
     gen = now;
   }
   return dev;
+}
+
+size_t split_parts(size_t num_stripes, size_t chunk, size_t ndev) {
+  const size_t whole_chunks = num_stripes / (chunk ? chunk : 1);
+  size_t parts = ndev < whole_chunks ? ndev : whole_chunks;
+  return parts ? parts : 1;
+}
+
+void part_range(size_t num_stripes, size_t parts, size_t i, size_t *s0, size_t *s1) {
+  const size_t per = (num_stripes + parts - 1) / parts;
+  *s0 = i * per < num_stripes ? i * per : num_stripes;
+  *s1 = (i + 1) * per < num_stripes ? (i + 1) * per : num_stripes;
 }
 
 DeviceScope::DeviceScope(int dev) {

@@ -14,6 +14,7 @@
 //   * coder-less host calls (CRC of a host buffer) run on a device the calling thread is given on first use;
 //   * device-pointer entry points run on the caller's current device (the one its pointers and stream belong to).
 #pragma once
+#include <cstddef>
 #include <vector>
 
 namespace ozec {
@@ -31,6 +32,18 @@ int thread_device();
 // 0 round_robin, 1 numa, 2 current
 int device_policy();
 int set_device_policy(int policy);
+// ozec_set_device was called: a process that picks its GPU itself is a one-process-per-GPU caller, so unless it chose
+// a device list or policy (API or environment) the policy becomes "current" -- its coders, host batches and pinned
+// buffers then stay on the GPU it selected instead of spreading over GPUs other processes own.  Returns
+// whether the policy changed.
+bool note_set_device();
+
+// How a host batch of `num_stripes` is split over `ndev` listed devices (capi.cpp host_batch_split): one part per device
+// while every part gets at least one pipeline chunk of `chunk` stripes, else fewer parts; part i is the contiguous range
+// [s0, s1) = ozone_amd/shard.py stripe_range(num_stripes, i, parts) -- the partition bench.py's ranks use, so a rank's
+// registered range is exactly libozec's part for its GPU (bench.py in_process_leg).
+size_t split_parts(size_t num_stripes, size_t chunk, size_t ndev);
+void part_range(size_t num_stripes, size_t parts, size_t i, size_t *s0, size_t *s1);
 
 // switch the calling thread to `dev` for the scope (restored on exit); ok() false when the switch failed
 class DeviceScope {

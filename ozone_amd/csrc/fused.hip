@@ -302,7 +302,9 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   EncCrcArgs ed = e;
   ed.work = used ? ws->ctr : nullptr;
   const hipError_t err = launch_nb_shape(ed, st, v);
-  if (ws) work_return(ws, st, used && err == hipSuccess);
+  // the event goes behind the launch whatever `err` says: an event behind a launch that never ran costs nothing, a
+  // kernel left running without one would share its counters with the slot's next lease
+  if (ws) work_return(ws, st, used);
   return err;
 }
 

@@ -369,6 +369,7 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
     // static persistent grid (profiles/r02/nb/ab_grid_*.log): C3r 56.2 % -> 63.5 %, C5dev 60.1 % -> 65.7 %.
     const int64_t cg = g_tune.crc_grid;
     if (cg > 0) g = std::min<int64_t>(cg, blocks);
+    (void)hipGetLastError();  // the error returned below must be this launch's, not a stale one (fused.hip work_return)
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(std::max<int64_t>(1, g))), dim3(WPB * 64), 0, st, e);
     return hipGetLastError();
   }

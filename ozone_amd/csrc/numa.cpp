@@ -17,6 +17,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <algorithm>
 #include <unordered_map>
 #include <vector>
 
@@ -33,19 +34,46 @@ constexpr size_t kHuge = 2u << 20;
 
 std::mutex g_mu;
 std::unordered_map<void *, size_t> g_allocs;  // pinned_alloc'ed regions -> mapped length
-// Freed pinned blocks are kept registered and mapped, and handed out again, instead of being unregistered and
-// unmapped: a host address range that was registered, unregistered and unmapped can come back from the kernel for an
-// unrelated pageable buffer, and HIP's pageable-copy path is suspected of faulting on such ranges ("GPU
-// faults").  Per NUMA node of the placement; bounded, past the bound a block is really freed.
-struct Cached {
-  void *p;
+// Address ranges of freed pinned blocks.  A freed block is unregistered at once and its pages go back to the kernel,
+// but its address range does not: it is replaced by an inaccessible reservation (PROT_NONE, mmap MAP_FIXED over the
+// block, so the range is never unmapped in between) and reused only for later pinned blocks.  No range libozec ever
+// registered with HIP can therefore come back from the kernel as an unrelated pageable buffer, which is the pattern the
+// round-4 faults shared ("GPU faults").  Adjacent reservations are merged; a block is carved from the
+// smallest one it fits.
+struct Range {
+  uint8_t *p;
   size_t len;
-  int node;
 };
-std::vector<Cached> g_cache;
-std::unordered_map<void *, int> g_nodes;  // pinned_alloc'ed regions -> NUMA node of their placement
-size_t g_cached = 0;
-constexpr size_t kCacheCap = size_t{4} << 30;
+std::vector<Range> g_reserved;  // guarded by g_mu
+constexpr int kRw = PROT_READ | PROT_WRITE;
+constexpr int kAnon = MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE;
+
+// caller holds g_mu
+void reserve_locked(uint8_t *p, size_t len) {
+  for (size_t i = 0; i < g_reserved.size();) {
+    Range &r = g_reserved[i];
+    if (r.p + r.len == p || p + len == r.p) {  // merge the neighbour into [p, p + len) and look again
+      p = std::min(p, r.p);
+      len += r.len;
+      g_reserved.erase(g_reserved.begin() + static_cast<std::ptrdiff_t>(i));
+      i = 0;
+      continue;
+    }
+    ++i;
+  }
+  g_reserved.push_back({p, len});
+}
+
+// turn a block back into a reservation; false when the kernel refused (the range is then simply unmapped)
+bool quarantine(void *p, size_t len) {
+  if (mmap(p, len, PROT_NONE, kAnon | MAP_FIXED, -1, 0) == MAP_FAILED) {
+    munmap(p, len);
+    return false;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  reserve_locked(static_cast<uint8_t *>(p), len);
+  return true;
+}
 
 size_t page_size() {
   static const size_t ps = static_cast<size_t>(sysconf(_SC_PAGESIZE));
@@ -138,42 +166,45 @@ int pinned_alloc(size_t bytes, int device, void **out) {
   if (bytes == 0) return 0;
   const size_t len = (bytes + kHuge - 1) / kHuge * kHuge;
   const int node = device >= 0 ? device_numa_node(device) : -1;
-  void *hit = nullptr;
-  {  // the smallest cached block of this placement that fits, if it wastes at most half of itself
+  uint8_t *reused = nullptr;
+  {  // carve the block from the smallest reservation it fits
     std::lock_guard<std::mutex> lk(g_mu);
-    size_t best = g_cache.size();
-    for (size_t i = 0; i < g_cache.size(); ++i)
-      if (g_cache[i].node == node && g_cache[i].len >= len && g_cache[i].len <= 2 * len &&
-          (best == g_cache.size() || g_cache[i].len < g_cache[best].len))
-        best = i;
-    if (best < g_cache.size()) {
-      const Cached c = g_cache[best];
-      g_cache.erase(g_cache.begin() + static_cast<std::ptrdiff_t>(best));
-      g_cached -= c.len;
-      g_allocs[c.p] = c.len;
-      g_nodes[c.p] = node;
-      hit = c.p;
+    size_t best = g_reserved.size();
+    for (size_t i = 0; i < g_reserved.size(); ++i)
+      if (g_reserved[i].len >= len && (best == g_reserved.size() || g_reserved[i].len < g_reserved[best].len)) best = i;
+    if (best < g_reserved.size()) {
+      const Range r = g_reserved[best];
+      g_reserved.erase(g_reserved.begin() + static_cast<std::ptrdiff_t>(best));
+      if (r.len > len) g_reserved.push_back({r.p + len, r.len - len});
+      reused = r.p;
     }
   }
-  if (hit) {
-    std::memset(hit, 0, bytes);  // as a fresh mapping
-    *out = hit;
-    return 0;
+  void *p = nullptr;
+  if (reused) {  // fresh zero pages over the reservation (MAP_FIXED replaces it in place)
+    p = mmap(reused, len, kRw, kAnon | MAP_FIXED, -1, 0);
+    if (p == MAP_FAILED) {
+      std::lock_guard<std::mutex> lk(g_mu);
+      reserve_locked(reused, len);
+      p = nullptr;
+    }
   }
-  void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-  if (p == MAP_FAILED) return -ENOMEM;
+  if (!p) {
+    p = mmap(nullptr, len, kRw, kAnon, -1, 0);
+    if (p == MAP_FAILED) return -ENOMEM;
+    reused = nullptr;
+  }
   (void)madvise(p, len, MADV_HUGEPAGE);  // fewer translations per DMA; best effort
   // placement first (pages are allocated on the first touch, which hipHostRegister does while pinning)
   (void)bind_to_node(p, len, node, false, false);
   if (hipHostRegister(p, len, hipHostRegisterPortable) != hipSuccess) {
     (void)hipGetLastError();
-    munmap(p, len);
+    if (reused) (void)quarantine(p, len);  // it stays reserved: never handed to the kernel
+    else munmap(p, len);
     return -ENOMEM;
   }
   {
     std::lock_guard<std::mutex> lk(g_mu);
     g_allocs[p] = len;
-    g_nodes[p] = node;
   }
   *out = p;
   return 0;
@@ -188,17 +219,20 @@ int pinned_free(void *p) {
     if (it == g_allocs.end()) return -EINVAL;
     len = it->second;
     g_allocs.erase(it);
-    const int node = g_nodes[p];
-    g_nodes.erase(p);
-    if (g_cached + len <= kCacheCap) {
-      g_cache.push_back({p, len, node});
-      g_cached += len;
-      return 0;
-    }
   }
+  // the callers have drained every stream that used the block (capi.cpp Slot / E2E, stripe_queue.cpp); hipHostUnregister
+  // waits for the device besides
   (void)hipHostUnregister(p);
-  munmap(p, len);
+  (void)hipGetLastError();
+  (void)quarantine(p, len);
   return 0;
+}
+
+size_t pinned_reserved_bytes() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  size_t n = 0;
+  for (const Range &r : g_reserved) n += r.len;
+  return n;
 }
 
 const void *pinned_alloc_base(const void *p) {

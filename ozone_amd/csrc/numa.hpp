@@ -15,9 +15,13 @@ int device_numa_node(int device);
 int bind_to_node(void *p, size_t bytes, int node, bool move, bool inner);
 // node of the page holding p (after it has been touched), -1 if unknown
 int page_node(const void *p);
-// pinned host allocation whose pages live on the device's node; free with pinned_free
+// pinned host allocation whose pages live on the device's node; free with pinned_free.  A freed block is unregistered
+// and its pages returned, but its address range stays reserved (PROT_NONE) and is reused only for later pinned blocks:
+// a range libozec registered never comes back from the kernel as a pageable buffer ("GPU faults")
 int pinned_alloc(size_t bytes, int device, void **out);
 int pinned_free(void *p);
+// bytes of address space reserved by freed pinned blocks (no memory behind them)
+size_t pinned_reserved_bytes();
 // start of the pinned / registered host allocation holding p (null when p is not in one): a DMA (a 2D copy's rows
 // included) must lie within one allocation
 const void *pinned_alloc_base(const void *p);

@@ -8,6 +8,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <set>
 #include <thread>
@@ -49,7 +50,17 @@ static int failures = 0;
     }                                                                     \
   } while (0)
 
-int main() {
+int main(int argc, char **argv) {
+  if (argc == 5 && !std::strcmp(argv[1], "parts")) {  // host-batch partition: "parts S chunk ndev" -> one "s0 s1" a line
+    const size_t S = std::strtoull(argv[2], nullptr, 10), chunk = std::strtoull(argv[3], nullptr, 10);
+    const size_t parts = ozec::split_parts(S, chunk, std::strtoull(argv[4], nullptr, 10));
+    for (size_t i = 0; i < parts; ++i) {
+      size_t s0 = 0, s1 = 0;
+      ozec::part_range(S, parts, i, &s0, &s1);
+      std::printf("%zu %zu\n", s0, s1);
+    }
+    return 0;
+  }
   unsigned cpu = 0, node = 0;
   syscall(SYS_getcpu, &cpu, &node, nullptr);
   // devices 0, 1 on another node than the caller's; 2, 3 on the caller's
@@ -58,6 +69,12 @@ int main() {
 
   const char *env = std::getenv("OZEC_DEVICES");
   std::vector<int> want = env ? std::vector<int>{3, 1} : std::vector<int>{0, 1, 2, 3};
+  // a process that selects its GPU itself (ozec_set_device) and configured nothing gets the "current" policy; one that
+  // chose a list (here OZEC_DEVICES) or a policy keeps it
+  CHECK(ozec::note_set_device() == (env == nullptr));
+  CHECK(ozec::device_policy() == (env ? 0 : 2));
+  CHECK(ozec::set_device_policy(0) == OZEC_OK);
+  CHECK(!ozec::note_set_device() && ozec::device_policy() == 0);
   CHECK(ozec::device_list() == want);  // "3,x,1,9" -> invalid entries skipped
   if (env) {
     CHECK(ozec::set_device_list(nullptr, 0) == OZEC_OK);  // n = 0: the default again (the env list)

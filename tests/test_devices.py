@@ -34,3 +34,18 @@ def test_device_policies(binary, env):
     r = subprocess.run([binary], capture_output=True, text=True, timeout=60, env=e)
     assert r.returncode == 0, r.stderr
     assert "devices policy OK" in r.stdout
+
+
+@pytest.mark.parametrize("S,chunk,ndev", [(8192, 32, 8), (8192, 32, 1), (8192, 32, 3), (100, 32, 8), (31, 32, 4),
+                                          (4097, 32, 8), (8192, 0, 5), (257, 16, 7)])
+def test_host_batch_partition_matches_the_bench_ranks(binary, S, chunk, ndev):
+    """bench.py's in-process C5 leg registers rank r's range = shard.stripe_range(S, r, N) and
+    relies on libozec splitting the same batch over N devices into exactly those ranges (devices.cpp split_parts /
+    part_range, used by capi.cpp host_batch_split); fewer parts when the batch has fewer whole chunks than devices."""
+    from ozone_amd.shard import stripe_range
+    r = subprocess.run([binary, "parts", str(S), str(chunk), str(ndev)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    got = [tuple(map(int, line.split())) for line in r.stdout.splitlines()]
+    parts = max(1, min(ndev, S // max(1, chunk)))
+    assert got == [stripe_range(S, i, parts) for i in range(parts)]
+    assert got[0][0] == 0 and got[-1][1] == S

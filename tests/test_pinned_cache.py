@@ -1,7 +1,8 @@
-"""libozec's pinned-block cache (ozone_amd/csrc/numa.cpp pinned_alloc / pinned_free) on the CPU, against a fake HIP
-runtime that counts registrations (tests/native/pinned_cache.cpp), under TSan: freed blocks stay registered and are
-reused per NUMA node, zeroed; past the bound they are really freed; foreign / double frees are refused; concurrent
-cycles never share a block.  Why the cache exists: DESIGN.md §4, "GPU faults"."""
+"""libozec's pinned blocks (ozone_amd/csrc/numa.cpp pinned_alloc / pinned_free) on the CPU, against a fake HIP runtime
+that counts registrations (tests/native/pinned_cache.cpp), under TSan: a freed block is unregistered and its pages
+returned at once, its address range stays reserved (PROT_NONE) and is reused only for later pinned blocks (carved,
+merged); a refused registration leaves the range reserved; foreign / double frees are refused; concurrent cycles never
+share a block.  Why the ranges are kept: DESIGN.md §4, "GPU faults"."""
 import os
 import subprocess
 import tempfile
@@ -28,4 +29,4 @@ def binary():
 def test_pinned_block_cache(binary):
     r = subprocess.run([binary], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
-    assert "pinned cache OK" in r.stdout
+    assert "pinned blocks OK" in r.stdout

@@ -872,35 +872,43 @@ def _rocprof_passes(child, tag_opts, timeout=300):
 _PMC_PASSES = (("FETCH_SIZE", ["--pmc", "FETCH_SIZE"]), ("WRITE_SIZE", ["--pmc", "WRITE_SIZE"]), ("stats", []))
 
 
-def _runs(rows, name_key, order_key):
-    """The dispatches in launch order cut into maximal runs of one kernel name.  A leg's warm-up and timed steps are one
-    such run: its set-up launches other kernels (the synthetic-data fill) before them."""
+FILL_KERNEL = "fill_splitmix64"  # every Workload starts by filling its synthetic cells with it
+
+
+def _leg_segments(rows, name_key, order_key):
+    """The dispatches in launch order cut into one segment per leg: each Workload's set-up starts with a run of
+    synthetic-data fill launches, and everything from there to the next leg's fills is that leg's (set-up, warm-up and
+    timed steps, with whatever else a step launches: the reconstruction's mismatch finisher, the runtime's memset that
+    zeroes a new WorkQueue slot)."""
     rows = sorted(rows, key=lambda r: int(r[order_key]))
-    runs = []
+    segs = []
+    prev_fill = False
     for r in rows:
-        if runs and runs[-1][0] == r[name_key]:
-            runs[-1][1].append(r)
-        else:
-            runs.append((r[name_key], [r]))
-    return runs
+        fill = FILL_KERNEL in r[name_key]
+        if fill and not prev_fill:
+            segs.append([])
+        if segs:
+            segs[-1].append(r)
+        prev_fill = fill
+    return segs
 
 
-def _leg_rows(rows, name_key, order_key, pat, occurrence, warmup, steps):
-    """The timed dispatches of a leg: the last `steps` of the `occurrence`-th run of at least warmup + steps dispatches
-    of a kernel matching `pat` (set-up launches of the same kernel -- the encode before a decode leg -- are shorter)."""
-    runs = [rs for nm, rs in _runs(rows, name_key, order_key) if _kernel_match(pat, nm) and len(rs) >= warmup + steps]
-    return runs[occurrence][-steps:]
+def _leg_rows(rows, name_key, order_key, pat, leg, steps):
+    """The timed dispatches of leg number `leg` of the child run: the last `steps` dispatches of its segment whose
+    kernel matches `pat` (set-up launches of the same kernel -- the encode before a decode leg -- come before them)."""
+    mine = [r for r in _leg_segments(rows, name_key, order_key)[leg] if _kernel_match(pat, r[name_key])]
+    if len(mine) < steps:
+        raise IndexError(f"leg {leg}: {len(mine)} dispatches of {pat}, {steps} expected")
+    return mine[-steps:]
 
 
-def _leg_stats(files, pat, occurrence, warmup, steps, alg_bytes):
-    """One leg's numbers from the three passes (the child runs the legs in order; `occurrence` counts the legs before
-    this one whose kernel matches the same pattern)."""
+def _leg_stats(files, pat, leg, steps, alg_bytes):
+    """One leg's numbers from the three passes (the child runs the legs in order; `leg` is this one's index)."""
     import csv
     out = {}
     st = [f for f in files["stats"] if f.endswith("kernel_stats.csv")]
     tr = [f for f in files["stats"] if f.endswith("kernel_trace.csv")]
-    timed = _leg_rows(list(csv.DictReader(open(tr[0]))), "Kernel_Name", "Start_Timestamp", pat, occurrence, warmup,
-                      steps)
+    timed = _leg_rows(list(csv.DictReader(open(tr[0]))), "Kernel_Name", "Start_Timestamp", pat, leg, steps)
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
     out["rocprof_kernel"] = timed[-1]["Kernel_Name"]
     out["rocprof_avg_ms"] = round(float(np.mean(dur)), 4)
@@ -916,7 +924,7 @@ def _leg_stats(files, pat, occurrence, warmup, steps, alg_bytes):
         cc = [f for f in files[tag] if f.endswith("counter_collection.csv")]
         vals = [float(r["Counter_Value"]) for r in _leg_rows([r for r in csv.DictReader(open(cc[0]))
                                                               if r["Counter_Name"] == tag], "Kernel_Name", "Dispatch_Id",
-                                                             pat, occurrence, warmup, steps)]
+                                                             pat, leg, steps)]
         if not vals:
             raise KeyError(f"no {tag} rows for kernel {pat}")
         out[tag + "_KiB"] = sum(vals) / len(vals)
@@ -952,7 +960,7 @@ def pmc_traffic(args, alg_bytes):
     files = {}
     try:
         files = _rocprof_passes(_child_base(args, args.workload), _PMC_PASSES)
-        return _leg_stats(files, pat, 0, args.warmup, args.steps, alg_bytes)
+        return _leg_stats(files, pat, 0, args.steps, alg_bytes)
     except (OSError, subprocess.SubprocessError, IndexError, KeyError, ValueError) as e:
         return None, {"error": f"{type(e).__name__}: {e}"}
     finally:
@@ -1013,10 +1021,7 @@ def device_legs(args, rank, world, dist, red_dev):
         try:
             files = _rocprof_passes(_child_base(args, "legs"), _PMC_PASSES, timeout=600)
             for i, (name, _) in enumerate(LEGS):
-                pat = KERNEL_PAT[name]
-                occurrence = sum(1 for nm, _ in LEGS[:i] if KERNEL_PAT[nm] == pat)
-                traffic, detail = _leg_stats(files, pat, occurrence, args.warmup, args.steps,
-                                             legs[i]["alg_bytes_per_launch"])
+                traffic, detail = _leg_stats(files, KERNEL_PAT[name], i, args.steps, legs[i]["alg_bytes_per_launch"])
                 legs[i]["traffic"] = traffic
                 legs[i]["pmc"] = detail
                 legs[i]["rocprof_avg_ms"] = detail["rocprof_avg_ms"]

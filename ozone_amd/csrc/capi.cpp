@@ -1076,9 +1076,21 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
   if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
   } else {
-    // unfused: encode, then one CRC pass per unit (crcs[s][u][w] layout kept)
+    // unfused: encode, then the CRC pass (crcs[s][u][w] layout kept): one launch over all S x units cells when they
+    // sit at one stride (the host batches' device layout [S][k + p][unit pitch]), else one per unit
     OZEC_HIP(ozec::launch_code(a, st));
-    for (int u = 0; u < units; ++u) {
+    const bool uniform = rows == enc->p && in_unit_stride == out_unit_stride && in_stripe_stride == out_stripe_stride &&
+                         d_out == d_in + k * in_unit_stride && in_stripe_stride == units * in_unit_stride;
+    if (uniform) {
+      CrcArgs c = e.crc;
+      c.base = d_in;
+      c.cell_stride = in_unit_stride;
+      c.ncells = static_cast<int64_t>(num_stripes) * units;
+      c.out = d_crcs;
+      c.out_cell_stride = nwin;
+      OZEC_HIP(ozec::launch_crc_windows(c, st));
+    }
+    for (int u = 0; u < units && !uniform; ++u) {
       CrcArgs c = e.crc;
       c.base = u < k ? d_in + u * in_unit_stride : d_out + (u - k) * out_unit_stride;
       c.cell_stride = u < k ? in_stripe_stride : out_stripe_stride;
@@ -1173,7 +1185,12 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
   const size_t C = std::min(num_stripes, stripes_per_chunk ? stripes_per_chunk
                                                           : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk.load())));
   const size_t nwin = with_crc ? (len + bpc - 1) / bpc : 0;
-  const size_t dstripe = static_cast<size_t>(k + p) * len;               // device layout [C][k+p][len]
+  // device layout [C][k+p][dunit]: the unit pitch is the cell length rounded up to 16 B, so every unit of the chunk
+  // buffer is 16-B aligned and the kernels take their vector paths whatever the length (a key's last, partial stripe:
+  // ECKeyOutputStream.java:276).  An odd pitch sent a 700,001-B stripe through the byte-wise kernels: 6.0 ms instead
+  // of 0.31 ms per stripe (bench.py --workload tail, round 5)
+  const size_t dunit = round_up(len, 16);
+  const size_t dstripe = static_cast<size_t>(k + p) * dunit;
   const size_t dcrc_off = round_up(C * dstripe, kStageAlign);            // then crcs [C][units][nwin]
   const size_t dbytes = dcrc_off + C * units * nwin * sizeof(uint32_t);
   const size_t ncrc = units * nwin;                                      // CRCs per stripe
@@ -1236,7 +1253,7 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
       for (size_t i = 0; i < cs; ++i)
         for (int r = 0; r < p; ++r)
           tasks.push_back({h_out + (s0 + i) * out_stripe_stride + r * out_unit_stride,
-                           P.hstage[b] + i * dstripe + static_cast<size_t>(k + r) * len, len});
+                           P.hstage[b] + i * dstripe + static_cast<size_t>(k + r) * dunit, len});
     if (with_crc && !crc_pinned)
       tasks.push_back({h_crcs + s0 * ncrc, P.hstage[b] + dcrc_off, cs * ncrc * sizeof(uint32_t)});
     ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, true, ctx->numa);
@@ -1253,7 +1270,7 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
         std::vector<ozec::CopyTask> tasks;
         for (size_t i = 0; i < cs; ++i)
           for (int j = 0; j < k; ++j)
-            tasks.push_back({P.hstage[b] + i * dstripe + static_cast<size_t>(j) * len,
+            tasks.push_back({P.hstage[b] + i * dstripe + static_cast<size_t>(j) * dunit,
                              h_in + (s0 + i) * in_stripe_stride + j * in_unit_stride, len});
         ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, true, ctx->numa);
       }
@@ -1272,8 +1289,12 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
     if (!in_pinned) {
       // staged cells are already in the device layout: one copy of the data cells per stripe
       for (size_t i = 0; i < cs; ++i)
-        OZEC_HIP(hipMemcpyAsync(d + i * dstripe, P.hstage[b] + i * dstripe, static_cast<size_t>(k) * len,
+        OZEC_HIP(hipMemcpyAsync(d + i * dstripe, P.hstage[b] + i * dstripe, static_cast<size_t>(k) * dunit,
                                 hipMemcpyHostToDevice, P.h2d));
+    } else if (dunit != len) {
+      for (size_t i = 0; i < cs; ++i)  // one rectangular copy per stripe: k rows of len bytes onto the unit pitch
+        OZEC_HIP(hipMemcpy2DAsync(d + i * dstripe, dunit, h_in + (s0 + i) * in_stripe_stride,
+                                  static_cast<size_t>(in_unit_stride), len, k, hipMemcpyHostToDevice, P.h2d));
     } else if (in_unit_stride == static_cast<int64_t>(len) && rect) {
       // one rectangular copy per chunk: cs rows of k*len bytes, source pitch = the batch's stripe stride
       OZEC_HIP(hipMemcpy2DAsync(d, dstripe, h_in + s0 * in_stripe_stride, static_cast<size_t>(in_stripe_stride),
@@ -1291,28 +1312,31 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
     }
     OZEC_HIP(hipEventRecord(P.h2d_done[b], P.h2d));
     OZEC_HIP(hipStreamWaitEvent(P.comp, P.h2d_done[b], 0));
-    const int64_t ds = static_cast<int64_t>(dstripe), us = static_cast<int64_t>(len);
+    const int64_t ds = static_cast<int64_t>(dstripe), us = static_cast<int64_t>(dunit);
     uint32_t *dcrc = reinterpret_cast<uint32_t *>(d + dcrc_off);
     if (with_crc) {
-      if (int rc = ozec_encode_crc_batch(enc, d, ds, us, d + static_cast<size_t>(k) * len, ds, us, cs, len,
+      if (int rc = ozec_encode_crc_batch(enc, d, ds, us, d + static_cast<size_t>(k) * dunit, ds, us, cs, len,
                                          checksum_type, bpc, dcrc, big_endian, P.comp))
         return rc;
     } else {
-      if (int rc = ozec_encode_batch(enc, d, ds, us, d + static_cast<size_t>(k) * len, ds, us, cs, len, P.comp))
+      if (int rc = ozec_encode_batch(enc, d, ds, us, d + static_cast<size_t>(k) * dunit, ds, us, cs, len, P.comp))
         return rc;
     }
     OZEC_HIP(hipEventRecord(P.comp_done[b], P.comp));
     OZEC_HIP(hipStreamWaitEvent(P.d2h, P.comp_done[b], 0));
     uint8_t *hs = staged ? P.hstage[b] : nullptr;
-    if (out_pinned && out_unit_stride == static_cast<int64_t>(len) && rect) {
+    if (out_pinned && out_unit_stride == static_cast<int64_t>(len) && dunit == len && rect) {
       OZEC_HIP(hipMemcpy2DAsync(h_out + s0 * out_stripe_stride, static_cast<size_t>(out_stripe_stride),
                                 d + static_cast<size_t>(k) * len, dstripe, static_cast<size_t>(p) * len, cs,
                                 hipMemcpyDeviceToHost, P.d2h));
     } else for (size_t i = 0; i < cs; ++i) {
-      uint8_t *src = d + i * dstripe + static_cast<size_t>(k) * len;
+      uint8_t *src = d + i * dstripe + static_cast<size_t>(k) * dunit;
       if (!out_pinned) {
-        OZEC_HIP(hipMemcpyAsync(hs + i * dstripe + static_cast<size_t>(k) * len, src, static_cast<size_t>(p) * len,
+        OZEC_HIP(hipMemcpyAsync(hs + i * dstripe + static_cast<size_t>(k) * dunit, src, static_cast<size_t>(p) * dunit,
                                 hipMemcpyDeviceToHost, P.d2h));
+      } else if (dunit != len) {
+        OZEC_HIP(hipMemcpy2DAsync(h_out + (s0 + i) * out_stripe_stride, static_cast<size_t>(out_unit_stride), src,
+                                  dunit, len, p, hipMemcpyDeviceToHost, P.d2h));
       } else if (out_unit_stride == static_cast<int64_t>(len)) {
         OZEC_HIP(hipMemcpyAsync(h_out + (s0 + i) * out_stripe_stride, src, static_cast<size_t>(p) * len,
                                 hipMemcpyDeviceToHost, P.d2h));
@@ -1437,7 +1461,21 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
       }
     }
     if (nrows) OZEC_HIP(ozec::launch_code(a, st));
-    for (int r = 0; r < n_erased; ++r) {
+    // the rebuilt units' CRCs: one launch over all S x n_erased cells when they sit at one stride, else one per unit
+    const bool uniform = out_stripe_stride == static_cast<int64_t>(n_erased) * out_unit_stride;
+    for (int r = nrows; r < n_erased && uniform; ++r)  // XOR decoders zero-fill outputs beyond erasedIndexes[0]
+      OZEC_HIP(hipMemset2DAsync(d_out + r * out_unit_stride, out_stripe_stride, 0, len, num_stripes, st));
+    if (uniform && n_erased) {
+      CrcArgs c = e.crc;
+      c.base = d_out;
+      c.cell_stride = out_unit_stride;
+      c.ncells = static_cast<int64_t>(num_stripes) * n_erased;
+      c.out = d_out_crcs;
+      c.out_cell_stride = nwin;
+      c.expected = nullptr;
+      OZEC_HIP(ozec::launch_crc_windows(c, st));
+    }
+    for (int r = 0; r < n_erased && !uniform; ++r) {
       if (r >= nrows) {  // XOR decoders zero-fill outputs beyond erasedIndexes[0]
         OZEC_HIP(hipMemset2DAsync(d_out + r * out_unit_stride, out_stripe_stride, 0, len, num_stripes, st));
       }
@@ -1500,7 +1538,8 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
   const size_t nwin = (len + bpc - 1) / bpc;
   // device layout of one chunk buffer: input slots [C][k+p][len], rebuilt [C][e][len], expected CRCs [C][k+p][nwin],
   // rebuilt CRCs [C][e][nwin], mismatch [C]
-  const size_t dstripe = static_cast<size_t>(n_all) * len, ostripe = static_cast<size_t>(e) * len;
+  const size_t dunit = round_up(len, 16);  // 16-B aligned unit pitch, as in encode_crc_host_batch_dev
+  const size_t dstripe = static_cast<size_t>(n_all) * dunit, ostripe = static_cast<size_t>(e) * dunit;
   const size_t dout_off = round_up(C * dstripe, kStageAlign);
   const size_t dexp_off = round_up(dout_off + C * ostripe, kStageAlign);
   const size_t dexp_bytes = h_expected ? C * n_all * nwin * sizeof(uint32_t) : 0;
@@ -1573,7 +1612,7 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
       for (size_t i = 0; i < cs; ++i)
         for (int r = 0; r < e; ++r)
           tasks.push_back({h_out + (s0 + i) * out_stripe_stride + r * out_unit_stride,
-                           P.hstage[b] + dout_off + i * ostripe + static_cast<size_t>(r) * len, len});
+                           P.hstage[b] + dout_off + i * ostripe + static_cast<size_t>(r) * dunit, len});
     if (!ocrc_pinned)
       tasks.push_back({h_out_crcs + s0 * e * nwin, P.hstage[b] + docrc_off, cs * e * nwin * sizeof(uint32_t)});
     if (!mis_pinned) tasks.push_back({h_mismatch + s0, P.hstage[b] + dmis_off, cs * sizeof(int32_t)});
@@ -1592,7 +1631,7 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
       if (!in_pinned)
         for (size_t i = 0; i < cs; ++i)
           for (int u : units)
-            tasks.push_back({hs + i * dstripe + static_cast<size_t>(u) * len,
+            tasks.push_back({hs + i * dstripe + static_cast<size_t>(u) * dunit,
                              h_in + (s0 + i) * in_stripe_stride + u * in_unit_stride, len});
       if (!exp_pinned)
         tasks.push_back({hs + dexp_off, h_expected + s0 * n_all * nwin, cs * n_all * nwin * sizeof(uint32_t)});
@@ -1603,16 +1642,21 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
       OZEC_HIP(hipStreamWaitEvent(P.h2d, P.d2h_done[b], 0));
     }
     for (const auto &run : runs) {
-      const size_t off = static_cast<size_t>(run.first) * len, width = static_cast<size_t>(run.second) * len;
+      const size_t off = static_cast<size_t>(run.first) * dunit, width = static_cast<size_t>(run.second) * dunit;
       if (!in_pinned) {
         OZEC_HIP(hipMemcpy2DAsync(d + off, dstripe, hs + off, dstripe, width, cs, hipMemcpyHostToDevice, P.h2d));
+      } else if (dunit != len) {
+        for (size_t i = 0; i < cs; ++i)  // one rectangular copy per stripe and run onto the unit pitch
+          OZEC_HIP(hipMemcpy2DAsync(d + i * dstripe + off, dunit,
+                                    h_in + (s0 + i) * in_stripe_stride + run.first * in_unit_stride,
+                                    static_cast<size_t>(in_unit_stride), len, run.second, hipMemcpyHostToDevice, P.h2d));
       } else if (in_unit_stride == static_cast<int64_t>(len)) {
         OZEC_HIP(hipMemcpy2DAsync(d + off, dstripe, h_in + s0 * in_stripe_stride + off,
                                   static_cast<size_t>(in_stripe_stride), width, cs, hipMemcpyHostToDevice, P.h2d));
       } else {
         for (size_t i = 0; i < cs; ++i)
           for (int u = run.first; u < run.first + run.second; ++u)
-            OZEC_HIP(hipMemcpyAsync(d + i * dstripe + static_cast<size_t>(u) * len,
+            OZEC_HIP(hipMemcpyAsync(d + i * dstripe + static_cast<size_t>(u) * dunit,
                                     h_in + (s0 + i) * in_stripe_stride + u * in_unit_stride, len, hipMemcpyHostToDevice,
                                     P.h2d));
       }
@@ -1624,8 +1668,8 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
     OZEC_HIP(hipEventRecord(P.h2d_done[b], P.h2d));
     OZEC_HIP(hipStreamWaitEvent(P.comp, P.h2d_done[b], 0));
     if (int rc = ozec_reconstruct_crc_batch(
-            dec, d, static_cast<int64_t>(dstripe), static_cast<int64_t>(len), present_units, num_present, erased, e,
-            d + dout_off, static_cast<int64_t>(ostripe), static_cast<int64_t>(len), cs, len, checksum_type, bpc,
+            dec, d, static_cast<int64_t>(dstripe), static_cast<int64_t>(dunit), present_units, num_present, erased, e,
+            d + dout_off, static_cast<int64_t>(ostripe), static_cast<int64_t>(dunit), cs, len, checksum_type, bpc,
             h_expected ? reinterpret_cast<const uint32_t *>(d + dexp_off) : nullptr, expected_big_endian,
             reinterpret_cast<uint32_t *>(d + docrc_off), out_big_endian,
             h_expected ? reinterpret_cast<int32_t *>(d + dmis_off) : nullptr, P.comp))
@@ -1635,6 +1679,10 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
     if (e) {
       if (!out_pinned) {
         OZEC_HIP(hipMemcpyAsync(hs + dout_off, d + dout_off, cs * ostripe, hipMemcpyDeviceToHost, P.d2h));
+      } else if (dunit != len) {
+        for (size_t i = 0; i < cs; ++i)
+          OZEC_HIP(hipMemcpy2DAsync(h_out + (s0 + i) * out_stripe_stride, static_cast<size_t>(out_unit_stride),
+                                    d + dout_off + i * ostripe, dunit, len, e, hipMemcpyDeviceToHost, P.d2h));
       } else if (out_unit_stride == static_cast<int64_t>(len)) {
         OZEC_HIP(hipMemcpy2DAsync(h_out + s0 * out_stripe_stride, static_cast<size_t>(out_stripe_stride), d + dout_off,
                                   ostripe, ostripe, cs, hipMemcpyDeviceToHost, P.d2h));

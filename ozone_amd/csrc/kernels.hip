@@ -928,7 +928,9 @@ int64_t stream_per_wave(int64_t total, int64_t bpc) {
     return (total + waves - 1) / waves;
   }
   const int64_t run = cr > 0 ? cr : int64_t{256} << 10;
-  return std::max<int64_t>(1, run / bpc);
+  // a small batch (one stripe's cells through the unfused path: tens of windows) is spread over at least ~2048 waves
+  // instead of a handful of 256 KiB runs; batches of 32 Ki windows and more keep the tuned run length
+  return std::max<int64_t>(1, std::min(run / bpc, total / 2048));
 }
 
 int64_t stream_grid(int64_t total, int64_t per_wave) {

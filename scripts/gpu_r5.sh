@@ -1,0 +1,58 @@
+#!/bin/bash
+# Round-5 GPU call: the fault probe's log phase, the whole GPU suite + smoke, the default bench line (C2 headline, every
+# device-resident leg with rocprof + PMC, C5 e2e multi-process and in-process, JNI per-call rows, CPU baseline), then
+# the probe's deterministic phase last (the one step that may fault).  Every GPU step has its own time limit; the
+# chain stops at the first failure.
+#   OUT=gpurun_out/r5a STEPS="probe tests bench fixed" scripts/gpu_r5.sh
+set -o pipefail
+OUT=${OUT:-gpurun_out/r5}
+STEPS=${STEPS:-probe tests bench fixed}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # name seconds cmd...
+  local name=$1 secs=$2
+  shift 2
+  echo "[gpu_r5 $(date +%T)] $name" | tee -a "$OUT/steps.log" >&2
+  timeout -k 10 "$secs" "$@"
+  local rc=$?
+  echo "[gpu_r5 $(date +%T)] $name rc=$rc" | tee -a "$OUT/steps.log" >&2
+  return $rc
+}
+for s in $STEPS; do
+  case $s in
+    probe)
+      for n in 65536 262144; do
+        run "probe log $n" 150 env AMD_LOG_LEVEL=4 python -u scripts/fault_probe.py log $n \
+          > "$OUT/probe_log_$n.out" 2> "$OUT/probe_log_$n.err" || exit 1
+        gzip -f "$OUT/probe_log_$n.err"
+      done ;;
+    tests)
+      run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 2; }
+      tail -3 "$OUT/pytest_gpu.log"
+      run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 3 ;;
+    bench)
+      run bench 900 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || { tail -20 "$OUT/bench_default.err"; exit 4; } ;;
+    jni)
+      run jni 300 python -u bench.py --workload jni > "$OUT/bench_jni.json" 2> "$OUT/bench_jni.err" || exit 5 ;;
+    tail)
+      run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
+    heap)
+      for n in 65536 262144; do
+        run "probe heap $n" 150 env AMD_LOG_LEVEL=4 python -u scripts/fault_probe.py heap $n \
+          > "$OUT/probe_heap_$n.out" 2> "$OUT/probe_heap_$n.err"
+        rc=$?
+        gzip -f "$OUT/probe_heap_$n.err"
+        [ $rc -eq 0 ] || exit 8
+      done ;;
+    fixed)
+      for n in 65536 262144; do
+        run "probe fixed $n" 150 env AMD_LOG_LEVEL=4 python -u scripts/fault_probe.py fixed $n \
+          > "$OUT/probe_fixed_$n.out" 2> "$OUT/probe_fixed_$n.err"
+        rc=$?
+        gzip -f "$OUT/probe_fixed_$n.err"
+        [ $rc -eq 0 ] || exit 7
+      done ;;
+  esac
+done
+echo "[gpu_r5 $(date +%T)] done" | tee -a "$OUT/steps.log"

@@ -1,11 +1,14 @@
 """bench.py's selection of each leg's timed dispatches in the rocprofv3 child run (every leg of the
-default line gets its rocprof average and PMC traffic).  The child runs the legs in order; a leg's warm-up and timed
-steps are one unbroken run of its kernel, its set-up launches other kernels first.  Synthetic trace rows, CPU only."""
+default line gets its rocprof average and PMC traffic).  The child runs the legs in order; each leg's set-up starts
+with the synthetic-data fill kernel, and its steps may launch other kernels between the measured ones (the
+reconstruction's mismatch finisher, the runtime's memset of a new WorkQueue slot).  Synthetic trace rows, CPU only."""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+import pytest  # noqa: E402
 
 import bench  # noqa: E402
 
@@ -24,10 +27,11 @@ def _legs_sequence(W, K):
                                                "crc_windows_g26s<4, 2, true>", "encode_crc_g26<2, 1, 2>",
                                                "fill_splitmix64")
     for name, _ in bench.LEGS:
-        if name == "c5dev":
-            seq += [fill] * 6 + [nb63] * (W + K)
+        if name == "c5dev":  # the persistent kernel's first launches each zero a new WorkQueue slot (a memset kernel)
+            ms = "__amd_rocclr_fillBufferAligned"
+            seq += [fill] * 6 + [nb63, ms, nb63, ms, nb63] + [nb63, ms] * 5 + [nb63] * (W + K - 8)
         elif name == "c3r":
-            seq += [fill] * 10 + [gf104, crc] + [nb104] * (W + K)
+            seq += [fill] * 10 + [gf104, crc] + [nb104, "finish_mismatch"] * (W + K)
         elif name == "c3":
             seq += [fill] * 10 + [gf104] + [gf104] * (W + K)  # the set-up encode runs into the decode steps
         elif name == "crc":
@@ -43,29 +47,38 @@ def test_each_leg_gets_its_own_timed_dispatches():
     W, K = 5, 20
     rows = _trace(_legs_sequence(W, K))
     seen = set()
+    last_end = -1
     for i, (name, _) in enumerate(bench.LEGS):
         pat = bench.KERNEL_PAT[name]
-        occ = sum(1 for nm, _ in bench.LEGS[:i] if bench.KERNEL_PAT[nm] == pat)
-        got = bench._leg_rows(rows, "Kernel_Name", "Start_Timestamp", pat, occ, W, K)
+        got = bench._leg_rows(rows, "Kernel_Name", "Start_Timestamp", pat, i, K)
         assert len(got) == K
         assert len({r["Kernel_Name"] for r in got}) == 1 and bench._kernel_match(pat, got[0]["Kernel_Name"])
         ts = [int(r["Start_Timestamp"]) for r in got]
-        assert ts == sorted(ts) and ts[-1] - ts[0] == 1000 * (K - 1)  # consecutive dispatches
-        assert not seen & set(ts)  # no two legs share a dispatch
+        assert ts == sorted(ts) and ts[0] > last_end  # legs in order, none sharing a dispatch
+        assert not seen & set(ts)
         seen |= set(ts)
-    # the verify leg is the second run of crc_windows_g26s: the verify kernel, not the compute one
+        last_end = ts[-1]
+    # the verify leg's timed dispatches are the verify kernel's, not the set-up CRC launch before them
     i = [n for n, _ in bench.LEGS].index("verify")
-    got = bench._leg_rows(rows, "Kernel_Name", "Start_Timestamp", bench.KERNEL_PAT["verify"], 1, W, K)
-    assert got[0]["Kernel_Name"].endswith("true>") and i > [n for n, _ in bench.LEGS].index("crc")
+    got = bench._leg_rows(rows, "Kernel_Name", "Start_Timestamp", bench.KERNEL_PAT["verify"], i, K)
+    assert all(r["Kernel_Name"].endswith("true>") for r in got)
+    # c3: the set-up encode of the same kernel precedes the decode steps and is not among them
+    i = [n for n, _ in bench.LEGS].index("c3")
+    seg = bench._leg_segments(rows, "Kernel_Name", "Start_Timestamp")[i]
+    first_gf = min(int(r["Start_Timestamp"]) for r in seg if r["Kernel_Name"].startswith("gf_code_vec"))
+    got = bench._leg_rows(rows, "Kernel_Name", "Start_Timestamp", bench.KERNEL_PAT["c3"], i, K)
+    assert int(got[0]["Start_Timestamp"]) > first_gf
 
 
 def test_pmc_rows_order_by_dispatch_id():
-    """counter rows carry Dispatch_Id, not timestamps; the same runs come out"""
+    """counter rows carry Dispatch_Id, not timestamps, and come in any order; too few dispatches is an error"""
     W, K = 2, 3
-    seq = ["fill"] + ["a<1>"] * (W + K) + ["fill"] + ["a<1>"] * (W + K + 1)
+    seq = ["fill_splitmix64"] + ["a<1>"] * (W + K) + ["fill_splitmix64"] * 2 + ["a<1>", "b"] * (W + K + 1)
     rows = [{"Kernel_Name": k, "Dispatch_Id": str(i + 1), "Counter_Value": str(i)} for i, k in enumerate(seq)]
-    rows = rows[::-1]  # file order does not matter
-    first = bench._leg_rows(rows, "Kernel_Name", "Dispatch_Id", "a<", 0, W, K)
-    second = bench._leg_rows(rows, "Kernel_Name", "Dispatch_Id", "a<", 1, W, K)
+    rows = rows[::-1]
+    first = bench._leg_rows(rows, "Kernel_Name", "Dispatch_Id", "a<", 0, K)
+    second = bench._leg_rows(rows, "Kernel_Name", "Dispatch_Id", "a<", 1, K)
     assert [int(r["Dispatch_Id"]) for r in first] == [4, 5, 6]
-    assert [int(r["Dispatch_Id"]) for r in second] == [11, 12, 13]
+    assert [int(r["Dispatch_Id"]) for r in second] == [15, 17, 19]
+    with pytest.raises(IndexError):
+        bench._leg_rows(rows, "Kernel_Name", "Dispatch_Id", "a<", 0, W + K + 1)

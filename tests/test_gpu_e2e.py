@@ -242,9 +242,6 @@ def test_reconstruct_host_batch_errors():
                                        4 * 4096, 4096, 1, 4096, ck.ChecksumType.CRC32C, 4096, np.zeros(4, np.uint32))
 
 
-_KEEP_REGISTERED = []  # host ranges this process registered and unregistered, kept mapped until exit
-
-
 def test_pinned_memory_is_numa_local():
     """ozec_host_alloc places its pages on the GPU's NUMA node (mbind before the pinning touch)."""
     node = device_numa_node(0)
@@ -262,7 +259,8 @@ def test_pinned_memory_is_numa_local():
     host_register(addr, 16 << 20, 0)
     assert page_node(addr) == node and page_node(addr + (16 << 20) - 1) == node
     host_unregister(addr)
-    _KEEP_REGISTERED.append((mm, anchor))  # not unmapped before exit (test_gpu_parity.py _KEEP_REGISTERED)
+    del anchor
+    mm.close()  # unregistered, then unmapped, as a caller would ("GPU faults")
 
 
 def _free_port():
@@ -430,3 +428,46 @@ def test_device_list_errors_and_default(device_list):
         rc.set_device_policy(name)
         assert rc.RawErasureEncoder(rc.ECReplicationConfig(3, 2)).device in range(n)
     rc.set_device_policy("round_robin")
+
+
+@pytest.mark.parametrize("n", [1007, 50001, 700001])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_batches_of_odd_cells_vs_oracle(n, pinned):
+    """A key's last, partial stripe has cells of any length (parityCellSize = dataBuffers[0].position(),
+    ECKeyOutputStream.java:276).  The host batches lay such cells out on a 16-B aligned unit pitch on the device
+    (capi.cpp dunit), so the kernels keep their vector paths; contiguous odd cells (unit stride = length, the
+    rectangular per-stripe copies) and a gapped layout, encode + CRC32C and the fused reconstruction, vs the oracle."""
+    k, p, S, bpc = 6, 3, 5, 16384
+    for gap in (0, 3):
+        buf, v, us = _batch(S, k, p, n, 4100 + n % 97 + gap, gap)
+        keep = None
+        if pinned:
+            keep = host_alloc(buf.nbytes)
+            keep.array[:] = buf
+            buf = keep.array
+            v = buf.reshape(S, k + p, us)
+        nwin = -(-n // bpc)
+        crcs = np.zeros(S * (k + p) * nwin, np.uint32)
+        enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+        enc.encode_crc_host_batch(buf.ctypes.data, (k + p) * us, us, buf.ctypes.data + k * us, (k + p) * us, us, S, n,
+                                  ck.ChecksumType.CRC32C, bpc, crcs, False, 2)
+        _check(v, crcs, "rs", k, p, n, S, ck.ChecksumType.CRC32C, bpc)
+        erased = [0, 4, 7]
+        present = [u for u in range(k + p) if u not in erased]
+        stored = crcs.reshape(S, k + p, nwin).copy()
+        truth = [[np.array(v[s, u, :n]) for u in erased] for s in range(S)]
+        out = np.zeros(S * 3 * n, np.uint8)
+        ocrc = np.zeros(S * 3 * nwin, np.uint32)
+        mism = np.zeros(S, np.int32)
+        dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
+        dec.reconstruct_crc_host_batch(buf, (k + p) * us, us, present, erased, out, 3 * n, n, S, n,
+                                       ck.ChecksumType.CRC32C, bpc, ocrc, h_expected=stored.reshape(-1),
+                                       h_mismatch=mism, stripes_per_chunk=2)
+        got, oc = out.reshape(S, 3, n), ocrc.reshape(S, 3, nwin)
+        assert (mism == -1).all(), (n, pinned, gap)
+        for s in range(S):
+            for q, u in enumerate(erased):
+                assert (got[s, q] == truth[s][q]).all() and (oc[s, q] == stored[s, u]).all(), (n, pinned, gap, s, u)
+        if keep is not None:
+            del v, buf
+            keep.free()

@@ -884,12 +884,6 @@ def test_host_path_pinned_buffers_dma_in_place(codec, k, p, n):
     pool.free()
 
 
-# Host memory this process registered (ozec_host_register) stays allocated until exit after it is unregistered: a
-# registered, unregistered and unmapped address range handed back by the kernel for a new pageable buffer is suspected
-# of faulting HIP's pageable copies (torch's .to / .cpu) in later tests ("GPU faults").
-_KEEP_REGISTERED = []
-
-
 @pytest.mark.parametrize("n", [1 << 16, 1 << 18])
 def test_host_path_separately_pinned_cells_at_one_stride(n):
     """cells at one constant stride that are pinned as SEPARATE allocations (one ozec_host_register per cell
@@ -922,10 +916,10 @@ def test_host_path_separately_pinned_cells_at_one_stride(n):
         dins = [None] + cells_[1:7] + [None] + cells_[8:]
         dec("rs", k, p).decode(dins, [0, 7], outs)
         assert all((o == t_).all() for o, t_ in zip(outs, truth))
-    finally:
+    finally:  # unregistered and freed as a caller would ("GPU faults": this sequence preceded two of them)
         for a in regs:
             host_unregister(a)
-        _KEEP_REGISTERED.append(buf)
+        del cells_, buf
 
 
 def test_host_graph_replays_match_the_oracle():

@@ -465,6 +465,9 @@ class Workload:
 # ------------------------------------------------------------------------------------------ C5 end to end
 
 
+_KEEP_MAPPED = []  # host ranges this process registered: mapped until exit (include/ozec.h, ozec_host_unregister)
+
+
 class HostBatch:
     """One batch of rs-6-3-1024k stripes in host memory shared by every rank ([stripe][9 units][1 MiB], then a
     CRC area with one page-aligned slot per rank), so the ranks really split ONE batch.  Each rank places its own
@@ -554,15 +557,14 @@ class HostBatch:
         return [page_node(self.base + self.data_off), page_node(self.base + self.data_off + self.data_len - 1)]
 
     def close(self, dist):
+        """Unregister; the mapping itself stays until the process exits (include/ozec.h: a range registered with
+        ozec_host_register stays mapped, DESIGN §4 "GPU faults"); the shared-memory object was unlinked at creation,
+        so its pages go with the last rank."""
         from ozone_amd.stripe_queue import host_unregister
         for a in self.registered:
             host_unregister(a)
         self.registered = []
-        del self._anchor
-        try:
-            self.mm.close()
-        except BufferError:  # a numpy view still alive: the mapping goes with the process
-            pass
+        _KEEP_MAPPED.append((self.mm, self._anchor))
         if dist is not None:
             dist.barrier()
 

@@ -268,10 +268,22 @@ int ozec_host_free(void *p);
 int ozec_device_numa_node(int device, int *node);
 /* NUMA node holding the (touched) page at p, -1 if unknown -- placement diagnostics */
 int ozec_host_page_node(const void *p, int *node);
+/* copy `count` host regions (dst[i] <- src[i], bytes[i]) with libozec's parallel copy pool -- the workers of the NUMA
+ * node of the calling thread's GPU, the caller taking part -- and return when all are done.  For glue layers that move
+ * caller memory to and from pinned buffers themselves: the JNI drop-in copies Java byte[] regions (held with
+ * GetPrimitiveArrayCritical for the copy only) into its pinned arena, as AbstractNativeRawEncoder.java:80-93 copies
+ * heap arrays into direct buffers.  to_pinned: the destinations are pinned buffers a DMA reads next (streaming stores
+ * where the CPU has them). */
+int ozec_host_copy(void *const *dst, const void *const *src, const size_t *bytes, int count, int to_pinned);
 /* pin caller-owned memory for DMA (e.g. one rank's stripe range of a batch shared between processes), placing
  * its pages on `device`'s NUMA node first (device < 0: no placement; only pages wholly inside the range move).
  * Placement is best effort: where the kernel refuses it the memory is pinned where it lies, and
- * ozec_host_placement_failures() counts such calls.  ozec_host_unregister undoes the pinning */
+ * ozec_host_placement_failures() counts such calls.  ozec_host_unregister undoes the pinning.
+ * Keep a range registered here MAPPED until the process exits, even after ozec_host_unregister: caller memory that
+ * was registered, unregistered and handed back to the allocator was followed, in the same process, by
+ * hipErrorIllegalAddress in HIP's next large pageable copy (one HIP does itself by locking the caller's pages; no
+ * libozec code runs in it) -- DESIGN.md 4, "GPU faults".  Memory that comes and goes should come from ozec_host_alloc /
+ * ozec_host_free: libozec never returns a range it registered to the kernel (its address range stays reserved). */
 int ozec_host_register(void *p, size_t bytes, int device);
 uint64_t ozec_host_placement_failures(void);
 int ozec_host_unregister(void *p);

@@ -11,8 +11,8 @@
  *                                    -> hadoop's performEncodeImpl / performDecodeImpl (HadoopNativeECAccessorUtil :32-58)
  *   encodeArrays / decodeArrays   <- doEncode(ByteArrayEncodingState) / doDecode(ByteArrayDecodingState); the reference
  *                                    copies heap arrays into direct buffers (:80-93), here into a pooled pinned
- *                                    arena (GetByteArrayRegion / SetByteArrayRegion, never a critical pin across
- *                                    device work: heap_* below)
+ *                                    arena (arrays held critical for the parallel copy only, never across device
+ *                                    work: heap_* below)
  *   coderCreate / coderRelease    <- NativeRSRawEncoder ctor / release (EC/rawcoder/NativeRSRawEncoder.java:39-62)
  *   crcUpdate* / checksumWindows* <- ChecksumByteBuffer.update (CM/ChecksumByteBuffer.java:32-44) and
  *                                    Checksum.computeChecksum (CM/Checksum.java:157-200)
@@ -110,10 +110,11 @@ static void refs_free(JNIEnv *env, array_set *as) {
 /* ---------------------------------------------------------------- heap arrays: copied, never pinned across the GPU
  * A byte[] pinned with GetPrimitiveArrayCritical for the whole call would hold the VM's GC locker through staging, H2D,
  * kernel and D2H (~0.3 ms per rs-6-3 stripe of 1 MiB cells; every ECKeyOutputStream writer passes heap buffers,
- * ECKeyOutputStream.java:701).  Instead each call copies the regions it reads with GetByteArrayRegion into a pinned
- * arena (ozec_host_alloc: pinned, on a listed GPU's NUMA node), runs on the arena -- libozec DMAs pinned memory in
- * place, one rectangular copy each way for cells at one stride -- and copies the outputs back with SetByteArrayRegion:
- * the two host copies libozec's own staging would make, with no JNI pin while libozec works, as the reference's bridge
+ * ECKeyOutputStream.java:701).  Instead each call copies the regions it reads into a pinned arena (ozec_host_alloc:
+ * pinned, on a listed GPU's NUMA node; the arrays held critical for that copy only, copy_regions), runs on the arena --
+ * libozec DMAs pinned memory in place, one rectangular copy each way for cells at one stride -- and copies the outputs
+ * back the same way: the two host copies libozec's own staging would make, with no JNI pin while libozec works, as the
+ * reference's bridge
  * copies heap arrays into direct buffers (AbstractNativeRawEncoder.java:80-93).  Calls are cut in column chunks of
  * HEAP_CHUNK bytes per cell (coding is byte-position-wise), so an arena holds at most (k + p) x 4 MiB.
  * Arenas come from a process-wide pool of ARENA_POOL, leased for one call: pinned memory stays bounded however many
@@ -246,6 +247,46 @@ static uint8_t *arena(arena_lease *l, size_t bytes, ozm_status *st) {
 
 static int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
+/* The array copies: every array of the set held with GetPrimitiveArrayCritical for the copy ONLY (released before
+ * libozec does any device work), and the regions moved by ozec_host_copy -- libozec's parallel copy pool on the GPU's
+ * NUMA node, as its own staging copies are -- instead of one GetByteArrayRegion after another on the calling thread:
+ * one rs-6-3 stripe of 1 MiB heap cells spends ~150 us in that single-threaded copy-in (bench.py jni rows).  Nothing
+ * in a critical section calls JNI or waits for a Java thread (the pool's workers are native threads).  An array the VM
+ * will not hand out (NULL) falls back to Get/SetByteArrayRegion. */
+static void copy_regions(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl,
+                         const ozm_buf *stage, int in) {
+  void *pin[MAX_BUFS] = {0};
+  void *dst[MAX_BUFS];
+  const void *src[MAX_BUFS];
+  size_t nb[MAX_BUFS];
+  int n = 0, slow = 0;
+  for (int i = 0; i < as->n; ++i) {
+    if (!as->arr[i] || !stage[i].present) continue;
+    pin[i] = (*env)->GetPrimitiveArrayCritical(env, as->arr[i], NULL);
+    if (!pin[i]) {
+      slow = 1;
+      continue;
+    }
+    uint8_t *arr = (uint8_t *)pin[i] + bufs[i].offset + off;
+    dst[n] = in ? (void *)stage[i].base : (void *)arr;
+    src[n] = in ? (const void *)arr : (const void *)stage[i].base;
+    nb[n] = (size_t)cl;
+    ++n;
+  }
+  const int rc = n ? ozec_host_copy(dst, src, nb, n, in) : 0;
+  for (int i = 0; i < as->n; ++i)
+    if (pin[i]) (*env)->ReleasePrimitiveArrayCritical(env, as->arr[i], pin[i], in ? JNI_ABORT : 0);
+  if (!slow && !rc) return;
+  for (int i = 0; i < as->n; ++i) {  /* the arrays not copied above, or all of them if the pool failed */
+    if (!as->arr[i] || !stage[i].present || (pin[i] && !rc)) continue;
+    if (in)
+      (*env)->GetByteArrayRegion(env, as->arr[i], (jsize)(bufs[i].offset + off), (jsize)cl, (jbyte *)stage[i].base);
+    else
+      (*env)->SetByteArrayRegion(env, as->arr[i], (jsize)(bufs[i].offset + off), (jsize)cl,
+                                 (const jbyte *)stage[i].base);
+  }
+}
+
 /* the present arrays' regions [offset + off, + cl) into consecutive arena slots of `stride` bytes from slot `first`
  * (absent ones take no slot); stage[i] describes the copy as a buffer at offset 0 */
 static void copy_in(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl, uint8_t *base,
@@ -254,12 +295,11 @@ static void copy_in(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64
   for (int i = 0; i < as->n; ++i) {
     memset(&stage[i], 0, sizeof(stage[i]));
     if (!as->arr[i]) continue;
-    uint8_t *dst = base + (int64_t)slot++ * stride;
-    (*env)->GetByteArrayRegion(env, as->arr[i], (jsize)(bufs[i].offset + off), (jsize)cl, (jbyte *)dst);
     stage[i].present = 1;
-    stage[i].base = dst;
+    stage[i].base = base + (int64_t)slot++ * stride;
     stage[i].capacity = cl;
   }
+  copy_regions(env, as, bufs, off, cl, stage, 1);
 }
 
 static void out_slots(const array_set *as, int64_t cl, uint8_t *base, int64_t stride, int first, ozm_buf *stage) {
@@ -273,10 +313,7 @@ static void out_slots(const array_set *as, int64_t cl, uint8_t *base, int64_t st
 
 static void copy_out(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl,
                      const ozm_buf *stage) {
-  for (int i = 0; i < as->n; ++i)
-    if (as->arr[i])
-      (*env)->SetByteArrayRegion(env, as->arr[i], (jsize)(bufs[i].offset + off), (jsize)cl,
-                                 (const jbyte *)stage[i].base);
+  copy_regions(env, as, bufs, off, cl, stage, 0);
 }
 
 static int present_count(const array_set *as) {

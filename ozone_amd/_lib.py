@@ -112,6 +112,7 @@ _SIGS = {
     "ozec_host_free": (ctypes.c_int, [c_voidp]),
     "ozec_device_numa_node": (ctypes.c_int, [ctypes.c_int, c_intp]),
     "ozec_host_page_node": (ctypes.c_int, [c_voidp, c_intp]),
+    "ozec_host_copy": (ctypes.c_int, [c_voidp, c_voidp, c_voidp, ctypes.c_int, ctypes.c_int]),
     "ozec_host_register": (ctypes.c_int, [c_voidp, c_size, ctypes.c_int]),
     "ozec_host_placement_failures": (ctypes.c_uint64, []),
     "ozec_host_unregister": (ctypes.c_int, [c_voidp]),

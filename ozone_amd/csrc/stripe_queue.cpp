@@ -268,6 +268,26 @@ int ozec_host_page_node(const void *p, int *node) {
   return OZEC_OK;
 }
 
+int ozec_host_copy(void *const *dst, const void *const *src, const size_t *bytes, int count, int to_pinned) {
+  if (count < 0 || (count > 0 && (!dst || !src || !bytes))) return set_error(OZEC_EINVAL, "null copy list");
+  std::vector<ozec::CopyTask> tasks;
+  tasks.reserve(static_cast<size_t>(count));
+  for (int i = 0; i < count; ++i) {
+    if (bytes[i] == 0) continue;
+    if (!dst[i] || !src[i]) return set_error(OZEC_EINVAL, "null pointer in the copy list");
+    tasks.push_back({dst[i], src[i], bytes[i]});
+  }
+  // the pool of the NUMA node of this thread's GPU, whose pinned buffers the copies fill or drain (cached per thread)
+  thread_local int dev = -2, node = -1;
+  const int d = ozec::thread_device();
+  if (d != dev) {
+    dev = d;
+    node = d >= 0 ? ozec::device_numa_node(d) : -1;
+  }
+  ozec::parallel_copy(tasks, to_pinned ? ozec::CopyDir::kToStaging : ozec::CopyDir::kFromStaging, true, node);
+  return OZEC_OK;
+}
+
 int ozec_host_register(void *p, size_t bytes, int device) {
   if (!p) return set_error(OZEC_EINVAL, "null pointer");
   if (bytes == 0) return OZEC_OK;

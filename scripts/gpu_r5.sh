@@ -35,6 +35,9 @@ for s in $STEPS; do
       run bench 900 python -u bench.py > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || { tail -20 "$OUT/bench_default.err"; exit 4; } ;;
     jni)
       run jni 300 python -u bench.py --workload jni > "$OUT/bench_jni.json" 2> "$OUT/bench_jni.err" || exit 5 ;;
+    rehearse)  # the N = 2 path on one GPU: two gloo ranks on device 0, C2 + C5 multi-process + in-process legs
+      run rehearse 600 env OZEC_BENCH_SAME_DEVICE=1 OZEC_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 5 \
+        --warmup 2 --no-legs --no-jni > "$OUT/bench_2rank.json" 2> "$OUT/bench_2rank.err" || { tail -20 "$OUT/bench_2rank.err"; exit 9; } ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     heap)

@@ -242,6 +242,9 @@ def test_reconstruct_host_batch_errors():
                                        4 * 4096, 4096, 1, 4096, ck.ChecksumType.CRC32C, 4096, np.zeros(4, np.uint32))
 
 
+_REGISTERED_KEEP = []  # caller memory registered with ozec_host_register stays mapped until exit (include/ozec.h)
+
+
 def test_pinned_memory_is_numa_local():
     """ozec_host_alloc places its pages on the GPU's NUMA node (mbind before the pinning touch)."""
     node = device_numa_node(0)
@@ -259,8 +262,7 @@ def test_pinned_memory_is_numa_local():
     host_register(addr, 16 << 20, 0)
     assert page_node(addr) == node and page_node(addr + (16 << 20) - 1) == node
     host_unregister(addr)
-    del anchor
-    mm.close()  # unregistered, then unmapped, as a caller would ("GPU faults")
+    _REGISTERED_KEEP.append((mm, anchor))  # mapped until exit (ozec.h, ozec_host_unregister)
 
 
 def _free_port():

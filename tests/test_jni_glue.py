@@ -393,9 +393,10 @@ def test_device_list_natives(J, java):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [1 << 16, (4 << 20) + 4096 + 3])  # one chunk; two chunks of the 4 MiB arena
 def test_heap_arrays_never_pinned_across_device_work(J, java, n):
-    """byte[] inputs and outputs are copied (Get/SetByteArrayRegion) into a pooled pinned arena, and
-    no array is pinned while libozec works -- the mock records the array pins outstanding at every wrapped ozec_encode
-    / ozec_decode / ozec_crc_update / ozec_checksum_windows call.  Results vs the oracle, calls longer than one arena
+    """byte[] inputs and outputs are copied into a pooled pinned arena (coder calls: the arrays held
+    critical for the parallel copy only, ozec_host_copy; checksum calls: Get/SetByteArrayRegion), and no array is
+    pinned while libozec works -- the mock records the array pins outstanding at every wrapped ozec_encode /
+    ozec_decode / ozec_crc_update / ozec_checksum_windows call.  Results vs the oracle, calls longer than one arena
     chunk included, inputs untouched and outputs written only inside their regions."""
     k, p, pos = 3, 2, 7
     h = call(J, "coderCreate", 0, 0, k, p)

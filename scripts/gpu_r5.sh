@@ -38,6 +38,11 @@ for s in $STEPS; do
     rehearse)  # the N = 2 path on one GPU: two gloo ranks on device 0, C2 + C5 multi-process + in-process legs
       run rehearse 600 env OZEC_BENCH_SAME_DEVICE=1 OZEC_DIST_BACKEND=gloo python -u bench.py --gpus 2 --steps 5 \
         --warmup 2 --no-legs --no-jni > "$OUT/bench_2rank.json" 2> "$OUT/bench_2rank.err" || { tail -20 "$OUT/bench_2rank.err"; exit 9; } ;;
+    prof)  # rocprofv3 kernel statistics of the headline and of every leg with the bench's own warm-up and steps
+      run "prof c2" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c2" -o run --output-format csv -- python3 bench.py \
+        --workload c2 --no-cpu --no-pmc --no-e2e --no-legs --no-jni > "$OUT/prof_c2.log" 2>&1 || exit 10
+      run "prof legs" 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_legs" -o run --output-format csv -- python3 \
+        bench.py --workload legs --no-cpu --no-pmc > "$OUT/prof_legs.log" 2>&1 || exit 11 ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     heap)

@@ -833,6 +833,7 @@ def cpu_baseline(workload, budget_s):
 
 HOST_PINNED = False  # --host-pinned (host workload)
 ORIG_AFFINITY = None  # the CPUs the process was started with, before each rank binds itself to its GPU's node
+TUNE = []  # --tune KEY=VALUE knobs, also handed to the JNI harness (OZEC_TUNE)
 
 KERNEL_PAT = {"c1": "gf_code_vec<3, 2", "c2": "gf_code_vec<6, 3", "c3": "gf_code_vec<10, 4",
               "c3r": ("encode_crc_nb<10, 4", "encode_crc_lv<10, 4", "encode_crc_g26<10, 4"), "c4": "encode_crc_g26<2, 1",
@@ -1171,7 +1172,7 @@ def _jni_percall_bin():
 def jni_percall(specs, seconds, dev=0):
     """Run the JNI harness over `specs` ("encode:6:3:65536:4", ...) in one child process pinned to GPU `dev`
     (OZEC_DEVICES), one JSON row per spec."""
-    env = dict(os.environ, OZEC_DEVICES=str(dev))
+    env = dict(os.environ, OZEC_DEVICES=str(dev), OZEC_TUNE=",".join(TUNE))
     r = subprocess.run([_jni_percall_bin(), str(seconds)] + list(specs), capture_output=True, text=True,
                        timeout=120 + 4 * seconds * len(specs), env=env)
     if r.returncode != 0:
@@ -1343,6 +1344,7 @@ def main():
             cpu_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(backend)
+    TUNE[:] = args.tune
     if args.tune:
         from ozone_amd import _lib
         for kv in args.tune:

@@ -59,6 +59,7 @@ int fail(int code, const std::string &msg) {
 struct Slot {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // D2H of a duplex direct call (staged_pipeline), created on first use
   uint8_t *pinned = nullptr;  // on the device's NUMA node (numa.hpp)
   size_t pinned_cap = 0;
   uint8_t *dbuf = nullptr;
@@ -135,9 +136,19 @@ struct Slot {
     return OZEC_OK;
   }
 
+  int ensure_events(size_t n) {
+    while (events.size() < n) {
+      hipEvent_t e;
+      OZEC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      events.push_back(e);
+    }
+    return OZEC_OK;
+  }
+
   // give the staging buffers back (an idle slot: its stream has drained)
   void shrink() {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (stream2) (void)hipStreamSynchronize(stream2);
     drop_graphs();
     if (pinned) (void)ozec::pinned_free(pinned);
     if (dbuf) (void)hipFree(dbuf);
@@ -443,9 +454,12 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
   // drain the slot's stream before the lease hands the slot to the next caller (declared after the lease, so
   // it runs first).
   struct DrainOnExit {
-    hipStream_t st;
-    ~DrainOnExit() { (void)hipStreamSynchronize(st); }
-  } drain{s->stream};
+    Slot *s;
+    ~DrainOnExit() {
+      (void)hipStreamSynchronize(s->stream);
+      if (s->stream2) (void)hipStreamSynchronize(s->stream2);
+    }
+  } drain{s};
   // Caller buffers that are all pinned (ozec_host_alloc / ozec_host_register; Java: OzecNative.allocatePinned) are
   // DMA'd in place: no staging copy and no chunking.  Units at one constant stride (a buffer pool's cells) go up and
   // come back as one rectangular copy each way; otherwise one copy per unit, which pays only for large cells (each
@@ -474,6 +488,41 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     const size_t dcp = round_up(len, kStageAlign), dop = round_up(obytes, kStageAlign);
     if (int rc = s->reserve_device(nin * dcp + nout * dop)) return rc;
     uint8_t *d = s->dbuf;
+    // Duplex (coding calls of large cells): the units go up, through the kernel and back in column chunks, the D2H
+    // of chunk c on the slot's second stream while the H2D of chunk c+1 runs on the first, so the two link
+    // directions overlap inside one call instead of running one after the other (a lone writer's 1 MiB-cell stripe:
+    // 6 MiB up, 3 MiB down).  Coding is byte-position-wise, so a column chunk is a complete call of its own.
+    const int64_t duplex = ozec::g_tune.host_duplex.load(std::memory_order_relaxed);
+    if (duplex > 0 && len >= static_cast<size_t>(duplex) && obytes == len && out_pos(0) == 0) {
+      const size_t cw = std::max<size_t>(256u << 10, round_up((len + 7) / 8, 4096));
+      const size_t nc = (len + cw - 1) / cw;
+      if (!s->stream2) OZEC_HIP(hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking));
+      if (int rc = s->ensure_events(nc)) return rc;
+      for (size_t c = 0; c < nc; ++c) {
+        const size_t off = c * cw, cl = std::min(cw, len - off);
+        if (rect) {
+          OZEC_HIP(hipMemcpy2DAsync(d + off, dcp, in[0] + off, static_cast<size_t>(sin), cl, nin, hipMemcpyHostToDevice,
+                                    s->stream));
+        } else {
+          for (int j = 0; j < nin; ++j)
+            OZEC_HIP(hipMemcpyAsync(d + j * dcp + off, in[j] + off, cl, hipMemcpyHostToDevice, s->stream));
+        }
+        OZEC_HIP(launch(d + off, static_cast<int64_t>(dcp), d + nin * dcp + off, static_cast<int64_t>(dop), off, cl,
+                        s->stream));
+        OZEC_HIP(hipEventRecord(s->events[c], s->stream));
+        OZEC_HIP(hipStreamWaitEvent(s->stream2, s->events[c], 0));
+        if (rect) {
+          OZEC_HIP(hipMemcpy2DAsync(const_cast<uint8_t *>(obase[0]) + off, static_cast<size_t>(sout), d + nin * dcp + off,
+                                    dop, cl, nout, hipMemcpyDeviceToHost, s->stream2));
+        } else {
+          for (int r = 0; r < nout; ++r)
+            OZEC_HIP(hipMemcpyAsync(const_cast<uint8_t *>(obase[r]) + off, d + nin * dcp + r * dop + off, cl,
+                                    hipMemcpyDeviceToHost, s->stream2));
+        }
+      }
+      OZEC_HIP(hipStreamSynchronize(s->stream2));
+      return OZEC_OK;
+    }
     if (rect) {
       OZEC_HIP(hipMemcpy2DAsync(d, dcp, in[0], static_cast<size_t>(sin), len, nin, hipMemcpyHostToDevice, s->stream));
     } else {
@@ -1938,6 +1987,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "host_graph") {
     if (value < 0) return bad();
     t.host_graph.store(value);
+  } else if (k == "host_duplex") {
+    if (value < 0) return bad();
+    t.host_duplex.store(value);
   } else {
     return fail(OZEC_EINVAL, "unknown tuning key " + k);
   }

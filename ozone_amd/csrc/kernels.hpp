@@ -157,6 +157,9 @@ struct TuneKnobs {
   std::atomic<int64_t> host_graph{256 << 10};  // host-buffer coding calls of one staged chunk up to this many bytes
                                                // per unit replay a cached hipGraph of H2D + kernel + D2H (0: off;
                                                // 64 KiB-cell rs-6-3 stripe from pageable cells 74 -> 64 us)
+  std::atomic<int64_t> host_duplex{512 << 10};  // pinned host-buffer coding calls of at least this many bytes per unit
+                                                // go up, through the kernel and back in column chunks, the D2H of
+                                                // chunk c on a second stream beside the H2D of chunk c+1 (0: off)
 };
 
 // Kernel alternates the library holds besides the defaults, selectable with ozec_set_tuning for A/B (0 = default).

@@ -43,6 +43,15 @@ for s in $STEPS; do
         --workload c2 --no-cpu --no-pmc --no-e2e --no-legs --no-jni > "$OUT/prof_c2.log" 2>&1 || exit 10
       run "prof legs" 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_legs" -o run --output-format csv -- python3 \
         bench.py --workload legs --no-cpu --no-pmc > "$OUT/prof_legs.log" 2>&1 || exit 11 ;;
+    duplex)  # A/B of the duplex column chunks of pinned per-call coding (host_duplex), same process order each way
+      i=0
+      for t in 0 524288 0 524288; do
+        i=$((i + 1))
+        run "jni duplex=$t" 300 python -u bench.py --workload jni --tune host_duplex=$t > "$OUT/jni_duplex_${t}_$i.json" \
+          2>> "$OUT/duplex.err" || exit 12
+        run "host pinned duplex=$t" 300 python -u bench.py --workload host --host-pinned --threads 1 --steps 5 \
+          --warmup 2 --tune host_duplex=$t > "$OUT/host_pinned_duplex_${t}_$i.json" 2>> "$OUT/duplex.err" || exit 13
+      done ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     heap)

@@ -19,6 +19,7 @@
 #include <time.h>
 
 #include "jni.h"
+#include "../../include/ozec.h"
 
 #define P(name) Java_org_apache_ozone_erasurecode_rawcoder_OzecNative_##name
 jlong P(coderCreate)(JNIEnv *, jclass, jboolean, jint, jint, jint);
@@ -185,7 +186,26 @@ static int run_spec(const char *spec) {
   return ok ? 0 : 3;
 }
 
+/* OZEC_TUNE="key=value,key=value": ozec_set_tuning knobs for A/B runs of the harness (bench.py --tune) */
+static int apply_tuning(void) {
+  const char *e = getenv("OZEC_TUNE");
+  if (!e || !*e) return 0;
+  char buf[512];
+  snprintf(buf, sizeof buf, "%s", e);
+  for (char *kv = strtok(buf, ","); kv; kv = strtok(NULL, ",")) {
+    char *eq = strchr(kv, '=');
+    if (!eq) return 1;
+    *eq = 0;
+    if (ozec_set_tuning(kv, atoll(eq + 1)) != 0) {
+      fprintf(stderr, "unknown tuning knob %s\n", kv);
+      return 1;
+    }
+  }
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (apply_tuning()) return 1;
   if (argc < 3) {
     fprintf(stderr, "usage: %s SECONDS encode|decode:K:P:CELL_BYTES:THREADS...\n", argv[0]);
     return 1;

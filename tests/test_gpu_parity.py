@@ -884,6 +884,43 @@ def test_host_path_pinned_buffers_dma_in_place(codec, k, p, n):
     pool.free()
 
 
+@pytest.mark.parametrize("n", [1 << 20, 700_001, 4 << 20])
+@pytest.mark.parametrize("duplex", [512 << 10, 0])
+def test_host_path_pinned_duplex_column_chunks(n, duplex):
+    """host_duplex (capi.cpp staged_pipeline, direct path): pinned coding calls of large cells go up, through the kernel
+    and back in column chunks, the D2H of chunk c on a second stream beside the H2D of chunk c+1.  Cells at one stride
+    in one pinned pool (one rectangular copy per chunk) and at scattered offsets (one copy per unit), lengths that are
+    and are not a multiple of the chunk, encode and decode vs the oracle, with the chunking on and off."""
+    from ozone_amd.stripe_queue import host_alloc
+    lib = L.lib()
+    k, p = 6, 3
+    assert lib.ozec_set_tuning(b"host_duplex", duplex) == 0
+    try:
+        data = cells(SEED, 96500 + n % 89, k, n)
+        ref = oracle.rs_encode(k, p, data)
+        for scattered in (False, True):
+            gap = 4096 + 16 if scattered else 0
+            pool = host_alloc((k + p + 2) * (n + gap) + 64 * 11)
+            views = [pool.array[i * (n + gap) + (3 * i if scattered else 0):][:n] for i in range(k + p + 2)]
+            for a, b in zip(views, data):
+                a[:] = b
+            for v in views[k:]:
+                v[:] = 0xA5
+            enc("rs", k, p).encode(views[:k], views[k:k + p])
+            assert all((a == b).all() for a, b in zip(views[k:k + p], ref)), (n, duplex, scattered)
+            erased = [1, 7]
+            units = views[:k + p]
+            dins = [None if u in erased else units[u] for u in range(k + p)]
+            outs = views[k + p:k + p + 2]
+            dec("rs", k, p).decode(dins, erased, outs)
+            truth = list(data) + ref
+            assert all((o == truth[u]).all() for o, u in zip(outs, erased)), (n, duplex, scattered)
+            del views, units, dins, outs
+            pool.free()
+    finally:
+        lib.ozec_set_tuning(b"host_duplex", 512 << 10)
+
+
 # Caller memory registered with ozec_host_register stays mapped until the process exits, as include/ozec.h asks of
 # callers: freed after ozec_host_unregister, it was followed by hipErrorIllegalAddress in HIP's next large pageable copy
 # (torch's .cpu()) -- round 4 three times, and again in round 5 the one time this list was removed (DESIGN §4).

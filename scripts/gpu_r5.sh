@@ -52,6 +52,13 @@ for s in $STEPS; do
         run "host pinned duplex=$t" 300 python -u bench.py --workload host --host-pinned --threads 1 --steps 5 \
           --warmup 2 --tune host_duplex=$t > "$OUT/host_pinned_duplex_${t}_$i.json" 2>> "$OUT/duplex.err" || exit 13
       done ;;
+    g6)  # same-process A/B of the 6-bit CRC groups (G6 variants 210-213) against the shipped 5-bit ones
+      run "ab c3r" 300 python -u scripts/ab.py c3r crc_variant ${C3R:-0,177,210} ${ROUNDS:-6} > "$OUT/ab_c3r.log" 2>&1 \
+        || { tail -20 "$OUT/ab_c3r.log"; exit 14; }
+      run "ab c5dev" 300 python -u scripts/ab.py c5dev crc_variant ${C5:-0,171,211,212} ${ROUNDS:-6} \
+        > "$OUT/ab_c5dev.log" 2>&1 || { tail -20 "$OUT/ab_c5dev.log"; exit 15; }
+      run "ab c3" 300 python -u scripts/ab.py c3 crc_variant ${C3:-0,177,210} ${ROUNDS:-6} > "$OUT/ab_c3.log" 2>&1 \
+        || { tail -20 "$OUT/ab_c3.log"; exit 16; } ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     heap)

@@ -59,6 +59,9 @@ for s in $STEPS; do
         > "$OUT/ab_c5dev.log" 2>&1 || { tail -20 "$OUT/ab_c5dev.log"; exit 15; }
       run "ab c3" 300 python -u scripts/ab.py c3 crc_variant ${C3:-0,177,210} ${ROUNDS:-6} > "$OUT/ab_c3.log" 2>&1 \
         || { tail -20 "$OUT/ab_c3.log"; exit 16; } ;;
+    ua)  # 16-B buffer loads / stores at unaligned byte offsets: bytes, bandwidth, the range edge (odd-length cells)
+      [ -x scripts/unaligned_probe ] || { echo "scripts/unaligned_probe not built" >&2; exit 17; }
+      run "unaligned probe" 120 scripts/unaligned_probe > "$OUT/unaligned_probe.json" 2> "$OUT/unaligned_probe.err" || exit 17 ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     heap)

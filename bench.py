@@ -1211,8 +1211,9 @@ def tail_rows(args, lens=(1007, 1008, 50000, 50001, 700000, 700001), seconds=0.4
     cells of any length.  (a) one stripe per call through the JNI path (encodeArrays, 1 and 16
     threads); (b) the fused encode + CRC32C of one stripe per call from pinned host memory
     (ozec_encode_crc_host_batch); (c) device-resident fused encode + CRC32C batches of such cells (unit stride
-    padded to 4 KiB), kernel time per launch -- a length that is not a multiple of 16 B takes the unfused path (encode,
-    then one CRC pass per unit)."""
+    padded to 4 KiB, and packed), kernel time per launch -- since round 5 every length runs on the nibble kernel (the
+    last 1-15 bytes of a unit in nb_tail; until then a length that was not a multiple of 16 B took the unfused path:
+    encode, then one CRC pass per unit, profiles/r05/tail/bench_tail_after.json)."""
     from ozone_amd import checksum as ck
     from ozone_amd import rawcoder as rc
     from ozone_amd.stripe_queue import host_alloc
@@ -1243,35 +1244,38 @@ def tail_rows(args, lens=(1007, 1008, 50000, 50001, 700000, 700001), seconds=0.4
         host.append({"cell_bytes": n, "us_per_stripe": round(us, 1), "GBps": round(k * n / us / 1e3, 3),
                      "cpu_1thread_encode_only_us": round(cpu[n], 1)})
         pb.free()
-        # device-resident batch of such stripes: about 2 GiB of data cells
+        # device-resident batches of such stripes, about 2 GiB of data cells: unit stride padded to 4 KiB, and packed
+        # (unit stride = n: units at odd byte offsets when n is odd)
         S = max(64, min(65536, (2 << 30) // (k * n)))
-        us_ = -(-n // 4096) * 4096
-        units = torch.zeros((S, k + p, us_), dtype=torch.uint8, device=dev)
-        for u in range(k):
-            rc.fill_splitmix64_cells(units[:, u], (k + p) * us_, S, n, SEED, u * S)
-        crcs = torch.empty((S, k + p, nwin), dtype=torch.int32, device=dev)
+        for layout in ("pitch 4 KiB", "packed"):
+            us_ = -(-n // 4096) * 4096 if layout == "pitch 4 KiB" else n
+            units = torch.zeros((S, k + p, us_), dtype=torch.uint8, device=dev)
+            for u in range(k):
+                rc.fill_splitmix64_cells(units[:, u], (k + p) * us_, S, n, SEED, u * S)
+            crcs = torch.empty((S, k + p, nwin), dtype=torch.int32, device=dev)
 
-        def launch():
-            enc.encode_crc_batch(units, (k + p) * us_, us_, units[:, k:], (k + p) * us_, us_, S, n,
-                                 ck.ChecksumType.CRC32C, bpc, crcs)
-        for _ in range(3):
-            launch()
-        st = torch.cuda.current_stream()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 10
-        e0.record(st)
-        for _ in range(reps):
-            launch()
-        e1.record(st)
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        alg = S * (k + p) * n + S * (k + p) * nwin * 4
-        dev_rows.append({"cell_bytes": n, "stripes": S, "ms_per_launch": round(ms, 4),
-                         "GBps_data": round(S * k * n / ms / 1e6, 1),
-                         "frac_hbm": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                         "path": "fused (nibble kernel)" if n % 16 == 0 else "unfused (encode + 9 CRC passes)"})
-        del units, crcs
-        torch.cuda.empty_cache()
+            def launch():
+                enc.encode_crc_batch(units, (k + p) * us_, us_, units[:, k:], (k + p) * us_, us_, S, n,
+                                     ck.ChecksumType.CRC32C, bpc, crcs)
+            for _ in range(3):
+                launch()
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 10
+            e0.record(st)
+            for _ in range(reps):
+                launch()
+            e1.record(st)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            alg = S * (k + p) * n + S * (k + p) * nwin * 4
+            dev_rows.append({"cell_bytes": n, "layout": layout, "unit_stride": us_, "stripes": S,
+                             "ms_per_launch": round(ms, 4), "GBps_data": round(S * k * n / ms / 1e6, 1),
+                             "frac_hbm": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                             "path": "fused (nibble kernel" + (f", last {n % 16} B per unit in nb_tail)" if n % 16
+                                                              else ")")})
+            del units, crcs
+            torch.cuda.empty_cache()
     out["fused_host_one_stripe_per_call"] = host
     out["fused_device_batch"] = dev_rows
     out["cpu"] = f"oracle/cpu_baseline.c percall_encode (1 thread, encode only), {flags}"

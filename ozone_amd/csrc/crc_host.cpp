@@ -7,7 +7,6 @@
 namespace ozec {
 
 int g26_bit(int g, int i);
-int g22_bit(int g, int i);
 
 namespace {
 
@@ -102,39 +101,6 @@ CrcMath::CrcMath(uint32_t poly) : poly_(poly) {
   mat_invert(adv, back);
   for (int g = 0; g < 7; ++g)
     for (uint32_t v = 0; v < 32; ++v) xo_[kXoInv + g * 32 + v] = apply(back, static_cast<uint32_t>(uint64_t{v} << (5 * g)));
-  // G6 blob: the same XO set and shifts on 6-bit groups (kernels.hpp kX6*)
-  g6_.assign(kX6Words, 0);
-  for (int g = 0; g < 22; ++g)
-    for (uint32_t v = 0; v < 64; ++v) {
-      uint32_t acc = 0;
-      for (int i = 0; i < 6; ++i) {
-        const int p = g22_bit(g, i);
-        if (p >= 0 && ((v >> i) & 1)) acc ^= bit[p];
-      }
-      g6_[g * 64 + v] = shift(acc, kXoAdvance);
-    }
-  auto fill6 = [&](int off, auto op) {  // 6 tables of a 32-bit register's 6-bit groups (g = 5: bits 30..31)
-    for (int g = 0; g < 6; ++g)
-      for (uint32_t v = 0; v < 64; ++v) g6_[off + g * 64 + v] = op(static_cast<uint32_t>(uint64_t{v} << (6 * g)));
-  };
-  fill6(kX6Inv, [&](uint32_t r) { return apply(back, r); });
-  fill6(kX6Sh1, [&](uint32_t r) { return shift(r, 1024); });
-  fill6(kX6Sh2, [&](uint32_t r) { return shift(r, 2048); });
-  for (int m = 0; m < 6; ++m) fill6(kX6Tree + m * kX6Shift, [&](uint32_t r) { return shift(r, uint64_t{16} << m); });
-}
-
-// Block bit that index bit i of G22 table g reads (-1 past the table's width).  Mirrors device.hpp g22_block:
-//   g = 4d+b (16 tables): w_d bits 8b+2..8b+7                                ((w_d >> 8b) & 0xfc)
-//   g = 16+b  (4 tables): y = (w0 & M) | (w1 & M) << 2 | (w2 & M) << 4, M = 0x03030303: byte b of y = bits 8b, 8b+1
-//                         of w0, w1, w2 (index bits 0-1, 2-3, 4-5)
-//   g = 20              : bits 0-1 of bytes 0, 1, 2 of w3
-//   g = 21    (2 bits)  : bits 24-25 of w3
-int g22_bit(int g, int i) {
-  if (i >= 6) return -1;
-  if (g < 16) return 32 * (g >> 2) + 8 * (g & 3) + 2 + i;
-  if (g < 20) return 32 * (i >> 1) + 8 * (g - 16) + (i & 1);
-  if (g == 20) return 96 + 8 * (i >> 1) + (i & 1);
-  return i < 2 ? 96 + 24 + i : -1;
 }
 
 // Block bit (0..127; dword d bit k = 32d + k, i.e. byte p/8 bit p%8) that index bit i of G26 table g reads,

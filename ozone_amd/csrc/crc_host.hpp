@@ -27,8 +27,6 @@ class CrcMath {
   const std::vector<uint32_t> &nib_tables() const { return nib_; }
   // the device XO blob (kernels.hpp kXo*)
   const std::vector<uint32_t> &xo_tables() const { return xo_; }
-  // the device G6 blob (kernels.hpp kX6*)
-  const std::vector<uint32_t> &g6_tables() const { return g6_; }
   uint32_t byte_table(int v) const { return t0_[v]; }
   uint32_t poly() const { return poly_; }
   // x^(8n) mod P in CrcUtil's reversed representation (CrcUtil.getMonomial)
@@ -54,7 +52,6 @@ class CrcMath {
   std::vector<uint32_t> g26_[kG26Slots];
   std::vector<uint32_t> nib_;
   std::vector<uint32_t> xo_;
-  std::vector<uint32_t> g6_;
   std::vector<uint32_t> build_blob(int B) const;
   std::vector<uint32_t> build_g26(int B, int D) const;
 };

@@ -461,97 +461,6 @@ __device__ __forceinline__ uint32_t g26_block(const uint32_t *T, const uint4 b, 
   return r ^ t[25];
 }
 
-// ---- G6: 6-bit groups (round 5; table layout kernels.hpp kX6*, host crc_host.cpp g22_bit) --------------------------
-// A 64-entry dword table covers the 64 LDS banks once, so a 6-bit index reads conflict-free under ds_read_b32 like a
-// 5-bit one.  `(w >> 8b) & 0xfc` is bits 8b+2..8b+7 of a dword times 4 -- one SDWA op per lookup for 16 of a block's
-// 22 groups (G26 reads 5 of those bits); the 32 bits left over (bits 8b, 8b+1 of every byte) make 6 more groups.
-// Block: 22 lookups and ~34 VALU (G26: 26 and 36); register shift: 6 lookups (G5: 7).
-
-// byte-offset index of 6-bit group g of a 32-bit register: bits 6g..6g+5 times 4
-template <int G>
-__device__ __forceinline__ uint32_t g6_idx4(uint32_t s) {
-  if constexpr (G == 0) return (s << 2) & 0xfcu;
-  else return (s >> (6 * G - 2)) & 0xfcu;
-}
-
-// register shift by the byte distance the 6 x 64 table block at T encodes
-__device__ __forceinline__ uint32_t g6_shift(const uint32_t *T, uint32_t s) {
-  const uint32_t t0 = lds_at(T, 0 * 256 + g6_idx4<0>(s)), t1 = lds_at(T, 1 * 256 + g6_idx4<1>(s));
-  const uint32_t t2 = lds_at(T, 2 * 256 + g6_idx4<2>(s)), t3 = lds_at(T, 3 * 256 + g6_idx4<3>(s));
-  const uint32_t t4 = lds_at(T, 4 * 256 + g6_idx4<4>(s)), t5 = lds_at(T, 5 * 256 + g6_idx4<5>(s));
-  return xor3(t0, t1, t2) ^ xor3(t3, t4, t5);
-}
-
-// XOR of the 22 lookups of block b in the G6 block set at T (22 x 64 words).  vm: 0xfc in a VGPR (byte_and_v).
-__device__ __forceinline__ uint32_t g22_block(const uint32_t *T, const uint4 b, uint32_t vm) {
-  const uint32_t w[4] = {b.x, b.y, b.z, b.w};
-  uint32_t t[12];
-  auto four = [&](uint32_t v, int g, int at0) {
-    t[at0] = lds_at(T, g * 256 + byte_and_v<0>(v, vm));
-    t[at0 + 1] = lds_at(T, (g + 1) * 256 + byte_and_v<1>(v, vm));
-    t[at0 + 2] = lds_at(T, (g + 2) * 256 + byte_and_v<2>(v, vm));
-    t[at0 + 3] = lds_at(T, (g + 3) * 256 + byte_and_v<3>(v, vm));
-  };
-  constexpr uint32_t M = 0x03030303u;
-  // y4: byte b holds (bits 8b, 8b+1 of w0, w1, w2) << 2 -- the index of group 16 + b times 4
-  const uint32_t y4 = ((w[0] & M) << 2) | ((w[1] & M) << 4) | ((w[2] & M) << 6);
-  const uint32_t z = w[3] & M;
-  // two halves of 12 and 10 lookups with a scheduling fence between them (at most 12 results live, as g26_block's
-  // HALVES form keeps at most 14)
-  four(w[0], 0, 0);
-  four(w[1], 4, 4);
-  four(y4, 16, 8);
-  uint32_t r = xor3(t[0], t[1], t[2]);
-#pragma unroll
-  for (int g = 3; g + 1 < 12; g += 2) r = xor3(r, t[g], t[g + 1]);
-  r ^= t[11];
-  __builtin_amdgcn_sched_barrier(0);
-  four(w[2], 8, 0);
-  four(w[3], 12, 4);
-  t[8] = lds_at(T, 20 * 256 + (((z | (z >> 6) | (z >> 12)) << 2) & 0xfcu));
-  t[9] = lds_at(T, 21 * 256 + ((z >> 22) & 0x0cu));
-  r = xor3(r, t[0], t[1]);
-#pragma unroll
-  for (int g = 2; g + 1 < 10; g += 2) r = xor3(r, t[g], t[g + 1]);
-  return r;
-}
-
-// g5_lane_tree_rs on 6-bit groups: the shifts of level m are the 6 x 64 tables at T + m * kX6Shift
-template <int U>
-__device__ __forceinline__ uint32_t g6_lane_tree_rs(const uint32_t *T, const uint32_t (&S)[U], int lane, int &unit) {
-  static_assert(U <= 32, "at most 32 registers");
-  constexpr int NP = tree_np(U);
-  constexpr int L = NP == 1 ? 0 : NP == 2 ? 1 : NP == 4 ? 2 : NP == 8 ? 3 : NP == 16 ? 4 : 5;
-  uint32_t r[NP];
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < NP; ++i) r[i] = i < U ? S[i] : 0u;
-  unit = 0;
-#pragma unroll
-  for (int m = 0; m < L; ++m) {
-    const int h = (NP >> m) >> 1;
-    const bool upper = (lane >> m) & 1;
-    const uint32_t um = upper ? 0xffffffffu : 0u;
-    unit += upper ? h : 0;
-#pragma unroll
-    for (int i = 0; i < h; ++i) {
-      __builtin_amdgcn_sched_barrier(0);
-      const uint32_t send = bsel(r[i], r[h + i], um);
-      const uint32_t keep = bsel(r[h + i], r[i], um);
-      const uint32_t recv = static_cast<uint32_t>(__shfl_xor(static_cast<int>(send), 1 << m, 64));
-      r[i] = g6_shift(T + m * kX6Shift, bsel(recv, keep, um)) ^ bsel(keep, recv, um);
-    }
-  }
-  uint32_t v = r[0];
-#pragma unroll
-  for (int m = L; m < 6; ++m) {
-    const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), 1 << m, 64));
-    const bool upper = (lane >> m) & 1;
-    v = g6_shift(T + m * kX6Shift, upper ? other : v) ^ (upper ? v : other);
-  }
-  return v;
-}
-
 // ------------------------------------------------------------------------------------------------
 // launch helpers
 

@@ -256,6 +256,13 @@ bool encode_crc_nb_supported(const EncCrcArgs &e) {
   return fused_shape(e.code, true) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len > 0 && e.code.len % 16 == 0;
 }
 
+// cells of any length at any byte offsets (round 5): the nibble kernel's EM variants run the whole 16-B blocks of the
+// last window as above and the last 1-15 bytes in nb_tail; gfx950 buffer accesses take unaligned offsets (probe:
+// profiles/r05/unaligned/, unaligned 16-B loads at full rate)
+bool encode_crc_nb_bytes_supported(const CodeArgs &a, int64_t bpc) {
+  return fused_shape(a, true) && bpc > 0 && bpc % 4096 == 0 && a.len > 0;
+}
+
 namespace {
 
 hipError_t launch_nb_shape(const EncCrcArgs &e, hipStream_t st, int v) {

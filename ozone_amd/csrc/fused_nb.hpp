@@ -102,6 +102,46 @@ __device__ __forceinline__ void nb_emit_lane(const EncCrcArgs &e, int64_t s, int
   }
 }
 
+// A cell whose length is not a multiple of 16 B (round 5; every key's last stripe has one, ECKeyOutputStream.java:276):
+// the window loop runs over the last window's whole 16-B blocks only, then the lane holding unit q's raw register
+// after the lane tree extends it bytewise over the unit's last tb (1..15) bytes at window offset o0, and the lanes of
+// the output units compute those bytes' GF products from the K inputs (s_gf: the R products of each input nibble,
+// byte r = output r) and store them.  Once per cell, a few hundred VALU on at most K + R lanes.  Unit offsets of such
+// cells are not 16-B (often not 4-B) aligned: gfx950 buffer accesses take any byte offset (the amdhsa ABI runs
+// shaders in unaligned access mode; hipcc emits 16-B loads for align-1 data itself).
+template <int K, int R>
+__device__ __forceinline__ uint32_t nb_tail(const EncCrcArgs &e, __amdgpu_buffer_rsrc_t rin,
+                                            __amdgpu_buffer_rsrc_t rout, const uint32_t *s_gf, int q, uint32_t v,
+                                            uint32_t o0, int32_t tb) {
+  const CodeArgs &a = e.code;
+  const uint32_t poly = e.crc.poly;
+  uint32_t uoff = static_cast<uint32_t>(a.in_off[0]);  // the lane's unit offset (select chain: kernarg arrays stay SGPR)
+#pragma unroll
+  for (int j = 1; j < K; ++j) uoff = q == j ? static_cast<uint32_t>(a.in_off[j]) : uoff;
+#pragma unroll
+  for (int r = 0; r < R; ++r) uoff = q == K + r ? static_cast<uint32_t>(a.out_off[r]) : uoff;
+  for (int32_t b = 0; b < tb; ++b) {
+    const uint32_t ob = o0 + static_cast<uint32_t>(b);
+    uint32_t byte;
+    if (q < K) {
+      byte = __builtin_amdgcn_raw_buffer_load_b8(rin, ob + uoff, 0, 0);
+    } else {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint32_t x = __builtin_amdgcn_raw_buffer_load_b8(rin, ob, static_cast<int>(a.in_off[j]), 0);
+        acc ^= s_gf[j * 32 + (x & 15)] ^ s_gf[j * 32 + 16 + (x >> 4)];
+      }
+      byte = (acc >> (8 * (q - K))) & 0xffu;
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rout, ob + uoff, 0, 0);
+    }
+    v ^= byte;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = (v >> 1) ^ (poly & (0u - (v & 1u)));
+  }
+  return v;
+}
+
 // K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
 // FENCE: dwords of a block whose lookups go between scheduling fences (2: halves, at most 16 results live; 1:
 // quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree;
@@ -115,12 +155,10 @@ __device__ __forceinline__ void nb_emit_lane(const EncCrcArgs &e, int64_t s, int
 // H (< K, XO with D = 2 only): only inputs 0..H-1 get the second distance set (K + H instead of 2K tables of 4 KiB, so
 // rs-10-x two-step groups fit two workgroups per CU); inputs H..K-1 are looked up in set 0 and shifted by one step
 // after every step (table at kSh1), inputs 0..H-1 by two at the group end
-// G6 (round 5; XO, RS, D <= 2): the output blocks, the register shifts and the lane tree on 6-bit groups (kernels.hpp
-// kX6*, device.hpp g22_block / g6_shift): 22 instead of 26 lookups per output block, 6 instead of 7 per shift
 // (Round-3 probes -- output-register groups, VALU / LDS pads, far-addressing without the index OR, late lane-tree
 // tables, guided and static persistent orders -- are measured in DESIGN 2.3 and were taken out of the library.)
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
-          bool EM = false, int H = K, bool G6 = false>
+          bool EM = false, int H = K>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -128,7 +166,6 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   static_assert((D * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
   static_assert(DYN == 0 || DYN == 1, "one wave per unit, or the persistent WorkQueue grid");
   static_assert(H == K || (XO && D == 2 && H >= 0 && H < K), "partial second distance set: XO, two-step groups");
-  static_assert(!G6 || (XO && RS && D <= 2), "6-bit groups: XO output registers, reduce-scatter tree, D <= 2");
   constexpr int kSets = K + (D - 1) * H;  // (d, j) nibble tables of 4 KiB: all K inputs in set 0, inputs < H in sets >= 1
   // one LDS block: G26 blob of D sets, then the (d, j, p) nibble tables, then the GF dwords of the setup.  Table
   // regions past the 16-bit ds_read offset range are reached with bit 15 set in the index register (one v_or_b32).
@@ -137,18 +174,15 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   constexpr uint32_t kShIn = XO ? 0 : g26_gshift(D);  // word offset of the input-register shift
   constexpr uint32_t kTree = XO ? 224 : g26_tree(D);  // and of the lane-tree shifts
   constexpr uint32_t kSh1 = kXoOff + kXoWords;  // H < K: one-step register shift (inputs H..K-1)
-  constexpr uint32_t kTW = G6 ? kX6Hot : XO ? kXoOff + kXoWords + (H < K ? 224 : 0) : g26_words(D);
+  constexpr uint32_t kTW = XO ? kXoOff + kXoWords + (H < K ? 224 : 0) : g26_words(D);
   constexpr uint32_t kTB = (kTW * 4 + 255) / 256 * 256;  // nibble tables
-  // G6: the cold tables (inverse advance, lane tree: once per window) after the nibble tables, so the hot ones keep
-  // the nibble tables low in LDS (fewer regions past the 16-bit ds_read offset range)
-  constexpr uint32_t kLds = kTB + kSets * 4096 + K * 32 * 4 + (G6 ? kX6Cold * 4 : 0);
+  constexpr uint32_t kLds = kTB + kSets * 4096 + K * 32 * 4;
   static_assert(kLds <= 160 * 1024, "LDS per workgroup");
   __shared__ __attribute__((aligned(256))) uint8_t s_all[kLds];
   uint32_t *const s_t = reinterpret_cast<uint32_t *>(s_all);
   uint2 *const s_c = reinterpret_cast<uint2 *>(s_all + kTB);
   uint32_t *const s_gf = reinterpret_cast<uint32_t *>(s_all + kTB + kSets * 4096);
   uint32_t *const s_tree = s_t + kTree;  // lane-tree shifts
-  uint32_t *const s_cold = reinterpret_cast<uint32_t *>(s_all + kTB + kSets * 4096 + K * 32 * 4) - kX6Hot;  // G6
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
   for (int t = threadIdx.x; t < K * 32; t += blockDim.x) {
@@ -158,10 +192,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     for (int r = 0; r < R; ++r) dw |= gf_mul_byte(a.coef[r * K + j], static_cast<uint32_t>(n) << (4 * h)) << (8 * r);
     s_gf[t] = dw;
   }
-  if constexpr (G6) {
-    load_tables(s_t, cr.g6, kX6Hot);
-    load_tables(s_cold + kX6Hot, cr.g6 + kX6Hot, kX6Cold);
-  } else if constexpr (XO) {
+  if constexpr (XO) {
     load_tables(s_t, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224 + 1344);
     load_tables(s_t + kXoOff, cr.xo, kXoWords);
     if constexpr (H < K) load_tables(s_t + kSh1, cr.g26[g26_slot(1, 1)] + g26_gshift(1), 224);
@@ -182,11 +213,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   const int64_t units = a.nstripes * nwin;
   const int32_t T = static_cast<int32_t>(cr.bpc >> 10);  // steps per window
   const uint32_t voff = static_cast<uint32_t>(lane) * 16u;
-  uint32_t v4, vf0, vfc;  // index-op operands in VGPRs (VOP2/SDWA with no SGPR or literal operand issue fastest)
+  uint32_t v4, vf0;  // index-op operands in VGPRs (VOP2/SDWA with no SGPR or literal operand issue fastest)
   asm volatile("v_mov_b32 %0, 4" : "=v"(v4));
   asm volatile("v_mov_b32 %0, 0xf0" : "=v"(vf0));
-  if constexpr (G6) asm volatile("v_mov_b32 %0, 0xfc" : "=v"(vfc));
-  else vfc = 0;
   int64_t off_max = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) off_max = a.in_off[j] > off_max ? a.in_off[j] : off_max;
@@ -209,8 +238,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     const int64_t w = uniform64(u - s * nwin);
     const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
     const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(a.out + out_off(a, s) + w * cr.bpc, out_extent);
-    // steps of this window: a cell's last window may be short (any whole number of 16-B blocks, nb_supported in
-    // fused.hip).  It is run as whole D-step groups with Pb virtual zero blocks in front, as the per-window kernel
+    // steps of this window: a cell's last window may be short (its whole 16-B blocks here, its last 1-15 bytes in
+    // nb_tail).  It is run as whole D-step groups with Pb virtual zero blocks in front, as the per-window kernel
     // does: a zero block leaves a zero CRC register at zero and has zero GF products, and the blocks after it keep
     // their distance to the window end.  Virtual blocks and the look-ahead past the window are addressed outside
     // both descriptors: their loads return zeros without a memory access and their stores are dropped.
@@ -296,11 +325,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
           __attribute__((ext_vector_type(4))) unsigned int dv = {p.x, p.y, p.z, p.w};
           __builtin_amdgcn_raw_buffer_store_b128(dv, rout, vcur, static_cast<int>(a.out_off[r]), 2);
           store_data_hold(p);
-          if constexpr (G6) {
-            uint4 px = p;
-            px.x ^= S[K + r];
-            S[K + r] = g22_block(s_t, px, vfc);
-          } else if constexpr (XO) {
+          if constexpr (XO) {
             uint4 px = p;
             px.x ^= S[K + r];
             S[K + r] = g26_block<true>(s_t + kXoOff, px);
@@ -312,31 +337,32 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         if constexpr (H < K) {
           if (rr + 1 < D) {
 #pragma unroll
-            for (int q = H; q < K; ++q) S[q] = G6 ? g6_shift(s_t + kX6Sh1, S[q]) : g5_shift(s_t + kSh1, S[q]);
+            for (int q = H; q < K; ++q) S[q] = g5_shift(s_t + kSh1, S[q]);
           }
         }
       }
       if (g + 1 < Gu) {
 #pragma unroll
-        for (int q = 0; q < (XO ? K : K + R); ++q) {
-          if constexpr (G6) S[q] = g6_shift(s_t + (q < H && D == 2 ? kX6Sh2 : kX6Sh1), S[q]);
-          else S[q] = g5_shift(s_t + (q < H ? kShIn : q < K ? kSh1 : g26_gshift(D)), S[q]);
-        }
+        for (int q = 0; q < (XO ? K : K + R); ++q)
+          S[q] = g5_shift(s_t + (q < H ? kShIn : q < K ? kSh1 : g26_gshift(D)), S[q]);
       }
     }
     const bool last = w == nwin - 1;
     const uint32_t init = last ? cr.init_last : cr.init_full;
     if constexpr (XO) {  // undo the advance of every output block
 #pragma unroll
-      for (int r = 0; r < R; ++r)
-        S[K + r] = G6 ? g6_shift(s_cold + kX6Inv, S[K + r]) : g5_shift(s_t + kXoOff + kXoInv, S[K + r]);
+      for (int r = 0; r < R; ++r) S[K + r] = g5_shift(s_t + kXoOff + kXoInv, S[K + r]);
     }
     if constexpr (RS) {
       int q = 0;
-      const uint32_t v = G6 ? g6_lane_tree_rs<K + R>(s_cold + kX6Tree, S, lane, q)
-                            : g5_lane_tree_rs<K + R>(s_tree - kG5Tree, S, lane, q);
+      const uint32_t v = g5_lane_tree_rs<K + R>(s_tree - kG5Tree, S, lane, q);
       if constexpr (EM) {
-        if (lane < tree_np(K + R) && q < K + R) nb_emit_lane<K, R>(e, s, w, q, v, init);
+        // the cell's last 1-15 bytes (nb_tail; launch_encode_crc sends such cells to EM variants only)
+        const int32_t tb = last ? static_cast<int32_t>((a.len - w * cr.bpc) & 15) : 0;
+        uint32_t vt = v;
+        if (tb != 0 && lane < tree_np(K + R) && q < K + R)
+          vt = nb_tail<K, R>(e, rin, rout, s_gf, q, v, static_cast<uint32_t>((a.len - w * cr.bpc) & ~int64_t{15}), tb);
+        if (lane < tree_np(K + R) && q < K + R) nb_emit_lane<K, R>(e, s, w, q, vt, init);
       } else if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
 #pragma unroll
         for (int qq = 0; qq < K + R; ++qq)
@@ -355,16 +381,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
-          bool EM = false, int H = K, bool G6 = false>
+          bool EM = false, int H = K>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
     constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
     static_assert(kNB != NB && (D * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, G6>(e, st);
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, G6>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
@@ -397,7 +423,7 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
 // whether variant v of the nibble kernel runs on the persistent WorkQueue grid (needs a leased counter slot)
 constexpr bool nb_variant_persistent(int v) { return v == 150 || v == 163 || v == 167 || v == 170 || v == 171 ||
                                                      v == 172 || v == 176 || v == 177 || v == 187 || (v >= 189 && v <= 194) ||
-                                                     v == 196 || (v >= 210 && v <= 213); }
+                                                     v == 196; }
 
 // variant (g_tune.crc_variant, kernels.hpp kCrcVariants): the measured alternates of the nibble-table kernel
 template <int K, int R>
@@ -444,12 +470,6 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 193: return launch_nb<K, R, 2, kNB, 14, 7, 2, true, 1, true, true>(e, st);
     case 194: return launch_nb<K, R, 2, kNB, 9, 7, 2, true, 1, true, true, kHh>(e, st);
     case 196: return launch_nb<K, R, 2, 2, 16, 4, 1, true, 1, true, true, kHh>(e, st);
-    // round 5, 6-bit groups (G6) for the output blocks, register shifts and lane tree: 210 = 177, 211 = 171, 212 = 172,
-    // 213 = 170 with G6 (22 instead of 26 lookups per output block, 6 instead of 7 per shift)
-    case 210: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true, true, kHh, true>(e, st);
-    case 211: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true, true, K, true>(e, st);
-    case 212: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, true, true, K, true>(e, st);
-    case 213: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true, K, true>(e, st);
     default: break;
   }
   return hipErrorInvalidValue;

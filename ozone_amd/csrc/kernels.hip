@@ -1064,7 +1064,8 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
   OZEC_FUSED_SHAPES(OZEC_SHAPE_OK)
 #undef OZEC_SHAPE_OK
   CodeArgs rb = a;
-  return kr && bpc > 0 && aligned16(bpc) && aligned16(a.len) && vec_ok(a) && rebase32(rb);
+  if (!kr || bpc <= 0 || !aligned16(bpc) || !rebase32(rb)) return false;
+  return (aligned16(a.len) && vec_ok(a)) || encode_crc_nb_bytes_supported(a, bpc);
 }
 
 hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
@@ -1074,6 +1075,12 @@ hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   // the RS shapes with whole windows and a short last window of any whole number of blocks: the nibble-table kernel
   // (fused_nb.hpp); 56 / 59 the streamed-input kernel (full windows only); variant 49 pins the per-window kernel
   const int v = g_tune.crc_variant.load(std::memory_order_relaxed);
+  if (!aligned16(e.code.len) || !vec_ok(e.code)) {
+    // byte-granular cells (a key's last stripe, odd unit strides): the nibble kernel's EM variants only (nb_tail); a
+    // pinned variant without EM falls back to the default one
+    if (!encode_crc_nb_bytes_supported(e.code, e.crc.bpc)) return hipErrorInvalidValue;
+    return launch_encode_crc_lv(e, st, v >= 170 && v < 300 ? v : 0);
+  }
   if (v == 0 || (v >= 50 && v < 300)) {
     const bool lv = v == 56 || v == 59;
     if (lv ? encode_crc_lv_supported(e) : encode_crc_nb_supported(e)) return launch_encode_crc_lv(e, st, v);

@@ -48,11 +48,11 @@ struct CrcArgs {
   const uint32_t *g26[6];     // device G26 table blobs for this CRC type, one per kG26Cfg entry
   const uint32_t *nib;        // device nibble table blob for this CRC type (kNib* layout)
   const uint32_t *xo;         // device XO table blob for this CRC type (kXo* layout)
-  const uint32_t *g6;         // device G6 table blob for this CRC type (kX6* layout)
   uint32_t init_full;      // shift(0xFFFFFFFF, bpc bytes)
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
   int32_t raw;             // emit the raw (init 0, no xorout) register instead of getValue()
+  uint32_t poly;           // reflected polynomial (bytewise register update of a cell's last 1-15 bytes, fused_nb.hpp)
   // verify mode (expected != null): instead of storing, compare with expected[c * out_cell_stride + w]
   // (stored big-endian when expected_be) and atomicMin (mismatch_base + w) into mismatch[c]
   const uint32_t *expected;
@@ -62,7 +62,8 @@ struct CrcArgs {
   int32_t unit_map;        // as CodeArgs::unit_map
 };
 
-// Fused encode + CRC (bpc % 16 == 0, len % 16 == 0, 16-B aligned).
+// Fused encode + CRC (bpc % 16 == 0; len % 16 == 0 and 16-B aligned units, or, on the nibble kernel's shapes with
+// bpc % 4096 == 0, any length and byte offsets: encode_crc_nb_bytes_supported).
 //   encode mode (verify == 0): crc.out = crcs[s][unit][w] for all K inputs and R outputs (out_cell_stride = nwin)
 //   reconstruct mode (verify == 1): the K inputs are checked against crc.expected[s][in_unit[j]][w]
 //     (exp_units units per stripe) with failures atomicMin'ed into crc.mismatch[s] as in_unit*nwin + w, and only
@@ -137,27 +138,6 @@ constexpr int kXoAdvance = 1024 - 16;
 constexpr int kXoInv = kG26Set;
 constexpr int kXoWords = kG26Set + 224;
 
-// Device CRC "G6" blob (round 5): the XO blob's output lookups, the register shifts and the lane tree on 6-bit groups.
-// A 64-entry table of dwords covers the 64 LDS banks once, so a 6-bit index is as conflict-free under ds_read_b32 as a
-// 5-bit one, and a 16-B block takes 22 lookups instead of 26, a 32-bit register 6 instead of 7 (device.hpp g22_block,
-// g6_shift; host crc_host.cpp g22_bit).  Tables of 64 words; the hot part (every step) first, the cold part (once per
-// window) after it, so a kernel can stage them in separate LDS regions:
-//   [0, kX6Set)               22 tables: block -> raw CRC advanced by kXoAdvance bytes (the XO output set)
-//   [kX6Sh1, +384)            register shift by 1024 bytes (one step of a 64-lane wave), 6 tables (bits 6g..6g+5;
-//                             g = 5 holds bits 30..31)
-//   [kX6Sh2, +384)            register shift by 2048 bytes (a two-step group)
-//   [kX6Inv, +384)            register shift by -kXoAdvance bytes (the cold part starts here)
-//   [kX6Tree, +6 * 384)       lane-tree shifts by 16 * 2^m bytes, m = 0..5
-constexpr int kX6Set = 22 * 64;
-constexpr int kX6Shift = 6 * 64;
-constexpr int kX6Sh1 = kX6Set;
-constexpr int kX6Sh2 = kX6Sh1 + kX6Shift;
-constexpr int kX6Hot = kX6Sh2 + kX6Shift;
-constexpr int kX6Inv = kX6Hot;
-constexpr int kX6Tree = kX6Inv + kX6Shift;
-constexpr int kX6Words = kX6Tree + 6 * kX6Shift;
-constexpr int kX6Cold = kX6Words - kX6Hot;
-
 // Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.  Process-wide harness knobs for A/B and profiling
 // runs (bench.py --tune, scripts/ab.py): every field is an atomic, so setting one while other threads launch is not a
 // data race, but a set knob applies to every caller's next launch -- a production process leaves them at 0.
@@ -194,12 +174,10 @@ struct TuneKnobs {
 //       (the round-1 default), 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps
 //     fused RS (launch_encode_crc): 49 per-window kernel, 56 / 59 streamed-input kernel (fused.hip), 62 / 87 / 150 /
-//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 nibble-table kernel, 210-213 the same on 6-bit CRC
-//       groups (fused_nb.hpp launch_nb_kr)
+//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 nibble-table kernel (fused_nb.hpp launch_nb_kr)
 constexpr int kGfVariants[] = {1, 5, 11};
 constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  49,  56,  59,  62,  87,  150, 163, 167, 170,
-                                 171, 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196, 210, 211,
-                                 212, 213};
+                                 171, 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196};
 
 extern TuneKnobs g_tune;
 
@@ -229,6 +207,7 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc);
 bool encode_crc_lv_supported(const EncCrcArgs &e);
 // the nibble-table kernel (fused_nb.hpp): the same shapes, and a short last window of any whole number of 16-B blocks
 bool encode_crc_nb_supported(const EncCrcArgs &e);
+bool encode_crc_nb_bytes_supported(const CodeArgs &a, int64_t bpc);
 hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant);
 
 // WorkQueue counter slots of the persistent kernels (device.hpp WorkQueue; pool in work_slots.cpp).  work_lease gives a

@@ -62,6 +62,13 @@ for s in $STEPS; do
     ua)  # 16-B buffer loads / stores at unaligned byte offsets: bytes, bandwidth, the range edge (odd-length cells)
       [ -x scripts/unaligned_probe ] || { echo "scripts/unaligned_probe not built" >&2; exit 17; }
       run "unaligned probe" 120 scripts/unaligned_probe > "$OUT/unaligned_probe.json" 2> "$OUT/unaligned_probe.err" || exit 17 ;;
+    abprev)  # the device-resident legs on the previous build (ab/libozec_prev.so) and this one, alternated
+      for i in 1 2; do
+        run "legs prev $i" 300 env OZEC_LIB_OVERRIDE=ab/libozec_prev.so python -u bench.py --workload legs --no-cpu \
+          --no-pmc > "$OUT/legs_prev_$i.json" 2>> "$OUT/abprev.err" || exit 18
+        run "legs new $i" 300 python -u bench.py --workload legs --no-cpu --no-pmc > "$OUT/legs_new_$i.json" \
+          2>> "$OUT/abprev.err" || exit 19
+      done ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     heap)

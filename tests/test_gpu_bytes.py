@@ -1,0 +1,91 @@
+"""Byte-granular cells on the fused encode + CRC path (round 5, fused_nb.hpp nb_tail) vs the oracle (GPU).
+
+Every key's last stripe has cells of any length (parityCellSize = dataBuffers[0].position(),
+ECKeyOutputStream.java:276), and a packed device batch of such stripes puts its units at odd byte offsets.  These
+cells now run on the nibble kernel: the whole 16-B blocks in the window loop, the last 1-15 bytes of each unit in
+nb_tail (bytewise CRC register update, GF products from the s_gf nibble products), with unaligned 16-B buffer
+accesses for the blocks.  Checked bit-exact against oracle.rs_encode / oracle.crc_windows (Checksum.java:157-200,
+RSRawEncoder), with guard bytes around the batch that must stay untouched.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from ozone_amd import checksum as ck  # noqa: E402
+from ozone_amd import _lib as L  # noqa: E402
+from ozone_amd import rawcoder as rc  # noqa: E402
+
+DEV = "cuda:0"
+GUARD = 64
+
+
+def _otype(ctype):
+    return oracle.CRC32 if ctype == ck.ChecksumType.CRC32 else oracle.CRC32C
+
+
+def _packed_case(k, p, n, S, bpc, ctype, shift, seed):
+    """S stripes of k + p units of n bytes back to back (unit stride n, stripe stride (k + p) n) starting `shift`
+    bytes into a device buffer with GUARD bytes of 0xA5 on both sides; parity written in place."""
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, (S, k, n), dtype=np.uint8)
+    flat = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
+    body = flat[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
+    body[:, :k] = data
+    d = torch.from_numpy(flat).to(DEV)
+    base = d[GUARD + shift:]
+    nwin = -(-n // bpc)
+    crcs = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    rc.RawErasureEncoder(rc.ECReplicationConfig(k, p)).encode_crc_batch(
+        base, (k + p) * n, n, base[k * n:], (k + p) * n, n, S, n, ctype, bpc, crcs)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    c = crcs.cpu().numpy().view(np.uint32)
+    assert (got[:GUARD + shift] == 0xA5).all() and (got[GUARD + shift + S * (k + p) * n:] == 0xA5).all()
+    units = got[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
+    ot = _otype(ctype)
+    for s in range(S):
+        ref = oracle.rs_encode(k, p, list(data[s]))
+        for q in range(p):
+            assert (units[s, k + q] == ref[q]).all(), (k, p, n, s, q)
+        for u, cell in enumerate(list(data[s]) + ref):
+            assert (c[s, u] == oracle.crc_windows(ot, cell, bpc)).all(), (k, p, n, bpc, s, u)
+
+
+@pytest.mark.parametrize("k,p", [(6, 3), (10, 4), (3, 2), (6, 1), (10, 2), (3, 1)])
+@pytest.mark.parametrize("n", [1, 5, 15, 17, 1007, 2 * 4096 + 5, 16384 + 3, 50001, 3 * 16384 + 15])
+def test_encode_crc_packed_odd_cells(k, p, n):
+    """Cells of 1 B up to several windows + 15 B, packed at odd strides, CRC32C per 16 KiB (4 KiB for the short)."""
+    bpc = 4096 if n < 16384 else 16384
+    _packed_case(k, p, n, 5, bpc, ck.ChecksumType.CRC32C, 0, [k, p, n])
+
+
+@pytest.mark.parametrize("ctype", [ck.ChecksumType.CRC32, ck.ChecksumType.CRC32C])
+@pytest.mark.parametrize("shift", [1, 3, 8])
+def test_encode_crc_unaligned_base(ctype, shift):
+    """A batch whose base pointer is 1 / 3 / 8 bytes past 16-B alignment, cells a multiple of 16 B (every unit
+    offset unaligned, no byte tail) and not (both)."""
+    for n in (65536, 65536 + 9):
+        _packed_case(6, 3, n, 4, 16384, ctype, shift, [shift, n])
+
+
+@pytest.mark.parametrize("variant", [0, 170, 171, 172, 173, 174, 177, 62, 87, 49, 56])
+def test_encode_crc_odd_cells_any_variant(variant):
+    """A pinned variant without the lane-parallel emit (62 / 87 nibble, 49 per-window, 56 streamed-input) falls back
+    to the default nibble variant for byte-granular cells; the EM variants run them as pinned."""
+    lib = L.lib()
+    assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+    try:
+        _packed_case(10, 4, 2 * 16384 + 4099, 3, 16384, ck.ChecksumType.CRC32C, 0, [variant])
+        _packed_case(6, 3, 16384 + 1, 3, 16384, ck.ChecksumType.CRC32C, 5, [variant, 1])
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+
+
+def test_encode_crc_odd_cells_c5_shape():
+    """rs-6-3 cells of 700,001 B (the odd-tail row of bench.py --workload tail) packed, 24 stripes: every stripe
+    against the oracle."""
+    _packed_case(6, 3, 700_001, 24, 16384, ck.ChecksumType.CRC32C, 0, [700_001])

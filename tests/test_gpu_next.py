@@ -70,6 +70,11 @@ def _stripe_units(codec, k, p, n, S, first):
     ("rs", 3, 2, [4], 1 << 16, 16384),            # fused shape (3,1): single-unit reconstruction
     ("rs", 6, 3, [2], 4 * 16384 + 3008, 16384),   # nibble kernel, a 3008-B last window (virtual zero blocks in front)
     ("rs", 10, 4, [0, 5, 11], 3 * 16384 + 16, 16384),  # ... and a one-block last window
+    # byte-granular cells at odd unit strides (round 5, nb_tail): blocks + a 3-B tail, a 7-B last window with no
+    # whole block (the planted corruption sits in it), 50,001 B (an 849-B last window: 53 blocks + 1 B)
+    ("rs", 6, 3, [0, 2, 7], 4 * 16384 + 3011, 16384),
+    ("rs", 10, 4, [1, 4, 10, 13], 3 * 16384 + 7, 16384),
+    ("rs", 3, 2, [0, 4], 50001, 16384),
 ])
 @pytest.mark.parametrize("variant", [0] + variants.RS_FUSED + [4, 5])
 def test_reconstruct_crc_batch(codec, k, p, erased, n, bpc, variant):

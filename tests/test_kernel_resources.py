@@ -19,11 +19,11 @@ def _b(v):
     return f"Lb{int(v)}E"
 
 
-def _nb(K, R, D, NB, WPB, DYN, H, G6=False):
-    """Mangled template-argument list of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H, G6> (XO, EM on),
+def _nb(K, R, D, NB, WPB, DYN, H):
+    """Mangled template-argument list of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H> (XO, EM on),
     closed, so that it names exactly one instantiation."""
     return "encode_crc_nbI" + "".join([_i(K), _i(R), _i(D), _i(NB), _i(WPB), _i(4), _i(2), _b(1), _i(DYN), _b(1),
-                                       _b(1), _i(H), _b(G6)]) + "EEvN"
+                                       _b(1), _i(H)]) + "EEvN"
 
 
 def _defaults():

@@ -1094,6 +1094,12 @@ uint32_t ozec_crc_value(int, uint32_t state) { return ~state; }
 
 // ---- fused encode + CRC --------------------------------------------------------------------------
 
+// whether a fused encode / reconstruct + CRC batch is large enough for the fused kernel, which runs one wave per
+// (stripe, window) unit (TuneKnobs::fused_min_units)
+static bool fused_pays(size_t num_stripes, int64_t nwin) {
+  return static_cast<int64_t>(num_stripes) * nwin >= ozec::g_tune.fused_min_units.load(std::memory_order_relaxed);
+}
+
 int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
                           uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes,
                           size_t len, int checksum_type, size_t bpc, uint32_t *d_crcs, int big_endian, void *stream) {
@@ -1123,7 +1129,7 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
   if (int rc = make_crc_args(ctx, checksum_type, nullptr, 0, num_stripes, len, bpc, d_crcs, nwin, big_endian, 0,
                              &e.crc))
     return rc;
-  if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
+  if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) && fused_pays(num_stripes, nwin)) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
   } else {
     // unfused: encode, then the CRC pass (crcs[s][u][w] layout kept): one launch over all S x units cells when they
@@ -1495,7 +1501,8 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
   e.verify = 1;
   e.exp_units = n_all;
   for (int j = 0; j < nin; ++j) e.in_unit[j] = units[j];
-  if (nrows && n_erased == nrows && ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
+  if (nrows && n_erased == nrows && ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) &&
+      fused_pays(num_stripes, nwin)) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
   } else {
     // unfused: verify the read units, decode, CRC the rebuilt units
@@ -1991,6 +1998,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "host_duplex") {
     if (value < 0) return bad();
     t.host_duplex.store(value);
+  } else if (k == "fused_min_units") {
+    if (value < 0) return bad();
+    t.fused_min_units.store(value);
   } else {
     return fail(OZEC_EINVAL, "unknown tuning key " + k);
   }

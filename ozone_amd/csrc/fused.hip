@@ -265,25 +265,25 @@ bool encode_crc_nb_bytes_supported(const CodeArgs &a, int64_t bpc) {
 
 namespace {
 
-hipError_t launch_nb_shape(const EncCrcArgs &e, hipStream_t st, int v) {
+hipError_t launch_nb_shape(const EncCrcArgs &e, hipStream_t st, int v, bool tail) {
   const int k = e.code.k, r = e.code.rows;
-  if (k == 6 && r == 3) return launch_nb_6_3(e, st, v);
-  if (k == 6 && r == 2) return launch_nb_6_2(e, st, v);
-  if (k == 6 && r == 1) return launch_nb_6_1(e, st, v);
-  if (k == 3 && r == 2) return launch_nb_3_2(e, st, v);
-  if (k == 3 && r == 1) return launch_nb_3_1(e, st, v);
-  if (k == 10 && r == 4) return launch_nb_10_4(e, st, v);
-  if (k == 10 && r == 3) return launch_nb_10_3(e, st, v);
-  if (k == 10 && r == 2) return launch_nb_10_2(e, st, v);
-  if (k == 10 && r == 1) return launch_nb_10_1(e, st, v);
+  if (k == 6 && r == 3) return launch_nb_6_3(e, st, v, tail);
+  if (k == 6 && r == 2) return launch_nb_6_2(e, st, v, tail);
+  if (k == 6 && r == 1) return launch_nb_6_1(e, st, v, tail);
+  if (k == 3 && r == 2) return launch_nb_3_2(e, st, v, tail);
+  if (k == 3 && r == 1) return launch_nb_3_1(e, st, v, tail);
+  if (k == 10 && r == 4) return launch_nb_10_4(e, st, v, tail);
+  if (k == 10 && r == 3) return launch_nb_10_3(e, st, v, tail);
+  if (k == 10 && r == 2) return launch_nb_10_2(e, st, v, tail);
+  if (k == 10 && r == 1) return launch_nb_10_1(e, st, v, tail);
   return hipErrorInvalidValue;
 }
 
 }  // namespace
 
-hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
+hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v, bool tail) {
   const int k = e.code.k, r = e.code.rows;
-  if (v == 56 || v == 59) {
+  if (!tail && (v == 56 || v == 59)) {
     if (k == 6 && r == 3) return launch_lv_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_lv_kr<6, 2>(e, st, v);
     if (k == 3 && r == 2) return launch_lv_kr<3, 2>(e, st, v);
@@ -304,11 +304,12 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v) {
   // profiles/r03/em/ab_*.log); rs-10-x takes two-step groups with the second distance set for half the inputs (177,
   // 0.5-1.3 % faster than 170 in three same-process A/Bs, profiles/r03/h/)
   WorkSlot *ws = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) ? work_lease(st) : nullptr;
+  if (tail && !nb_variant_tail(v)) v = 0;  // byte-granular cells: the TAIL instantiations of the EM variants
   if (v == 0) v = k == 10 ? (ws ? 177 : 173) : !ws ? 174 : k == 6 ? 171 : 172;
   const bool used = ws && nb_variant_persistent(v);
   EncCrcArgs ed = e;
   ed.work = used ? ws->ctr : nullptr;
-  const hipError_t err = launch_nb_shape(ed, st, v);
+  const hipError_t err = launch_nb_shape(ed, st, v, tail);
   // the event goes behind the launch whatever `err` says: an event behind a launch that never ran costs nothing, a
   // kernel left running without one would share its counters with the slot's next lease
   if (ws) work_return(ws, st, used);

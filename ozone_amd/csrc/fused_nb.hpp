@@ -9,7 +9,7 @@ namespace ozec {
 
 
 #define OZEC_NB_SHAPES(X) X(6, 3) X(6, 2) X(6, 1) X(3, 2) X(3, 1) X(10, 4) X(10, 3) X(10, 2) X(10, 1)
-#define OZEC_NB_DECL(K, R) hipError_t launch_nb_##K##_##R(const EncCrcArgs &e, hipStream_t st, int v);
+#define OZEC_NB_DECL(K, R) hipError_t launch_nb_##K##_##R(const EncCrcArgs &e, hipStream_t st, int v, bool tail);
 OZEC_NB_SHAPES(OZEC_NB_DECL)
 
 namespace {
@@ -158,7 +158,7 @@ __device__ __forceinline__ uint32_t nb_tail(const EncCrcArgs &e, __amdgpu_buffer
 // (Round-3 probes -- output-register groups, VALU / LDS pads, far-addressing without the index OR, late lane-tree
 // tables, guided and static persistent orders -- are measured in DESIGN 2.3 and were taken out of the library.)
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
-          bool EM = false, int H = K>
+          bool EM = false, int H = K, bool TAIL = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -166,6 +166,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   static_assert((D * K) % NB == 0, "the ring must divide the unrolled group so ring indices are compile-time");
   static_assert(DYN == 0 || DYN == 1, "one wave per unit, or the persistent WorkQueue grid");
   static_assert(H == K || (XO && D == 2 && H >= 0 && H < K), "partial second distance set: XO, two-step groups");
+  static_assert(!TAIL || (RS && EM), "byte tails leave through the lane-parallel emit");
   constexpr int kSets = K + (D - 1) * H;  // (d, j) nibble tables of 4 KiB: all K inputs in set 0, inputs < H in sets >= 1
   // one LDS block: G26 blob of D sets, then the (d, j, p) nibble tables, then the GF dwords of the setup.  Table
   // regions past the 16-bit ds_read offset range are reached with bit 15 set in the index register (one v_or_b32).
@@ -357,11 +358,13 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
       int q = 0;
       const uint32_t v = g5_lane_tree_rs<K + R>(s_tree - kG5Tree, S, lane, q);
       if constexpr (EM) {
-        // the cell's last 1-15 bytes (nb_tail; launch_encode_crc sends such cells to EM variants only)
-        const int32_t tb = last ? static_cast<int32_t>((a.len - w * cr.bpc) & 15) : 0;
         uint32_t vt = v;
-        if (tb != 0 && lane < tree_np(K + R) && q < K + R)
-          vt = nb_tail<K, R>(e, rin, rout, s_gf, q, v, static_cast<uint32_t>((a.len - w * cr.bpc) & ~int64_t{15}), tb);
+        if constexpr (TAIL) {  // the cell's last 1-15 bytes (nb_tail)
+          const int32_t tb = last ? static_cast<int32_t>((a.len - w * cr.bpc) & 15) : 0;
+          if (tb != 0 && lane < tree_np(K + R) && q < K + R)
+            vt = nb_tail<K, R>(e, rin, rout, s_gf, q, v, static_cast<uint32_t>((a.len - w * cr.bpc) & ~int64_t{15}),
+                               tb);
+        }
         if (lane < tree_np(K + R) && q < K + R) nb_emit_lane<K, R>(e, s, w, q, vt, init);
       } else if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
 #pragma unroll
@@ -381,16 +384,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
-          bool EM = false, int H = K>
+          bool EM = false, int H = K, bool TAIL = false>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
     constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
     static_assert(kNB != NB && (D * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H>(e, st);
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
@@ -470,6 +473,28 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 193: return launch_nb<K, R, 2, kNB, 14, 7, 2, true, 1, true, true>(e, st);
     case 194: return launch_nb<K, R, 2, kNB, 9, 7, 2, true, 1, true, true, kHh>(e, st);
     case 196: return launch_nb<K, R, 2, 2, 16, 4, 1, true, 1, true, true, kHh>(e, st);
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+// cells of any length at any byte offsets (encode_crc_nb_bytes_supported): the defaults and their alternates with the
+// lane-parallel emit, instantiated a second time with the nb_tail epilogue (TAIL), so the kernels of 16-B cells keep
+// their code (the epilogue in every instantiation cost C3r 1.3-2 %, profiles/r05/bytes/)
+constexpr bool nb_variant_tail(int v) { return v == 170 || v == 171 || v == 172 || v == 173 || v == 174 || v == 177; }
+
+template <int K, int R>
+hipError_t launch_nb_tail_kr(const EncCrcArgs &e, hipStream_t st, int v) {
+  constexpr int kD2 = K * 2 * 4096 + g26_words(2) * 4 <= 65536 ? 2 : 1;
+  constexpr int kNB = K % 2 == 0 && K > 2 ? K / 2 : K;
+  constexpr int kHh = K / 2;
+  switch (v) {
+    case 170: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true, K, true>(e, st);
+    case 171: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true, true, K, true>(e, st);
+    case 172: return launch_nb<K, R, 2, 2, 16, 4, 2, true, 1, true, true, K, true>(e, st);
+    case 173: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, true, true, K, true>(e, st);
+    case 174: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, true, true, K, true>(e, st);
+    case 177: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true, true, kHh, true>(e, st);
     default: break;
   }
   return hipErrorInvalidValue;

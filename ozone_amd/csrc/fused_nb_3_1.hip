@@ -2,5 +2,7 @@
 #include "fused_nb.hpp"
 
 namespace ozec {
-hipError_t launch_nb_3_1(const EncCrcArgs &e, hipStream_t st, int v) { return launch_nb_kr<3, 1>(e, st, v); }
+hipError_t launch_nb_3_1(const EncCrcArgs &e, hipStream_t st, int v, bool tail) {
+  return tail ? launch_nb_tail_kr<3, 1>(e, st, v) : launch_nb_kr<3, 1>(e, st, v);
+}
 }  // namespace ozec

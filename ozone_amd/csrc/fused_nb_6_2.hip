@@ -2,5 +2,7 @@
 #include "fused_nb.hpp"
 
 namespace ozec {
-hipError_t launch_nb_6_2(const EncCrcArgs &e, hipStream_t st, int v) { return launch_nb_kr<6, 2>(e, st, v); }
+hipError_t launch_nb_6_2(const EncCrcArgs &e, hipStream_t st, int v, bool tail) {
+  return tail ? launch_nb_tail_kr<6, 2>(e, st, v) : launch_nb_kr<6, 2>(e, st, v);
+}
 }  // namespace ozec

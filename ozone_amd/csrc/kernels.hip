@@ -1076,10 +1076,10 @@ hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   // (fused_nb.hpp); 56 / 59 the streamed-input kernel (full windows only); variant 49 pins the per-window kernel
   const int v = g_tune.crc_variant.load(std::memory_order_relaxed);
   if (!aligned16(e.code.len) || !vec_ok(e.code)) {
-    // byte-granular cells (a key's last stripe, odd unit strides): the nibble kernel's EM variants only (nb_tail); a
-    // pinned variant without EM falls back to the default one
+    // byte-granular cells (a key's last stripe, odd unit strides): the nibble kernel's TAIL instantiations (nb_tail);
+    // a pinned variant without one falls back to the default
     if (!encode_crc_nb_bytes_supported(e.code, e.crc.bpc)) return hipErrorInvalidValue;
-    return launch_encode_crc_lv(e, st, v >= 170 && v < 300 ? v : 0);
+    return launch_encode_crc_lv(e, st, v, true);
   }
   if (v == 0 || (v >= 50 && v < 300)) {
     const bool lv = v == 56 || v == 59;

@@ -162,6 +162,9 @@ struct TuneKnobs {
   std::atomic<int64_t> host_duplex{512 << 10};  // pinned host-buffer coding calls of at least this many bytes per unit
                                                 // go up, through the kernel and back in column chunks, the D2H of
                                                 // chunk c on a second stream beside the H2D of chunk c+1 (0: off)
+  std::atomic<int64_t> fused_min_units{0};  // fused encode / reconstruct + CRC batches of fewer (stripe, window) units
+                                            // take the unfused kernels (coding, then the CRC pass), which spread a
+                                            // small batch over more waves (0: always fused)
 };
 
 // Kernel alternates the library holds besides the defaults, selectable with ozec_set_tuning for A/B (0 = default).
@@ -208,7 +211,7 @@ bool encode_crc_lv_supported(const EncCrcArgs &e);
 // the nibble-table kernel (fused_nb.hpp): the same shapes, and a short last window of any whole number of 16-B blocks
 bool encode_crc_nb_supported(const EncCrcArgs &e);
 bool encode_crc_nb_bytes_supported(const CodeArgs &a, int64_t bpc);
-hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant);
+hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant, bool tail = false);
 
 // WorkQueue counter slots of the persistent kernels (device.hpp WorkQueue; pool in work_slots.cpp).  work_lease gives a
 // zeroed slot of the current device, not in use by any launch still running, or null (capturing stream, pool full,

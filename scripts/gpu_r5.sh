@@ -69,6 +69,9 @@ for s in $STEPS; do
         run "legs new $i" 300 python -u bench.py --workload legs --no-cpu --no-pmc > "$OUT/legs_new_$i.json" \
           2>> "$OUT/abprev.err" || exit 19
       done ;;
+    small)  # per-call time of small fused batches: fused kernel vs unfused kernels (fused_min_units)
+      run "small batches" 400 python -u scripts/small_batch_ab.py ${ROUNDS:-5} > "$OUT/small_batch_ab.json" \
+        2> "$OUT/small_batch_ab.err" || { tail -20 "$OUT/small_batch_ab.err"; exit 20; } ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     heap)

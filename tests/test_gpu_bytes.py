@@ -74,8 +74,9 @@ def test_encode_crc_unaligned_base(ctype, shift):
 
 @pytest.mark.parametrize("variant", [0, 170, 171, 172, 173, 174, 177, 62, 87, 49, 56])
 def test_encode_crc_odd_cells_any_variant(variant):
-    """A pinned variant without the lane-parallel emit (62 / 87 nibble, 49 per-window, 56 streamed-input) falls back
-    to the default nibble variant for byte-granular cells; the EM variants run them as pinned."""
+    """Byte-granular cells run on the TAIL instantiations of the nibble kernel (fused_nb.hpp launch_nb_tail_kr:
+    170-174, 177 as pinned); any other pinned variant (62 / 87 nibble, 49 per-window, 56 streamed-input) falls back to
+    the default one."""
     lib = L.lib()
     assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
     try:
@@ -89,3 +90,15 @@ def test_encode_crc_odd_cells_c5_shape():
     """rs-6-3 cells of 700,001 B (the odd-tail row of bench.py --workload tail) packed, 24 stripes: every stripe
     against the oracle."""
     _packed_case(6, 3, 700_001, 24, 16384, ck.ChecksumType.CRC32C, 0, [700_001])
+
+
+@pytest.mark.parametrize("k,p,n", [(6, 3, 1 << 20), (10, 4, 700_001), (3, 2, 1007)])
+def test_fused_min_units_routes_small_batches_unfused(k, p, n):
+    """Batches below fused_min_units (stripe x window units) take the unfused kernels: same bytes and CRCs."""
+    lib = L.lib()
+    try:
+        for m in (0, 1 << 40):
+            assert lib.ozec_set_tuning(b"fused_min_units", m) == 0
+            _packed_case(k, p, n, 2, 16384, ck.ChecksumType.CRC32C, 0, [k, n])
+    finally:
+        lib.ozec_set_tuning(b"fused_min_units", 0)

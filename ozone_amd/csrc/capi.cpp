@@ -1094,12 +1094,6 @@ uint32_t ozec_crc_value(int, uint32_t state) { return ~state; }
 
 // ---- fused encode + CRC --------------------------------------------------------------------------
 
-// whether a fused encode / reconstruct + CRC batch is large enough for the fused kernel, which runs one wave per
-// (stripe, window) unit (TuneKnobs::fused_min_units)
-static bool fused_pays(size_t num_stripes, int64_t nwin) {
-  return static_cast<int64_t>(num_stripes) * nwin >= ozec::g_tune.fused_min_units.load(std::memory_order_relaxed);
-}
-
 int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
                           uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes,
                           size_t len, int checksum_type, size_t bpc, uint32_t *d_crcs, int big_endian, void *stream) {
@@ -1129,7 +1123,8 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
   if (int rc = make_crc_args(ctx, checksum_type, nullptr, 0, num_stripes, len, bpc, d_crcs, nwin, big_endian, 0,
                              &e.crc))
     return rc;
-  if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) && fused_pays(num_stripes, nwin)) {
+  // a small batch of 16-B cells runs faster unfused: the fused kernel gives each (stripe, window) one wave
+  if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) && ozec::encode_crc_fused_pays(a, nwin)) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
   } else {
     // unfused: encode, then the CRC pass (crcs[s][u][w] layout kept): one launch over all S x units cells when they
@@ -1501,8 +1496,7 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
   e.verify = 1;
   e.exp_units = n_all;
   for (int j = 0; j < nin; ++j) e.in_unit[j] = units[j];
-  if (nrows && n_erased == nrows && ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) &&
-      fused_pays(num_stripes, nwin)) {
+  if (nrows && n_erased == nrows && ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
   } else {
     // unfused: verify the read units, decode, CRC the rebuilt units

@@ -1068,6 +1068,11 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
   return (aligned16(a.len) && vec_ok(a)) || encode_crc_nb_bytes_supported(a, bpc);
 }
 
+bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin) {
+  if (!aligned16(a.len) || !vec_ok(a)) return true;  // byte-granular: the unfused kernels take their byte paths
+  return a.nstripes * nwin >= g_tune.fused_min_units.load(std::memory_order_relaxed);
+}
+
 hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   if (e0.code.nstripes * e0.crc.nwin <= 0) return hipSuccess;
   EncCrcArgs e = e0;

@@ -159,12 +159,18 @@ struct TuneKnobs {
   std::atomic<int64_t> host_graph{256 << 10};  // host-buffer coding calls of one staged chunk up to this many bytes
                                                // per unit replay a cached hipGraph of H2D + kernel + D2H (0: off;
                                                // 64 KiB-cell rs-6-3 stripe from pageable cells 74 -> 64 us)
-  std::atomic<int64_t> host_duplex{512 << 10};  // pinned host-buffer coding calls of at least this many bytes per unit
-                                                // go up, through the kernel and back in column chunks, the D2H of
-                                                // chunk c on a second stream beside the H2D of chunk c+1 (0: off)
-  std::atomic<int64_t> fused_min_units{0};  // fused encode / reconstruct + CRC batches of fewer (stripe, window) units
-                                            // take the unfused kernels (coding, then the CRC pass), which spread a
-                                            // small batch over more waves (0: always fused)
+  std::atomic<int64_t> host_duplex{0};  // pinned host-buffer coding calls of at least this many bytes per unit go
+                                        // up, through the kernel and back in column chunks, the D2H of chunk c on a
+                                        // second stream beside the H2D of chunk c+1 (0: off, the default: 512 KiB
+                                        // lost in both A/Bs -- JNI 1 MiB cells 263-294 -> 317-343 us at 1 thread,
+                                        // 492-501 -> 774-779 us at 4; pinned batches 28.1-29.6 -> 23.4-23.5 GB/s,
+                                        // profiles/r05/duplex/)
+  std::atomic<int64_t> fused_min_units{5120};  // fused encode + CRC batches of 16-B cells with fewer (stripe, window)
+                                               // units take the unfused kernels (coding, then one CRC pass), which
+                                               // spread a small batch over many more waves: one rs-6-3 stripe of
+                                               // 1 MiB cells 15 us instead of 164 us, 64 stripes 228 vs 262 us, 128
+                                               // stripes 410 vs 308 us (scripts/small_batch_ab.py,
+                                               // profiles/r05/small/; 0: always fused)
 };
 
 // Kernel alternates the library holds besides the defaults, selectable with ozec_set_tuning for A/B (0 = default).
@@ -206,6 +212,8 @@ hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t nc
                                   uint64_t first_stream, hipStream_t stream);
 // true when the fused kernel supports this (k, rows) pair with the given geometry
 bool encode_crc_supported(const CodeArgs &a, int64_t bpc);
+// whether a supported fused batch should run fused (TuneKnobs::fused_min_units; byte-granular layouts always do)
+bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin);
 // the streamed-input fused kernel (fused.hip): RS shapes with full windows, bpc % 4096 == 0; `e` already rebased
 bool encode_crc_lv_supported(const EncCrcArgs &e);
 // the nibble-table kernel (fused_nb.hpp): the same shapes, and a short last window of any whole number of 16-B blocks

@@ -1,5 +1,7 @@
-"""Per-call time of small fused encode + CRC32C batches, fused kernel vs unfused kernels (TuneKnobs fused_min_units),
-device-resident and from pinned host memory, interleaved in one process (sets the fused_min_units default).
+"""Per-call time of small fused encode + CRC32C batches of 16-B cells, fused kernel vs unfused kernels (TuneKnobs
+fused_min_units), device-resident and from pinned host memory, interleaved in one process: where the
+fused_min_units default comes from.  (Byte-granular cells always run fused: their unfused kernels take byte paths,
+7-8x slower in the first run of this script, profiles/r05/small/.)
 usage: python scripts/small_batch_ab.py [ROUNDS]"""
 import json
 import os
@@ -44,6 +46,7 @@ def host_case(S, n):
     def call():
         enc.encode_crc_host_batch(a.ctypes.data, (k + p) * n, n, a.ctypes.data + k * n, (k + p) * n, n, S, n,
                                   ck.ChecksumType.CRC32C, bpc, crc)
+    call.keep = pb  # the pinned buffer lives as long as the call that uses it
     return call, None
 
 
@@ -57,7 +60,7 @@ def timed(call, reps):
 
 
 for where, make in (("device", dev_case), ("host_pinned", host_case)):
-    for n in (1 << 20, 700_001, 65536):
+    for n in (1 << 20, 700_000, 65536):
         for S in (1, 2, 4, 8, 16, 32, 64, 128):
             if where == "host_pinned" and S > 32:
                 continue
@@ -83,4 +86,4 @@ for where, make in (("device", dev_case), ("host_pinned", host_case)):
                 row[f"{m}_us"] = round(float(np.median(res[m])), 1)
             row["unfused_over_fused"] = round(row["unfused_us"] / row["fused_us"], 3)
             print(json.dumps(row), flush=True)
-lib.ozec_set_tuning(b"fused_min_units", 0)
+lib.ozec_set_tuning(b"fused_min_units", 5120)

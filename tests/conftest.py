@@ -28,3 +28,20 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _fused_kernels_in_gpu_tests(request):
+    """GPU tests run the fused kernels at every batch size: libozec's default sends batches of 16-B cells below
+    fused_min_units (stripe x window units) to the unfused kernels, which would take the small parity batches away
+    from the fused kernels and variants they are written for.  tests/test_gpu_bytes.py covers both routes."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from ozone_amd import _lib as L
+    lib = L.lib()
+    assert lib.ozec_set_tuning(b"fused_min_units", 0) == 0
+    try:
+        yield
+    finally:
+        lib.ozec_set_tuning(b"fused_min_units", 5120)

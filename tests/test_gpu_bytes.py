@@ -94,11 +94,12 @@ def test_encode_crc_odd_cells_c5_shape():
 
 @pytest.mark.parametrize("k,p,n", [(6, 3, 1 << 20), (10, 4, 700_001), (3, 2, 1007)])
 def test_fused_min_units_routes_small_batches_unfused(k, p, n):
-    """Batches below fused_min_units (stripe x window units) take the unfused kernels: same bytes and CRCs."""
+    """Batches of 16-B cells below fused_min_units (stripe x window units) take the unfused kernels, byte-granular
+    ones stay fused: same bytes and CRCs either way."""
     lib = L.lib()
     try:
         for m in (0, 1 << 40):
             assert lib.ozec_set_tuning(b"fused_min_units", m) == 0
             _packed_case(k, p, n, 2, 16384, ck.ChecksumType.CRC32C, 0, [k, n])
     finally:
-        lib.ozec_set_tuning(b"fused_min_units", 0)
+        lib.ozec_set_tuning(b"fused_min_units", 5120)

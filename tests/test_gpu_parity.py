@@ -918,7 +918,7 @@ def test_host_path_pinned_duplex_column_chunks(n, duplex):
             del views, units, dins, outs
             pool.free()
     finally:
-        lib.ozec_set_tuning(b"host_duplex", 512 << 10)
+        lib.ozec_set_tuning(b"host_duplex", 0)
 
 
 # Caller memory registered with ozec_host_register stays mapped until the process exits, as include/ozec.h asks of

@@ -19,20 +19,22 @@ def _b(v):
     return f"Lb{int(v)}E"
 
 
-def _nb(K, R, D, NB, WPB, DYN, H):
-    """Mangled template-argument list of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H> (XO, EM on),
-    closed, so that it names exactly one instantiation."""
+def _nb(K, R, D, NB, WPB, DYN, H, tail):
+    """Mangled template-argument list of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H, TAIL> (XO, EM
+    on), closed, so that it names exactly one instantiation."""
     return "encode_crc_nbI" + "".join([_i(K), _i(R), _i(D), _i(NB), _i(WPB), _i(4), _i(2), _b(1), _i(DYN), _b(1),
-                                       _b(1), _i(H)]) + "EEvN"
+                                       _b(1), _i(H), _b(tail)]) + "EEvN"
 
 
 def _defaults():
     """fused.hip: rs-10-x 177 (queue) / 173, rs-6-x 171 / 174, rs-3-x 172 / 174 (fused_nb.hpp launch_nb_kr), x = 1-4."""
-    out = [_nb(10, R, 2, 5, 16, 1, 5) for R in (1, 2, 3, 4)]     # 177
-    out += [_nb(10, R, 1, 5, 8, 0, 10) for R in (1, 2, 3, 4)]    # 173
-    out += [_nb(6, R, 2, 3, 16, 1, 6) for R in (1, 2, 3)]   # 171
-    out += [_nb(6, R, 2, 2, 12, 0, 6) for R in (1, 2, 3)]   # 174 (kD2 = 2 for K = 6)
-    out += [_nb(3, R, 2, 2, 16, 1, 3) for R in (1, 2)] + [_nb(3, R, 2, 2, 12, 0, 3) for R in (1, 2)]  # 172, 174
+    out = []
+    for t in (False, True):  # 16-B cells, and the byte-tail (TAIL) instantiation of the same variant
+        out += [_nb(10, R, 2, 5, 16, 1, 5, t) for R in (1, 2, 3, 4)]     # 177
+        out += [_nb(10, R, 1, 5, 8, 0, 10, t) for R in (1, 2, 3, 4)]    # 173
+        out += [_nb(6, R, 2, 3, 16, 1, 6, t) for R in (1, 2, 3)]   # 171
+        out += [_nb(6, R, 2, 2, 12, 0, 6, t) for R in (1, 2, 3)]   # 174 (kD2 = 2 for K = 6)
+        out += [_nb(3, R, 2, 2, 16, 1, 3, t) for R in (1, 2)] + [_nb(3, R, 2, 2, 12, 0, 3, t) for R in (1, 2)]
     return out
 
 

@@ -1124,7 +1124,8 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
                              &e.crc))
     return rc;
   // a small batch of 16-B cells runs faster unfused: the fused kernel gives each (stripe, window) one wave
-  if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) && ozec::encode_crc_fused_pays(a, nwin)) {
+  if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) &&
+      ozec::encode_crc_fused_pays(a, nwin, ozec::g_tune.fused_min_units.load(std::memory_order_relaxed))) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
   } else {
     // unfused: encode, then the CRC pass (crcs[s][u][w] layout kept): one launch over all S x units cells when they
@@ -1496,7 +1497,8 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
   e.verify = 1;
   e.exp_units = n_all;
   for (int j = 0; j < nin; ++j) e.in_unit[j] = units[j];
-  if (nrows && n_erased == nrows && ozec::encode_crc_supported(a, static_cast<int64_t>(bpc))) {
+  if (nrows && n_erased == nrows && ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) &&
+      ozec::encode_crc_fused_pays(a, nwin, ozec::g_tune.rec_min_units.load(std::memory_order_relaxed))) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
   } else {
     // unfused: verify the read units, decode, CRC the rebuilt units
@@ -1992,9 +1994,10 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "host_duplex") {
     if (value < 0) return bad();
     t.host_duplex.store(value);
-  } else if (k == "fused_min_units") {
+  } else if (k == "fused_min_units" || k == "rec_min_units" || k == "nb_small_units") {
     if (value < 0) return bad();
-    t.fused_min_units.store(value);
+    auto &knob = k == "fused_min_units" ? t.fused_min_units : k == "rec_min_units" ? t.rec_min_units : t.nb_small_units;
+    knob.store(value);
   } else {
     return fail(OZEC_EINVAL, "unknown tuning key " + k);
   }

@@ -473,6 +473,12 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 193: return launch_nb<K, R, 2, kNB, 14, 7, 2, true, 1, true, true>(e, st);
     case 194: return launch_nb<K, R, 2, kNB, 9, 7, 2, true, 1, true, true, kHh>(e, st);
     case 196: return launch_nb<K, R, 2, 2, 16, 4, 1, true, 1, true, true, kHh>(e, st);
+    // round 5, small batches: 173 (one-step groups, one wave per (stripe, window) unit, no WorkQueue) in workgroups of
+    // 1 / 2 / 4 waves, so a batch of a few hundred units spreads over as many CUs instead of 16-wave workgroups on a
+    // handful (the LDS pipe of each CU serves all its waves)
+    case 220: return launch_nb<K, R, 1, kNB, 1, 4, 2, true, 0, true, true>(e, st);
+    case 221: return launch_nb<K, R, 1, kNB, 2, 4, 2, true, 0, true, true>(e, st);
+    case 222: return launch_nb<K, R, 1, kNB, 4, 4, 2, true, 0, true, true>(e, st);
     default: break;
   }
   return hipErrorInvalidValue;
@@ -481,7 +487,9 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
 // cells of any length at any byte offsets (encode_crc_nb_bytes_supported): the defaults and their alternates with the
 // lane-parallel emit, instantiated a second time with the nb_tail epilogue (TAIL), so the kernels of 16-B cells keep
 // their code (the epilogue in every instantiation cost C3r 1.3-2 %, profiles/r05/bytes/)
-constexpr bool nb_variant_tail(int v) { return v == 170 || v == 171 || v == 172 || v == 173 || v == 174 || v == 177; }
+constexpr bool nb_variant_tail(int v) {
+  return v == 170 || v == 171 || v == 172 || v == 173 || v == 174 || v == 177 || (v >= 220 && v <= 222);
+}
 
 template <int K, int R>
 hipError_t launch_nb_tail_kr(const EncCrcArgs &e, hipStream_t st, int v) {
@@ -495,6 +503,9 @@ hipError_t launch_nb_tail_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 173: return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, true, true, K, true>(e, st);
     case 174: return launch_nb<K, R, kD2, 2, 12, 4, 2, true, 0, true, true, K, true>(e, st);
     case 177: return launch_nb<K, R, 2, kNB, 16, 4, 2, true, 1, true, true, kHh, true>(e, st);
+    case 220: return launch_nb<K, R, 1, kNB, 1, 4, 2, true, 0, true, true, K, true>(e, st);
+    case 221: return launch_nb<K, R, 1, kNB, 2, 4, 2, true, 0, true, true, K, true>(e, st);
+    case 222: return launch_nb<K, R, 1, kNB, 4, 4, 2, true, 0, true, true, K, true>(e, st);
     default: break;
   }
   return hipErrorInvalidValue;

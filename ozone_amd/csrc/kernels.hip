@@ -1068,9 +1068,11 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
   return (aligned16(a.len) && vec_ok(a)) || encode_crc_nb_bytes_supported(a, bpc);
 }
 
-bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin) {
-  if (!aligned16(a.len) || !vec_ok(a)) return true;  // byte-granular: the unfused kernels take their byte paths
-  return a.nstripes * nwin >= g_tune.fused_min_units.load(std::memory_order_relaxed);
+bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin, int64_t min_units) {
+  // units at unaligned offsets: the unfused kernels would take their byte paths (7-8x slower, profiles/r05/small/).
+  // An odd length on 16-B aligned units (a host batch's device pitch) keeps their vector paths, byte tail aside.
+  if (!vec_ok(a)) return true;
+  return a.nstripes * nwin >= min_units;
 }
 
 hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {

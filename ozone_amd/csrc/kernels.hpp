@@ -165,12 +165,15 @@ struct TuneKnobs {
                                         // lost in both A/Bs -- JNI 1 MiB cells 263-294 -> 317-343 us at 1 thread,
                                         // 492-501 -> 774-779 us at 4; pinned batches 28.1-29.6 -> 23.4-23.5 GB/s,
                                         // profiles/r05/duplex/)
-  std::atomic<int64_t> fused_min_units{5120};  // fused encode + CRC batches of 16-B cells with fewer (stripe, window)
-                                               // units take the unfused kernels (coding, then one CRC pass), which
-                                               // spread a small batch over many more waves: one rs-6-3 stripe of
-                                               // 1 MiB cells 15 us instead of 164 us, 64 stripes 228 vs 262 us, 128
-                                               // stripes 410 vs 308 us (scripts/small_batch_ab.py,
+  std::atomic<int64_t> fused_min_units{5120};  // fused encode + CRC batches on 16-B aligned units with fewer
+                                               // (stripe, window) units take the unfused kernels (coding, then one
+                                               // CRC pass), which spread a small batch over many more waves: one
+                                               // rs-6-3 stripe of 1 MiB cells 15 us instead of 160 us, 64 stripes
+                                               // 227 vs 262 us, 128 stripes 402 vs 310 us (scripts/small_batch_ab.py,
                                                // profiles/r05/small/; 0: always fused)
+  std::atomic<int64_t> rec_min_units{0};  // the same for fused reconstructions (verify + decode + CRC; 0: always fused)
+  std::atomic<int64_t> nb_small_units{0};  // fused batches of fewer units take the small-batch nibble geometry
+                                           // (variants 220-222: workgroups of 1-4 waves) when no variant is pinned
 };
 
 // Kernel alternates the library holds besides the defaults, selectable with ozec_set_tuning for A/B (0 = default).
@@ -183,10 +186,11 @@ struct TuneKnobs {
 //       (the round-1 default), 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps
 //     fused RS (launch_encode_crc): 49 per-window kernel, 56 / 59 streamed-input kernel (fused.hip), 62 / 87 / 150 /
-//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 nibble-table kernel (fused_nb.hpp launch_nb_kr)
+//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 / 220-222 nibble-table kernel (fused_nb.hpp
+//       launch_nb_kr)
 constexpr int kGfVariants[] = {1, 5, 11};
-constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  49,  56,  59,  62,  87,  150, 163, 167, 170,
-                                 171, 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196};
+constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  49,  56,  59,  62,  87,  150, 163, 167, 170, 171,
+                                 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196, 220, 221, 222};
 
 extern TuneKnobs g_tune;
 
@@ -212,8 +216,9 @@ hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t nc
                                   uint64_t first_stream, hipStream_t stream);
 // true when the fused kernel supports this (k, rows) pair with the given geometry
 bool encode_crc_supported(const CodeArgs &a, int64_t bpc);
-// whether a supported fused batch should run fused (TuneKnobs::fused_min_units; byte-granular layouts always do)
-bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin);
+// whether a supported fused batch of nwin windows per stripe should run fused: at least min_units (stripe, window)
+// units (TuneKnobs::fused_min_units / rec_min_units); units at unaligned offsets always do
+bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin, int64_t min_units);
 // the streamed-input fused kernel (fused.hip): RS shapes with full windows, bpc % 4096 == 0; `e` already rebased
 bool encode_crc_lv_supported(const EncCrcArgs &e);
 // the nibble-table kernel (fused_nb.hpp): the same shapes, and a short last window of any whole number of 16-B blocks

@@ -1,7 +1,10 @@
-"""Per-call time of small fused encode + CRC32C batches of 16-B cells, fused kernel vs unfused kernels (TuneKnobs
-fused_min_units), device-resident and from pinned host memory, interleaved in one process: where the
-fused_min_units default comes from.  (Byte-granular cells always run fused: their unfused kernels take byte paths,
-7-8x slower in the first run of this script, profiles/r05/small/.)
+"""Per-call time of small fused batches: the fused nibble kernel's default geometry, its small-batch geometries
+(variants 220-222: workgroups of 1 / 2 / 4 waves) and the unfused kernels (TuneKnobs fused_min_units /
+rec_min_units), interleaved in one process with outputs checked bit-exact across the routes first.  Encode + CRC32C
+of rs-6-3 stripes (device-resident and from pinned host memory) and verify + decode + CRC of rs-10-4 / rs-6-3
+reconstructions (device-resident): where the fused_min_units / rec_min_units / nb_small_units defaults come from.
+(Units at unaligned offsets always run fused: their unfused kernels take byte paths, 7-8x slower in the first run of
+this script, profiles/r05/small/small_batch_ab_first.json.)
 usage: python scripts/small_batch_ab.py [ROUNDS]"""
 import json
 import os
@@ -20,12 +23,23 @@ from ozone_amd.stripe_queue import host_alloc  # noqa: E402
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 lib = L.lib()
 torch.cuda.set_device(0)
-k, p, bpc = 6, 3, 16384
-enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
-MODES = {"fused": 0, "unfused": 1 << 40}
+bpc = 16384
+BIG = 1 << 40
+DEFAULTS = {b"crc_variant": 0, b"fused_min_units": 5120, b"rec_min_units": 0, b"nb_small_units": 0}
+MODES = [("fused", {b"fused_min_units": 0, b"rec_min_units": 0}),
+         ("nb220", {b"crc_variant": 220, b"fused_min_units": 0, b"rec_min_units": 0}),
+         ("nb221", {b"crc_variant": 221, b"fused_min_units": 0, b"rec_min_units": 0}),
+         ("nb222", {b"crc_variant": 222, b"fused_min_units": 0, b"rec_min_units": 0}),
+         ("unfused", {b"fused_min_units": BIG, b"rec_min_units": BIG})]
 
 
-def dev_case(S, n):
+def apply(settings):
+    for key, v in {**DEFAULTS, **settings}.items():
+        assert lib.ozec_set_tuning(key, v) == 0, key
+
+
+def enc_dev(S, n, k=6, p=3):
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
     nwin = -(-n // bpc)
     units = torch.randint(0, 256, (S, k + p, n), dtype=torch.uint8, device="cuda")
     crcs = torch.empty((S, k + p, nwin), dtype=torch.int32, device="cuda")
@@ -36,7 +50,26 @@ def dev_case(S, n):
     return call, lambda: (units[:, k:].clone(), crcs.clone())
 
 
-def host_case(S, n):
+def rec_dev(S, n, k, p, erased):
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+    dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
+    nwin = -(-n // bpc)
+    units = torch.randint(0, 256, (S, k + p, n), dtype=torch.uint8, device="cuda")
+    stored = torch.empty((S, k + p, nwin), dtype=torch.int32, device="cuda")
+    enc.encode_crc_batch(units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n, ck.ChecksumType.CRC32C, bpc, stored)
+    present = [u for u in range(k + p) if u not in erased]
+    out = torch.empty((S, len(erased), n), dtype=torch.uint8, device="cuda")
+    ocrc = torch.empty((S, len(erased), nwin), dtype=torch.int32, device="cuda")
+    mism = torch.empty(S, dtype=torch.int32, device="cuda")
+
+    def call():
+        dec.reconstruct_crc_batch(units, (k + p) * n, n, present, erased, out, len(erased) * n, n, S, n,
+                                  ck.ChecksumType.CRC32C, bpc, ocrc, d_expected=stored, d_mismatch=mism)
+    return call, lambda: (out.clone(), ocrc.clone(), mism.clone())
+
+
+def enc_host(S, n, k=6, p=3):
+    enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
     nwin = -(-n // bpc)
     pb = host_alloc(S * (k + p) * n + S * (k + p) * nwin * 4)
     a = pb.array
@@ -47,7 +80,7 @@ def host_case(S, n):
         enc.encode_crc_host_batch(a.ctypes.data, (k + p) * n, n, a.ctypes.data + k * n, (k + p) * n, n, S, n,
                                   ck.ChecksumType.CRC32C, bpc, crc)
     call.keep = pb  # the pinned buffer lives as long as the call that uses it
-    return call, None
+    return call, lambda: (torch.from_numpy(a.copy()),)
 
 
 def timed(call, reps):
@@ -59,31 +92,35 @@ def timed(call, reps):
     return (time.perf_counter() - t0) / reps * 1e6
 
 
-for where, make in (("device", dev_case), ("host_pinned", host_case)):
-    for n in (1 << 20, 700_000, 65536):
-        for S in (1, 2, 4, 8, 16, 32, 64, 128):
-            if where == "host_pinned" and S > 32:
-                continue
-            call, snap = make(S, n)
-            ref = None
-            for m, v in MODES.items():  # bit-exact across the two routes before timing
-                lib.ozec_set_tuning(b"fused_min_units", v)
-                call()
-                torch.cuda.synchronize()
-                if snap:
-                    got = snap()
-                    ref = ref or got
-                    assert all(torch.equal(x, y) for x, y in zip(ref, got)), (where, n, S, m)
-            reps = max(5, min(200, int(2e5 / (S * n / 1e3 + 50))))
-            res = {m: [] for m in MODES}
-            for _ in range(rounds):
-                for m, v in MODES.items():
-                    lib.ozec_set_tuning(b"fused_min_units", v)
-                    call()
-                    res[m].append(timed(call, reps))
-            row = {"where": where, "cell_bytes": n, "stripes": S, "units": S * -(-n // bpc)}
-            for m in MODES:
-                row[f"{m}_us"] = round(float(np.median(res[m])), 1)
-            row["unfused_over_fused"] = round(row["unfused_us"] / row["fused_us"], 3)
-            print(json.dumps(row), flush=True)
-lib.ozec_set_tuning(b"fused_min_units", 5120)
+CASES = [("encode rs-6-3 device", n, S, lambda S, n: enc_dev(S, n)) for n in (1 << 20, 65536)
+         for S in (1, 2, 4, 8, 16, 32, 64, 128, 256)]
+CASES += [(f"reconstruct rs-10-4 {{0,1,2,3}} device", 1 << 20, S, lambda S, n: rec_dev(S, n, 10, 4, [0, 1, 2, 3]))
+          for S in (1, 2, 4, 8, 16, 32, 64, 128)]
+CASES += [(f"reconstruct rs-6-3 {{1}} device", 1 << 20, S, lambda S, n: rec_dev(S, n, 6, 3, [1]))
+          for S in (1, 4, 16, 64, 128)]
+CASES += [("encode rs-6-3 host pinned", 1 << 20, S, lambda S, n: enc_host(S, n)) for S in (1, 4, 16)]
+
+for what, n, S, make in CASES:
+    call, snap = make(S, n)
+    ref = None
+    for name, st in MODES:  # bit-exact across the routes before timing
+        apply(st)
+        call()
+        torch.cuda.synchronize()
+        got = snap()
+        ref = ref or got
+        assert all(torch.equal(x, y) for x, y in zip(ref, got)), (what, n, S, name)
+    reps = max(5, min(200, int(2e5 / (S * n / 1e3 + 50))))
+    res = {name: [] for name, _ in MODES}
+    for _ in range(rounds):
+        for name, st in MODES:
+            apply(st)
+            call()
+            res[name].append(timed(call, reps))
+    row = {"case": what, "cell_bytes": n, "stripes": S, "units": S * -(-n // bpc)}
+    for name, _ in MODES:
+        row[f"{name}_us"] = round(float(np.median(res[name])), 1)
+    row["best"] = min((row[f"{name}_us"], name) for name, _ in MODES)[1]
+    print(json.dumps(row), flush=True)
+    del call, snap
+apply({})

@@ -305,7 +305,9 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v, bool
   // 0.5-1.3 % faster than 170 in three same-process A/Bs, profiles/r03/h/)
   WorkSlot *ws = e.code.nstripes * e.crc.nwin <= (int64_t{1} << 30) ? work_lease(st) : nullptr;
   if (tail && !nb_variant_tail(v)) v = 0;  // byte-granular cells: the TAIL instantiations of the EM variants
-  if (v == 0 && e.code.nstripes * e.crc.nwin < g_tune.nb_small_units.load(std::memory_order_relaxed)) v = 221;
+  // a small batch: workgroups of 4 waves spread its units over many CUs (the 16-wave persistent workgroups put them on
+  // a few, whose LDS pipes then serve all their waves; kernels.hpp TuneKnobs::nb_small_units)
+  if (v == 0 && e.code.nstripes * e.crc.nwin < g_tune.nb_small_units.load(std::memory_order_relaxed)) v = 222;
   if (v == 0) v = k == 10 ? (ws ? 177 : 173) : !ws ? 174 : k == 6 ? 171 : 172;
   const bool used = ws && nb_variant_persistent(v);
   EncCrcArgs ed = e;

@@ -165,15 +165,19 @@ struct TuneKnobs {
                                         // lost in both A/Bs -- JNI 1 MiB cells 263-294 -> 317-343 us at 1 thread,
                                         // 492-501 -> 774-779 us at 4; pinned batches 28.1-29.6 -> 23.4-23.5 GB/s,
                                         // profiles/r05/duplex/)
-  std::atomic<int64_t> fused_min_units{5120};  // fused encode + CRC batches on 16-B aligned units with fewer
+  // Small fused batches (scripts/small_batch_ab.py, profiles/r05/small/: rs-6-3 encode + CRC32C of 1 MiB cells, us per
+  // call for the persistent default / the 4-wave geometry 222 / the unfused kernels):
+  //   1 stripe 161 / 57 / 14, 16 stripes 145 / 61 / 65, 128 stripes 306 / 235 / 424, 256 stripes 513 / 487 / 808;
+  //   full C3r / C5dev size (2048 / 4096 stripes) 222 is 8 % slower than the default.  rs-10-4 reconstruction of 4
+  //   units: 1 stripe 241 / 91 / 95, 64 stripes 366 / 226 / 400.
+  std::atomic<int64_t> fused_min_units{1024};  // fused encode + CRC batches on 16-B aligned units with fewer
                                                // (stripe, window) units take the unfused kernels (coding, then one
-                                               // CRC pass), which spread a small batch over many more waves: one
-                                               // rs-6-3 stripe of 1 MiB cells 15 us instead of 160 us, 64 stripes
-                                               // 227 vs 262 us, 128 stripes 402 vs 310 us (scripts/small_batch_ab.py,
-                                               // profiles/r05/small/; 0: always fused)
-  std::atomic<int64_t> rec_min_units{0};  // the same for fused reconstructions (verify + decode + CRC; 0: always fused)
-  std::atomic<int64_t> nb_small_units{0};  // fused batches of fewer units take the small-batch nibble geometry
-                                           // (variants 220-222: workgroups of 1-4 waves) when no variant is pinned
+                                               // CRC pass), which spread a small batch over many more waves (0: always
+                                               // fused)
+  std::atomic<int64_t> rec_min_units{0};       // the same for fused reconstructions (verify + decode + CRC): 0, the
+                                               // 4-wave geometry is never slower than their k + 2 unfused launches
+  std::atomic<int64_t> nb_small_units{16384};  // fused batches of fewer units take the 4-wave nibble geometry (variant
+                                               // 222) when no variant is pinned (0: off)
 };
 
 // Kernel alternates the library holds besides the defaults, selectable with ozec_set_tuning for A/B (0 = default).

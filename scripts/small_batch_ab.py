@@ -25,8 +25,8 @@ lib = L.lib()
 torch.cuda.set_device(0)
 bpc = 16384
 BIG = 1 << 40
-DEFAULTS = {b"crc_variant": 0, b"fused_min_units": 5120, b"rec_min_units": 0, b"nb_small_units": 0}
-MODES = [("fused", {b"fused_min_units": 0, b"rec_min_units": 0}),
+DEFAULTS = {b"crc_variant": 0, b"fused_min_units": 1024, b"rec_min_units": 0, b"nb_small_units": 16384}
+MODES = [("fused", {b"fused_min_units": 0, b"rec_min_units": 0, b"nb_small_units": 0}),
          ("nb220", {b"crc_variant": 220, b"fused_min_units": 0, b"rec_min_units": 0}),
          ("nb221", {b"crc_variant": 221, b"fused_min_units": 0, b"rec_min_units": 0}),
          ("nb222", {b"crc_variant": 222, b"fused_min_units": 0, b"rec_min_units": 0}),

@@ -44,4 +44,4 @@ def _fused_kernels_in_gpu_tests(request):
     try:
         yield
     finally:
-        lib.ozec_set_tuning(b"fused_min_units", 5120)
+        lib.ozec_set_tuning(b"fused_min_units", 1024)

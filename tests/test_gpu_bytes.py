@@ -102,4 +102,4 @@ def test_fused_min_units_routes_small_batches_unfused(k, p, n):
             assert lib.ozec_set_tuning(b"fused_min_units", m) == 0
             _packed_case(k, p, n, 2, 16384, ck.ChecksumType.CRC32C, 0, [k, n])
     finally:
-        lib.ozec_set_tuning(b"fused_min_units", 5120)
+        lib.ozec_set_tuning(b"fused_min_units", 1024)

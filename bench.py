@@ -1274,6 +1274,28 @@ def tail_rows(args, lens=(1007, 1008, 50000, 50001, 700000, 700001), seconds=0.4
                              "frac_hbm": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                              "path": "fused (nibble kernel" + (f", last {n % 16} B per unit in nb_tail)" if n % 16
                                                               else ")")})
+            if layout == "packed":
+                # the same packed stripes through the coding-only and checksum-only entry points (units at odd
+                # offsets when n is odd: gf_code_vec through buffer descriptors and crc_windows_g26 with align-1 loads
+                # since round 5; gf_code_bytes / crc_windows_bytes before)
+                def ms_of(fn):
+                    for _ in range(2):
+                        fn()
+                    e0.record(st)
+                    for _ in range(reps):
+                        fn()
+                    e1.record(st)
+                    torch.cuda.synchronize()
+                    return e0.elapsed_time(e1) / reps
+                ms_code = ms_of(lambda: enc.encode_batch(units, (k + p) * us_, us_, units[:, k:], (k + p) * us_, us_,
+                                                         S, n))
+                ms_crc = ms_of(lambda: ck.checksum_windows_batch(ck.ChecksumType.CRC32C, units, us_, S * (k + p), n,
+                                                                 bpc, crcs))
+                dev_rows[-1]["encode_only_ms"] = round(ms_code, 4)
+                dev_rows[-1]["encode_only_frac_hbm"] = round(S * (k + p) * n / (ms_code * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+                dev_rows[-1]["checksum_only_ms"] = round(ms_crc, 4)
+                dev_rows[-1]["checksum_only_frac_hbm"] = round(S * (k + p) * (n + nwin * 4) / (ms_crc * 1e-3) / 1e9 /
+                                                               PEAK_HBM_GBS, 4)
             del units, crcs
             torch.cuda.empty_cache()
     out["fused_host_one_stripe_per_call"] = host

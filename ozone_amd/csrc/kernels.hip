@@ -255,7 +255,9 @@ __global__ __launch_bounds__(kBlock) void gf_code_bytes(const CodeArgs a, int64_
 // into its register through the table set of the block's distance to the group end (no per-step register
 // shift): S = shift_group(S) ^ XOR_{steps r, blocks s} G26[r*B+s](block).  Windows are front-padded with
 // virtual zero blocks to whole groups; virtual blocks are not loaded and add nothing.
-template <int B, int D, int PD = 1>
+// UA (round 5): cells at any byte offset -- 16-B loads through an align-1 copy (global_load_dwordx4 at the unaligned
+// address, which gfx950 serves at full rate, profiles/r05/unaligned/) instead of the aligned non-temporal load.
+template <int B, int D, int PD = 1, bool UA = false>
 __global__ __launch_bounds__(kBlock) void crc_windows_g26(const CrcArgs a) {
   constexpr int E = B * D;
   static_assert(D % 2 == 0, "two register sets alternate across steps");
@@ -283,8 +285,12 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26(const CrcArgs a) {
       for (int q = 0; q < B; ++q) {
         const int64_t vb = t * 64 * B + lane * B + q - P;
         if (!pad || vb >= 0) {
-          const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(win + vb * 16));
-          dst[q] = make_uint4(d[0], d[1], d[2], d[3]);
+          if constexpr (UA) {
+            __builtin_memcpy(&dst[q], win + vb * 16, 16);
+          } else {
+            const u32x4 d = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(win + vb * 16));
+            dst[q] = make_uint4(d[0], d[1], d[2], d[3]);
+          }
         } else {
           dst[q] = make_uint4(0, 0, 0, 0);
         }
@@ -897,12 +903,22 @@ hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
   return hipSuccess;
 }
 
+// the instantiated gf_code_vec shapes read and write through raw buffer descriptors, which take any byte offset
+// (round 5: a packed batch of odd-length cells ran gf_code_bytes at ~5 GB/s, profiles/r05/small/)
+bool kr_any_offset(const CodeArgs &a) {
+  if (a.all_ones && a.rows == 1) return false;  // xor_vec: typed 16-B accesses
+  const bool kr = (a.k == 3 && a.rows >= 1 && a.rows <= 2) || (a.k == 6 && a.rows >= 1 && a.rows <= 3) ||
+                  (a.k == 10 && a.rows >= 1 && a.rows <= 4);
+  CodeArgs rb = a;
+  return kr && rebase32(rb);
+}
+
 }  // namespace
 
 hipError_t launch_code(const CodeArgs &a, hipStream_t st) {
   if (a.len <= 0 || a.nstripes <= 0) return hipSuccess;
   int64_t start = 0;
-  if (vec_ok(a) && a.len >= 16) {
+  if ((vec_ok(a) || kr_any_offset(a)) && a.len >= 16) {
     hipError_t err = launch_vec(a, st);
     if (err != hipSuccess) return err;
     start = a.len & ~static_cast<int64_t>(15);
@@ -989,6 +1005,13 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
     const int64_t g = cg > 0 ? cg : 16384;
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
     hipLaunchKernelGGL((crc_windows_g26<1, 4, 2>), grid, block, 0, st, a);
+  } else if (aligned16(a.bpc)) {
+    // cells at unaligned offsets (a packed batch of odd-length cells): the per-window kernel with align-1 loads.  The
+    // byte-at-a-time kernel below ran 16 KiB windows one thread each
+    const int64_t cg = g_tune.crc_grid;
+    const int64_t g = cg > 0 ? cg : 16384;
+    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
+    hipLaunchKernelGGL((crc_windows_g26<1, 4, 2, true>), grid, block, 0, st, a);
   } else {
     hipLaunchKernelGGL(crc_windows_bytes, dim3(grid_for(units, kBlock)), dim3(kBlock), 0, st, a);
   }

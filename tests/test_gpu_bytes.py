@@ -103,3 +103,35 @@ def test_fused_min_units_routes_small_batches_unfused(k, p, n):
             _packed_case(k, p, n, 2, 16384, ck.ChecksumType.CRC32C, 0, [k, n])
     finally:
         lib.ozec_set_tuning(b"fused_min_units", 1024)
+
+
+@pytest.mark.parametrize("k,p,n", [(6, 3, 700_001), (10, 4, 16384 + 3), (3, 2, 1007), (6, 2, 50_001)])
+def test_packed_odd_cells_coding_and_checksum_entry_points(k, p, n):
+    """The coding-only and checksum-only device entry points on the same packed odd-offset stripes (ozec_encode_batch:
+    gf_code_vec through buffer descriptors at any byte offset; ozec_checksum_windows_batch: crc_windows_g26 with
+    align-1 loads), vs the oracle, guard bytes untouched."""
+    S, bpc = 3, 16384
+    rng = np.random.default_rng([k, p, n, 7])
+    data = rng.integers(0, 256, (S, k, n), dtype=np.uint8)
+    shift = 5
+    flat = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
+    body = flat[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
+    body[:, :k] = data
+    d = torch.from_numpy(flat).to(DEV)
+    base = d[GUARD + shift:]
+    rc.RawErasureEncoder(rc.ECReplicationConfig(k, p)).encode_batch(base, (k + p) * n, n, base[k * n:], (k + p) * n,
+                                                                     n, S, n)
+    nwin = -(-n // bpc)
+    crcs = torch.zeros((S * (k + p), nwin), dtype=torch.int32, device=DEV)
+    ck.checksum_windows_batch(ck.ChecksumType.CRC32C, base, n, S * (k + p), n, bpc, crcs)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    c = crcs.cpu().numpy().view(np.uint32).reshape(S, k + p, nwin)
+    assert (got[:GUARD + shift] == 0xA5).all() and (got[GUARD + shift + S * (k + p) * n:] == 0xA5).all()
+    units = got[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
+    for s in range(S):
+        ref = oracle.rs_encode(k, p, list(data[s]))
+        for q in range(p):
+            assert (units[s, k + q] == ref[q]).all(), (k, p, n, s, q)
+        for u, cell in enumerate(list(data[s]) + ref):
+            assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (k, p, n, s, u)

@@ -1241,7 +1241,7 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
   // buffer is 16-B aligned and the kernels take their vector paths whatever the length (a key's last, partial stripe:
   // ECKeyOutputStream.java:276).  An odd pitch sent a 700,001-B stripe through the byte-wise kernels: 6.0 ms instead
   // of 0.31 ms per stripe (bench.py --workload tail, round 5)
-  const size_t dunit = round_up(len, 16);
+  const size_t dunit = ozec::g_tune.host_pitch16.load(std::memory_order_relaxed) ? round_up(len, 16) : len;
   const size_t dstripe = static_cast<size_t>(k + p) * dunit;
   const size_t dcrc_off = round_up(C * dstripe, kStageAlign);            // then crcs [C][units][nwin]
   const size_t dbytes = dcrc_off + C * units * nwin * sizeof(uint32_t);
@@ -1591,7 +1591,8 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
   const size_t nwin = (len + bpc - 1) / bpc;
   // device layout of one chunk buffer: input slots [C][k+p][len], rebuilt [C][e][len], expected CRCs [C][k+p][nwin],
   // rebuilt CRCs [C][e][nwin], mismatch [C]
-  const size_t dunit = round_up(len, 16);  // 16-B aligned unit pitch, as in encode_crc_host_batch_dev
+  // 16-B aligned unit pitch, as in encode_crc_host_batch_dev
+  const size_t dunit = ozec::g_tune.host_pitch16.load(std::memory_order_relaxed) ? round_up(len, 16) : len;
   const size_t dstripe = static_cast<size_t>(n_all) * dunit, ostripe = static_cast<size_t>(e) * dunit;
   const size_t dout_off = round_up(C * dstripe, kStageAlign);
   const size_t dexp_off = round_up(dout_off + C * ostripe, kStageAlign);
@@ -1994,6 +1995,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "host_duplex") {
     if (value < 0) return bad();
     t.host_duplex.store(value);
+  } else if (k == "host_pitch16") {
+    if (value != 0 && value != 1) return bad();
+    t.host_pitch16.store(static_cast<int>(value));
   } else if (k == "fused_min_units" || k == "rec_min_units" || k == "nb_small_units") {
     if (value < 0) return bad();
     auto &knob = k == "fused_min_units" ? t.fused_min_units : k == "rec_min_units" ? t.rec_min_units : t.nb_small_units;

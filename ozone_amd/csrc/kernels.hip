@@ -1092,9 +1092,9 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
 }
 
 bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin, int64_t min_units) {
-  // units at unaligned offsets: the unfused kernels would take their byte paths (7-8x slower, profiles/r05/small/).
-  // An odd length on 16-B aligned units (a host batch's device pitch) keeps their vector paths, byte tail aside.
-  if (!vec_ok(a)) return true;
+  // units at unaligned offsets: the unfused kernels of the nibble shapes take them at full rate too since round 5
+  // (gf_code_vec through buffer descriptors, crc_windows_g26 with align-1 loads; before, their byte paths ran 7-8x
+  // slower, profiles/r05/small/small_batch_ab_first.json)
   return a.nstripes * nwin >= min_units;
 }
 

@@ -165,6 +165,7 @@ struct TuneKnobs {
                                         // lost in both A/Bs -- JNI 1 MiB cells 263-294 -> 317-343 us at 1 thread,
                                         // 492-501 -> 774-779 us at 4; pinned batches 28.1-29.6 -> 23.4-23.5 GB/s,
                                         // profiles/r05/duplex/)
+  std::atomic<int> host_pitch16{1};  // host batches: device unit pitch = cell length rounded up to 16 B (0: the length)
   // Small fused batches (scripts/small_batch_ab.py, profiles/r05/small/: rs-6-3 encode + CRC32C of 1 MiB cells, us per
   // call for the persistent default / the 4-wave geometry 222 / the unfused kernels):
   //   1 stripe 161 / 57 / 14, 16 stripes 145 / 61 / 65, 128 stripes 306 / 235 / 424, 256 stripes 513 / 487 / 808;

@@ -74,6 +74,9 @@ for s in $STEPS; do
         2> "$OUT/small_batch_ab.err" || { tail -20 "$OUT/small_batch_ab.err"; exit 20; } ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
+    tailnp)  # the same with the host batches' device unit pitch = the cell length (host_pitch16=0)
+      run "tail pitch=len" 300 python -u bench.py --workload tail --tune host_pitch16=0 > "$OUT/bench_tail_np.json" \
+        2> "$OUT/bench_tail_np.err" || exit 21 ;;
     heap)
       for n in 65536 262144; do
         run "probe heap $n" 150 env AMD_LOG_LEVEL=4 python -u scripts/fault_probe.py heap $n \

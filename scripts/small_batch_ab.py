@@ -94,6 +94,7 @@ def timed(call, reps):
 
 CASES = [("encode rs-6-3 device", n, S, lambda S, n: enc_dev(S, n)) for n in (1 << 20, 65536)
          for S in (1, 2, 4, 8, 16, 32, 64, 128, 256)]
+CASES += [("encode rs-6-3 device packed", 700_001, S, lambda S, n: enc_dev(S, n)) for S in (1, 8, 64)]
 CASES += [(f"reconstruct rs-10-4 {{0,1,2,3}} device", 1 << 20, S, lambda S, n: rec_dev(S, n, 10, 4, [0, 1, 2, 3]))
           for S in (1, 2, 4, 8, 16, 32, 64, 128)]
 CASES += [(f"reconstruct rs-6-3 {{1}} device", 1 << 20, S, lambda S, n: rec_dev(S, n, 6, 3, [1]))

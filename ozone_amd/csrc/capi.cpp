@@ -1237,10 +1237,12 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
   const size_t C = std::min(num_stripes, stripes_per_chunk ? stripes_per_chunk
                                                           : static_cast<size_t>(std::max<int64_t>(1, ozec::g_tune.e2e_chunk.load())));
   const size_t nwin = with_crc ? (len + bpc - 1) / bpc : 0;
-  // device layout [C][k+p][dunit]: the unit pitch is the cell length rounded up to 16 B, so every unit of the chunk
-  // buffer is 16-B aligned and the kernels take their vector paths whatever the length (a key's last, partial stripe:
-  // ECKeyOutputStream.java:276).  An odd pitch sent a 700,001-B stripe through the byte-wise kernels: 6.0 ms instead
-  // of 0.31 ms per stripe (bench.py --workload tail, round 5)
+  // device layout [C][k+p][dunit]: the unit pitch is the cell length (a key's last, partial stripe has any length,
+  // ECKeyOutputStream.java:276).  Early in round 5 an odd pitch sent a 700,001-B stripe through the byte-wise kernels
+  // (6.0 ms instead of 0.31 ms), so the pitch was rounded up to 16 B at the cost of a 2D copy per stripe; since the
+  // kernels take units at any byte offset at full rate (fused_nb.hpp nb_tail, gf_code_vec through buffer
+  // descriptors, crc_windows_g26 UA), the plain pitch is faster again: 190 us against 245 us for that stripe
+  // (TuneKnobs::host_pitch16 = 1 restores the rounded pitch)
   const size_t dunit = ozec::g_tune.host_pitch16.load(std::memory_order_relaxed) ? round_up(len, 16) : len;
   const size_t dstripe = static_cast<size_t>(k + p) * dunit;
   const size_t dcrc_off = round_up(C * dstripe, kStageAlign);            // then crcs [C][units][nwin]

@@ -165,7 +165,10 @@ struct TuneKnobs {
                                         // lost in both A/Bs -- JNI 1 MiB cells 263-294 -> 317-343 us at 1 thread,
                                         // 492-501 -> 774-779 us at 4; pinned batches 28.1-29.6 -> 23.4-23.5 GB/s,
                                         // profiles/r05/duplex/)
-  std::atomic<int> host_pitch16{1};  // host batches: device unit pitch = cell length rounded up to 16 B (0: the length)
+  std::atomic<int> host_pitch16{0};  // host batches: device unit pitch = the cell length (0, default) or the length
+                                     // rounded up to 16 B (1: every unit 16-B aligned, at the cost of a 2D copy per
+                                     // stripe each way; one rs-6-3 stripe of 700,001-B cells 245 -> 190 us, of
+                                     // 1,007-B cells 117 -> 68 us with 0, profiles/r05/bytes/)
   // Small fused batches (scripts/small_batch_ab.py, profiles/r05/small/: rs-6-3 encode + CRC32C of 1 MiB cells, us per
   // call for the persistent default / the 4-wave geometry 222 / the unfused kernels):
   //   1 stripe 161 / 57 / 14, 16 stripes 145 / 61 / 65, 128 stripes 306 / 235 / 424, 256 stripes 513 / 487 / 808;

@@ -434,11 +434,22 @@ def test_device_list_errors_and_default(device_list):
 
 @pytest.mark.parametrize("n", [1007, 50001, 700001])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_host_batches_of_odd_cells_vs_oracle(n, pinned):
+@pytest.mark.parametrize("pitch16", [0, 1])
+def test_host_batches_of_odd_cells_vs_oracle(n, pinned, pitch16):
     """A key's last, partial stripe has cells of any length (parityCellSize = dataBuffers[0].position(),
-    ECKeyOutputStream.java:276).  The host batches lay such cells out on a 16-B aligned unit pitch on the device
-    (capi.cpp dunit), so the kernels keep their vector paths; contiguous odd cells (unit stride = length, the
-    rectangular per-stripe copies) and a gapped layout, encode + CRC32C and the fused reconstruction, vs the oracle."""
+    ECKeyOutputStream.java:276).  The host batches lay such cells out on the device at a unit pitch of the length
+    (units at odd offsets: the kernels take any byte offset) or, with host_pitch16 = 1, of the length rounded up to
+    16 B (capi.cpp dunit); contiguous odd cells (unit stride = length) and a gapped layout, encode + CRC32C and the
+    fused reconstruction, vs the oracle."""
+    lib = L.lib()
+    assert lib.ozec_set_tuning(b"host_pitch16", pitch16) == 0
+    try:
+        _odd_host_batches(n, pinned)
+    finally:
+        lib.ozec_set_tuning(b"host_pitch16", 0)
+
+
+def _odd_host_batches(n, pinned):
     k, p, S, bpc = 6, 3, 5, 16384
     for gap in (0, 3):
         buf, v, us = _batch(S, k, p, n, 4100 + n % 97 + gap, gap)

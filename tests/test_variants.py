@@ -63,7 +63,7 @@ def test_listed_variants_accepted_and_reset():
                                           (b"queue_batches", 65, 0), (b"crc_grid", -1, 0), (b"host_graph", -1, 256 << 10),
                                           (b"host_duplex", -1, 0), (b"fused_min_units", -1, 1024),
                                           (b"rec_min_units", -1, 0), (b"nb_small_units", -1, 16384),
-                                          (b"host_pitch16", 2, 1)])
+                                          (b"host_pitch16", 2, 0)])
 def test_knob_ranges(key, bad, good):
     lib = L.lib()
     assert lib.ozec_set_tuning(key, bad) == L.OZEC_EINVAL

@@ -15,6 +15,7 @@ from synth import SEED, cells
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
+from ozone_amd import _lib as L  # noqa: E402
 from ozone_amd import checksum as ck  # noqa: E402
 from ozone_amd import rawcoder as rc  # noqa: E402
 from ozone_amd.shard import stripe_range  # noqa: E402

@@ -1,4 +1,4 @@
-"""Summarise the SQ counter passes of scripts/gpu_final_r4.sh phase c (<dir>/sq_<workload>_p<1|2>/run_counter_collection.csv)
+"""Summarise the SQ counter passes of scripts/gpu_final_r4.sh phase c / scripts/gpu_r5.sh step sq (<dir>/sq_<workload>_p<1|2>/run_counter_collection.csv)
 for each workload's dominant kernel: per-dispatch means and the derived LDS / VALU busy fractions.  The counters of one
 XCD are reported (x8 for the chip): LDS busy per CU = SQ_LDS_IDX_ACTIVE x 8 / (GRBM_GUI_ACTIVE x 256 CUs), VALU issue per
 SIMD = SQ_ACTIVE_INST_VALU x 8 / (GRBM_GUI_ACTIVE x 1024 SIMDs).
@@ -10,7 +10,8 @@ import os
 import sys
 from collections import defaultdict
 
-PAT = {"c3r": "encode_crc_nb", "c5dev": "encode_crc_nb", "c4": "encode_crc_g26", "c2": "gf_code_vec"}
+PAT = {"c3r": "encode_crc_nb", "c5dev": "encode_crc_nb", "c4": "encode_crc_g26", "c2": "gf_code_vec",
+       "c3": "gf_code_vec", "crc": "crc_windows_g26s"}
 root = sys.argv[1]
 out = {}
 for w, pat in PAT.items():

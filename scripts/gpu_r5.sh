@@ -72,6 +72,18 @@ for s in $STEPS; do
     small)  # per-call time of small fused batches: fused kernel vs unfused kernels (fused_min_units)
       run "small batches" 400 python -u scripts/small_batch_ab.py ${ROUNDS:-5} > "$OUT/small_batch_ab.json" \
         2> "$OUT/small_batch_ab.err" || { tail -20 "$OUT/small_batch_ab.err"; exit 20; } ;;
+    sq)  # SQ counters of each leg's dominant kernel, two passes (scripts/final_sq_summary.py writes sq_summary.json)
+      P1="GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAVE_CYCLES"
+      P2="GRBM_GUI_ACTIVE SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+      for wl in ${SQ_WORKLOADS:-c3r c5dev c3 crc c4 c2}; do
+        for p in 1 2; do
+          eval PM=\$P$p
+          run "sq $wl p$p" 120 rocprofv3 --pmc $PM --kernel-trace -d "$OUT/sq_${wl}_p$p" -o run --output-format csv -- \
+            python3 bench.py --workload $wl --steps 3 --warmup 1 --no-cpu --no-pmc --no-e2e --no-legs --no-jni \
+            > "$OUT/sq_${wl}_p$p.log" 2>&1 || { tail -5 "$OUT/sq_${wl}_p$p.log"; exit 22; }
+        done
+      done
+      python3 scripts/final_sq_summary.py "$OUT" > "$OUT/sq_summary.log" 2>&1 || exit 23 ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     tailnp)  # the same with the host batches' device unit pitch = the cell length (host_pitch16=0)

@@ -197,6 +197,7 @@ struct DevCtx {
   uint32_t *g26_tables[2][ozec::kG26Slots] = {};  // [type][kG26Cfg slot]
   uint32_t *nib_tables[2] = {};                   // [type]
   uint32_t *xo_tables[2] = {};                    // [type]
+  uint32_t *cv_tables[2] = {};                    // [type]
 
   int acquire(Slot **out) {
     std::unique_lock<std::mutex> lk(pool_mu);
@@ -268,6 +269,9 @@ int get_ctx(DevCtx **out) {
       const auto &xo = CrcMath::get(static_cast<CrcType>(t)).xo_tables();
       OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->xo_tables[t]), xo.size() * sizeof(uint32_t)));
       OZEC_HIP(hipMemcpy(c->xo_tables[t], xo.data(), xo.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+      const auto &cv = CrcMath::get(static_cast<CrcType>(t)).cv_tables();
+      OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->cv_tables[t]), cv.size() * sizeof(uint32_t)));
+      OZEC_HIP(hipMemcpy(c->cv_tables[t], cv.data(), cv.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     g_ctx[dev] = std::move(c);
   }
@@ -980,6 +984,7 @@ static int make_crc_args(DevCtx *ctx, int checksum_type, const uint8_t *d_base, 
   for (int i = 0; i < ozec::kG26Slots; ++i) a->g26[i] = ctx->g26_tables[static_cast<int>(t)][i];
   a->nib = ctx->nib_tables[static_cast<int>(t)];
   a->xo = ctx->xo_tables[static_cast<int>(t)];
+  a->cv = ctx->cv_tables[static_cast<int>(t)];
   a->init_full = cm.shift(0xffffffffu, bpc);
   a->init_last = cm.shift(0xffffffffu, len - (a->nwin ? (a->nwin - 1) * bpc : 0));
   a->big_endian = big_endian;

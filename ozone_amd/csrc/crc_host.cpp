@@ -101,6 +101,16 @@ CrcMath::CrcMath(uint32_t poly) : poly_(poly) {
   mat_invert(adv, back);
   for (int g = 0; g < 7; ++g)
     for (uint32_t v = 0; v < 32; ++v) xo_[kXoInv + g * 32 + v] = apply(back, static_cast<uint32_t>(uint64_t{v} << (5 * g)));
+  // CV blob: input j's nibble tables and the register shift, both by w_j = j * kCvStride bytes
+  cv_.assign(kCvWords, 0);
+  for (int j = 0; j < kCvMaxK; ++j) {
+    uint32_t wj[32];
+    shift_matrix(static_cast<uint64_t>(j) * kCvStride, wj);
+    for (int i = 0; i < 512; ++i) cv_[j * 512 + i] = apply(wj, nib_[i]);
+    for (int g = 0; g < 7; ++g)
+      for (uint32_t v = 0; v < 32; ++v)
+        cv_[kCvShift + j * 224 + g * 32 + v] = apply(wj, static_cast<uint32_t>(uint64_t{v} << (5 * g)));
+  }
 }
 
 // Block bit (0..127; dword d bit k = 32d + k, i.e. byte p/8 bit p%8) that index bit i of G26 table g reads,

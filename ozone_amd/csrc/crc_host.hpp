@@ -27,6 +27,8 @@ class CrcMath {
   const std::vector<uint32_t> &nib_tables() const { return nib_; }
   // the device XO blob (kernels.hpp kXo*)
   const std::vector<uint32_t> &xo_tables() const { return xo_; }
+  // the device CV blob (kernels.hpp kCv*)
+  const std::vector<uint32_t> &cv_tables() const { return cv_; }
   uint32_t byte_table(int v) const { return t0_[v]; }
   uint32_t poly() const { return poly_; }
   // x^(8n) mod P in CrcUtil's reversed representation (CrcUtil.getMonomial)
@@ -52,6 +54,7 @@ class CrcMath {
   std::vector<uint32_t> g26_[kG26Slots];
   std::vector<uint32_t> nib_;
   std::vector<uint32_t> xo_;
+  std::vector<uint32_t> cv_;
   std::vector<uint32_t> build_blob(int B) const;
   std::vector<uint32_t> build_g26(int B, int D) const;
 };

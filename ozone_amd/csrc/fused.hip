@@ -245,6 +245,32 @@ bool fused_shape(const CodeArgs &a, bool nb) {
 }
 }  // namespace
 
+// After a CV variant (fused_nb.hpp): every stripe whose combined input check failed (mismatch == kMismatchSuspect) is
+// checked again unit by unit, window by window, and gets the reference's first failing (unit, window) -- the rare path,
+// one block per stripe, a bytewise CRC per (input, window) thread; other stripes leave at once.
+__global__ __launch_bounds__(256) void nb_reverify(const EncCrcArgs e) {
+  const CodeArgs &a = e.code;
+  const CrcArgs &cr = e.crc;
+  const int64_t nwin = cr.nwin;
+  const uint32_t *t0 = cr.tables[0] + kG5T0;
+  for (int64_t s = blockIdx.x; s < a.nstripes; s += gridDim.x) {
+    if (cr.mismatch[s] != kMismatchSuspect) continue;
+    for (int64_t t = threadIdx.x; t < a.k * nwin; t += blockDim.x) {
+      const int j = static_cast<int>(t / nwin);
+      const int64_t w = t - j * nwin;
+      const bool last = w == nwin - 1;
+      const int64_t n = last ? a.len - w * cr.bpc : cr.bpc;
+      const uint8_t *p = a.in + in_off(a, s) + a.in_off[j] + w * cr.bpc;
+      uint32_t reg = 0;
+      for (int64_t i = 0; i < n; ++i) reg = (reg >> 8) ^ t0[(reg ^ p[i]) & 0xff];
+      const uint32_t ex0 = cr.expected[(s * e.exp_units + e.in_unit[j]) * nwin + w];
+      const uint32_t ex = cr.expected_be ? __builtin_bswap32(ex0) : ex0;
+      if (crc_finish(reg, last ? cr.init_last : cr.init_full, 0, 0) != ex)
+        atomicMin(cr.mismatch + s, static_cast<int32_t>(e.in_unit[j] * nwin + w));
+    }
+  }
+}
+
 bool encode_crc_lv_supported(const EncCrcArgs &e) {
   return fused_shape(e.code, false) && e.crc.bpc > 0 && e.crc.bpc % 4096 == 0 && e.code.len % e.crc.bpc == 0;
 }
@@ -312,7 +338,12 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v, bool
   const bool used = ws && nb_variant_persistent(v);
   EncCrcArgs ed = e;
   ed.work = used ? ws->ctr : nullptr;
-  const hipError_t err = launch_nb_shape(ed, st, v, tail);
+  hipError_t err = launch_nb_shape(ed, st, v, tail);
+  if (err == hipSuccess && !tail && nb_variant_cv(v) && e.verify && e.crc.expected) {
+    const int64_t g = std::min<int64_t>(e.code.nstripes, 4096);
+    hipLaunchKernelGGL(nb_reverify, dim3(static_cast<unsigned>(g)), dim3(256), 0, st, e);
+    err = hipGetLastError();
+  }
   // the event goes behind the launch whatever `err` says: an event behind a launch that never ran costs nothing, a
   // kernel left running without one would share its counters with the slot's next lease
   if (ws) work_return(ws, st, used);

@@ -142,6 +142,30 @@ __device__ __forceinline__ uint32_t nb_tail(const EncCrcArgs &e, __amdgpu_buffer
   return v;
 }
 
+// CV: the combined check of one window, by the whole wave.  `have` marks the lane holding the combined register's total
+// v (XOR_j x^(8 w_j) raw_j after the lane tree); lanes 0..K-1 turn input j's stored CRC back into its raw register
+// (crc_finish inverted: ~ex ^ init), weight it by x^(8 w_j) (table s_cvs + 224 j) and the 16-lane XOR gives the
+// expected combination.  A difference marks the stripe for nb_reverify.
+template <int K>
+__device__ __forceinline__ void nb_check_combined(const EncCrcArgs &e, const uint32_t *s_cvs, int64_t s, int64_t w,
+                                                  int lane, bool have, uint32_t v, uint32_t init) {
+  const CrcArgs &cr = e.crc;
+  const uint64_t holder = __ballot(have);
+  const uint32_t got = static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(__builtin_ctzll(holder)), 64));
+  uint32_t t = 0;
+  if (lane < K) {
+    int32_t unit = e.in_unit[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) unit = lane == j ? e.in_unit[j] : unit;
+    const uint32_t ex0 = cr.expected[(s * e.exp_units + unit) * cr.nwin + w];
+    const uint32_t ex = cr.expected_be ? __builtin_bswap32(ex0) : ex0;
+    t = g5_shift(s_cvs + lane * 224, ~ex ^ init);
+  }
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) t ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(t), m, 64));
+  if (lane == 0 && got != t) atomicMin(cr.mismatch + s, kMismatchSuspect);
+}
+
 // K inputs, R outputs, D steps per CRC group, NB input ring slots, WPB waves per block, WAVES min waves per SIMD,
 // FENCE: dwords of a block whose lookups go between scheduling fences (2: halves, at most 16 results live; 1:
 // quarters; 4: one fence per input block; 0: no fences, the compiler may overlap inputs); RS: reduce-scatter lane tree;
@@ -155,10 +179,16 @@ __device__ __forceinline__ uint32_t nb_tail(const EncCrcArgs &e, __amdgpu_buffer
 // H (< K, XO with D = 2 only): only inputs 0..H-1 get the second distance set (K + H instead of 2K tables of 4 KiB, so
 // rs-10-x two-step groups fit two workgroups per CU); inputs H..K-1 are looked up in set 0 and shifted by one step
 // after every step (table at kSh1), inputs 0..H-1 by two at the group end
+// TAIL: the last 1-15 bytes of cells of any length (nb_tail)
+// CV (round 5; reconstructions that verify, 16-B cells): the K input registers are ONE, fed by nibble tables whose CRC
+// halves are pre-multiplied by x^(8 w_j) per input (kernels.hpp kCv*), checked against the same combination of the
+// stored CRCs; a failing stripe is marked kMismatchSuspect and re-verified unit by unit (nb_reverify).  Saves the
+// shifts and lane trees of K - 1 registers: for rs-10-4 one shift per step instead of ~7.5 (H = 5, D = 2) and 5
+// registers through the lane tree instead of 14.
 // (Round-3 probes -- output-register groups, VALU / LDS pads, far-addressing without the index OR, late lane-tree
 // tables, guided and static persistent orders -- are measured in DESIGN 2.3 and were taken out of the library.)
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
-          bool EM = false, int H = K, bool TAIL = false>
+          bool EM = false, int H = K, bool TAIL = false, bool CV = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -167,6 +197,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   static_assert(DYN == 0 || DYN == 1, "one wave per unit, or the persistent WorkQueue grid");
   static_assert(H == K || (XO && D == 2 && H >= 0 && H < K), "partial second distance set: XO, two-step groups");
   static_assert(!TAIL || (RS && EM), "byte tails leave through the lane-parallel emit");
+  static_assert(!CV || (D == 1 && XO && EM && RS && H == K && !TAIL && K <= 16), "combined verify: one-step groups");
+  constexpr int kInRegs = CV ? 1 : K;  // input registers
   constexpr int kSets = K + (D - 1) * H;  // (d, j) nibble tables of 4 KiB: all K inputs in set 0, inputs < H in sets >= 1
   // one LDS block: G26 blob of D sets, then the (d, j, p) nibble tables, then the GF dwords of the setup.  Table
   // regions past the 16-bit ds_read offset range are reached with bit 15 set in the index register (one v_or_b32).
@@ -177,13 +209,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   constexpr uint32_t kSh1 = kXoOff + kXoWords;  // H < K: one-step register shift (inputs H..K-1)
   constexpr uint32_t kTW = XO ? kXoOff + kXoWords + (H < K ? 224 : 0) : g26_words(D);
   constexpr uint32_t kTB = (kTW * 4 + 255) / 256 * 256;  // nibble tables
-  constexpr uint32_t kLds = kTB + kSets * 4096 + K * 32 * 4;
+  constexpr uint32_t kLds = kTB + kSets * 4096 + K * 32 * 4 + (CV ? K * 224 * 4 : 0);
   static_assert(kLds <= 160 * 1024, "LDS per workgroup");
   __shared__ __attribute__((aligned(256))) uint8_t s_all[kLds];
   uint32_t *const s_t = reinterpret_cast<uint32_t *>(s_all);
   uint2 *const s_c = reinterpret_cast<uint2 *>(s_all + kTB);
   uint32_t *const s_gf = reinterpret_cast<uint32_t *>(s_all + kTB + kSets * 4096);
   uint32_t *const s_tree = s_t + kTree;  // lane-tree shifts
+  uint32_t *const s_cvs = s_gf + K * 32;  // CV: input j's weight shift (x^(8 w_j)), 7 tables of 32
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
   for (int t = threadIdx.x; t < K * 32; t += blockDim.x) {
@@ -197,6 +230,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     load_tables(s_t, cr.g26[g26_slot(1, D)] + g26_gshift(D), 224 + 1344);
     load_tables(s_t + kXoOff, cr.xo, kXoWords);
     if constexpr (H < K) load_tables(s_t + kSh1, cr.g26[g26_slot(1, 1)] + g26_gshift(1), 224);
+    if constexpr (CV) load_tables(s_cvs, cr.cv + kCvShift, K * 224);
   } else {
     load_tables(s_t, cr.g26[g26_slot(1, D)], g26_words(D));
   }
@@ -204,7 +238,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
   for (int q = threadIdx.x; q < kSets * 512; q += blockDim.x) {
     const int t = q >> 4, n = q & 15, p = t & 31, dj = t >> 5, j = dj % K, d = dj / K;
     const uint32_t off = static_cast<uint32_t>((t >> 1) * 256 + n * 16 + (t & 1) * 8);
-    s_c[off >> 3] = make_uint2(s_gf[j * 32 + (p & 1) * 16 + n], cr.nib[(d * 32 + p) * 16 + n]);
+    s_c[off >> 3] = make_uint2(s_gf[j * 32 + (p & 1) * 16 + n],
+                               CV ? cr.cv[(j * 32 + p) * 16 + n] : cr.nib[(d * 32 + p) * 16 + n]);
   }
   __syncthreads();
 
@@ -282,7 +317,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
           const uint4 x = ring[ii % NB];
           const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
           XorChain ch;
-          ch.push(S[j]);
+          if constexpr (!CV) ch.push(S[j]);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             if (FENCE > 0 && c > 0 && c % (FENCE > 0 ? FENCE : 1) == 0) __builtin_amdgcn_sched_barrier(0);
@@ -303,7 +338,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
               ch.push(hi.y);
             }
           }
-          S[j] = ch.get();
+          if constexpr (CV) S[0] ^= ch.get();  // the lookups' tree first, the running register last
+          else S[j] = ch.get();
           if (FENCE > 0) __builtin_amdgcn_sched_barrier(0);
         }
         // 4x4 byte transposes: A[4c + q] byte r -> output r, dword c, byte q
@@ -344,7 +380,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
       }
       if (g + 1 < Gu) {
 #pragma unroll
-        for (int q = 0; q < (XO ? K : K + R); ++q)
+        for (int q = 0; q < (XO ? kInRegs : K + R); ++q)
           S[q] = g5_shift(s_t + (q < H ? kShIn : q < K ? kSh1 : g26_gshift(D)), S[q]);
       }
     }
@@ -354,7 +390,17 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
       for (int r = 0; r < R; ++r) S[K + r] = g5_shift(s_t + kXoOff + kXoInv, S[K + r]);
     }
-    if constexpr (RS) {
+    if constexpr (CV) {
+      // registers through the tree: the combined input register, then the R outputs
+      uint32_t Sc[1 + R];
+      Sc[0] = S[0];
+#pragma unroll
+      for (int r = 0; r < R; ++r) Sc[1 + r] = S[K + r];
+      int q = 0;
+      const uint32_t v = g5_lane_tree_rs<1 + R>(s_tree - kG5Tree, Sc, lane, q);
+      if (lane < tree_np(1 + R) && q >= 1 && q < 1 + R) nb_emit_lane<K, R>(e, s, w, K + q - 1, v, init);
+      if (cr.expected) nb_check_combined<K>(e, s_cvs, s, w, lane, lane < tree_np(1 + R) && q == 0, v, init);
+    } else if constexpr (RS) {
       int q = 0;
       const uint32_t v = g5_lane_tree_rs<K + R>(s_tree - kG5Tree, S, lane, q);
       if constexpr (EM) {
@@ -384,16 +430,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
-          bool EM = false, int H = K, bool TAIL = false>
+          bool EM = false, int H = K, bool TAIL = false, bool CV = false>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
     constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
     static_assert(kNB != NB && (D * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL>(e, st);
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL, CV>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL, CV>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
@@ -426,7 +472,9 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
 // whether variant v of the nibble kernel runs on the persistent WorkQueue grid (needs a leased counter slot)
 constexpr bool nb_variant_persistent(int v) { return v == 150 || v == 163 || v == 167 || v == 170 || v == 171 ||
                                                      v == 172 || v == 176 || v == 177 || v == 187 || (v >= 189 && v <= 194) ||
-                                                     v == 196; }
+                                                     v == 196 || v == 230 || v == 231; }
+// whether variant v checks a reconstruction's inputs through one combined register (then nb_reverify follows it)
+constexpr bool nb_variant_cv(int v) { return v == 230 || v == 231; }
 
 // variant (g_tune.crc_variant, kernels.hpp kCrcVariants): the measured alternates of the nibble-table kernel
 template <int K, int R>
@@ -479,6 +527,14 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 220: return launch_nb<K, R, 1, kNB, 1, 4, 2, true, 0, true, true>(e, st);
     case 221: return launch_nb<K, R, 1, kNB, 2, 4, 2, true, 0, true, true>(e, st);
     case 222: return launch_nb<K, R, 1, kNB, 4, 4, 2, true, 0, true, true>(e, st);
+    // round 5, combined input verification (CV) for reconstructions that check stored CRCs: 230 = 170 (8-wave
+    // workgroups), 231 = 170 in 16-wave workgroups; anything else (encode, no expected CRCs) runs 170 itself
+    case 230:
+      if (!e.verify || !e.crc.expected) return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true>(e, st);
+      return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true, K, false, true>(e, st);
+    case 231:
+      if (!e.verify || !e.crc.expected) return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true>(e, st);
+      return launch_nb<K, R, 1, kNB, 16, 4, 2, true, 1, true, true, K, false, true>(e, st);
     default: break;
   }
   return hipErrorInvalidValue;

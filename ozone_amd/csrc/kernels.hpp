@@ -48,6 +48,7 @@ struct CrcArgs {
   const uint32_t *g26[6];     // device G26 table blobs for this CRC type, one per kG26Cfg entry
   const uint32_t *nib;        // device nibble table blob for this CRC type (kNib* layout)
   const uint32_t *xo;         // device XO table blob for this CRC type (kXo* layout)
+  const uint32_t *cv;         // device CV table blob for this CRC type (kCv* layout)
   uint32_t init_full;      // shift(0xFFFFFFFF, bpc bytes)
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
@@ -138,6 +139,21 @@ constexpr int kXoAdvance = 1024 - 16;
 constexpr int kXoInv = kG26Set;
 constexpr int kXoWords = kG26Set + 224;
 
+// Device CRC "CV" blob of the combined input verification (fused_nb.hpp, CV variants; round 5).  A reconstruction
+// checks the window CRCs of the K units it reads; instead of K raw registers (K shifts per step, K lane trees) the CV
+// kernel keeps ONE register: input j's nibble contributions are pre-multiplied by x^(8 w_j), w_j = j * kCvStride
+// bytes, so the register ends as XOR_j x^(8 w_j) raw_j, and is compared with the same combination of the stored
+// CRCs.  Distinct weights make any single-unit error, and two units with the same error pattern, change the
+// combination (x^(8 w_a) + x^(8 w_b) is a unit mod P for every pair: tests/test_cv_weights.py); a stripe that fails
+// is re-verified unit by unit (nb_reverify), so the first failing (unit, window) reported is the reference's.
+//   [j * 512 + p * 16 + n]            nibble table of input j (as kNib* set 0), advanced by j * kCvStride bytes
+//   [kCvShift + j * 224 + g * 32 + v] register shift by j * kCvStride bytes, 7 tables of 5-bit groups
+constexpr int kCvMaxK = 16;
+constexpr int kCvStride = 1024;
+constexpr int kCvShift = kCvMaxK * 512;
+constexpr int kCvWords = kCvShift + kCvMaxK * 224;
+constexpr int32_t kMismatchSuspect = 0x7ffffffe;  // mismatch[s] while a stripe awaits its unit-by-unit re-verify
+
 // Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.  Process-wide harness knobs for A/B and profiling
 // runs (bench.py --tune, scripts/ab.py): every field is an atomic, so setting one while other threads launch is not a
 // data race, but a set knob applies to every caller's next launch -- a production process leaves them at 0.
@@ -194,11 +210,12 @@ struct TuneKnobs {
 //       (the round-1 default), 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps
 //     fused RS (launch_encode_crc): 49 per-window kernel, 56 / 59 streamed-input kernel (fused.hip), 62 / 87 / 150 /
-//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 / 220-222 nibble-table kernel (fused_nb.hpp
+//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 / 220-222 / 230-231 nibble-table kernel (fused_nb.hpp
 //       launch_nb_kr)
 constexpr int kGfVariants[] = {1, 5, 11};
 constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  49,  56,  59,  62,  87,  150, 163, 167, 170, 171,
-                                 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196, 220, 221, 222};
+                                 172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196, 220, 221, 222,
+                                 230, 231};
 
 extern TuneKnobs g_tune;
 

@@ -1,0 +1,132 @@
+"""Combined input verification (fused_nb.hpp CV variants 230 / 231, round 5) vs the oracle (GPU).
+
+A reconstruction that checks the stored CRCs of the units it reads keeps one register for all of them, weighted per
+input (kernels.hpp kCv*), and re-verifies a failing stripe unit by unit (fused.hip nb_reverify).  The report must be
+the reference's first failing (unit, window) (ChecksumData.java:118-150) whatever the corruption: one unit, two units
+with the same error pattern at the same offsets (the pair the weights separate, tests/test_cv_weights.py), several
+windows and units, every stripe of a batch; the rebuilt units and their CRCs bit-exact either way.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from synth import SEED, cells
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from ozone_amd import _lib as L  # noqa: E402
+from ozone_amd import checksum as ck  # noqa: E402
+from ozone_amd import rawcoder as rc  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def _units(k, p, n, S, first):
+    out = []
+    for s in range(S):
+        d = cells(SEED, first + s * k, k, n)
+        out.append(np.stack(d + oracle.rs_encode(k, p, d)))
+    return np.stack(out)
+
+
+def _first_failure(units, corrupted, read, nwin, bpc, otype):
+    """the reference's report: min over the read units u and windows w of u * nwin + w whose CRC changed"""
+    for u in sorted(read):
+        a = oracle.crc_windows(otype, units[u], bpc)
+        b = oracle.crc_windows(otype, corrupted[u], bpc)
+        diff = np.nonzero(np.asarray(a) != np.asarray(b))[0]
+        if len(diff):
+            return u * nwin + int(diff[0])
+    return -1
+
+
+CASES = {
+    "none": [],
+    "one unit": [(2, 3 * 16384 + 5, 0x01)],
+    "two units, same pattern": [(1, 7 * 16384 + 100, 0x80), (4, 7 * 16384 + 100, 0x80)],
+    "two units, same zeroed range": "zero",
+    "several windows and units": [(9, 2 * 16384, 0x10), (3, 60 * 16384 + 7, 0xff), (3, 5, 0x02)],
+}
+
+
+@pytest.mark.parametrize("variant", [230, 231, 0])
+@pytest.mark.parametrize("case", sorted(CASES))
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
+def test_combined_verify_reports_the_first_failure(variant, case, ctype, otype):
+    k, p, n, bpc, S = 10, 4, 1 << 20, 16384, 3
+    erased = [1, 4, 10, 13]
+    present = [u for u in range(k + p) if u not in erased]
+    read = present[:k]
+    nwin = n // bpc
+    units = _units(k, p, n, S, 91000)
+    stored = np.stack([np.stack([oracle.crc_windows(otype, units[s, u], bpc) for u in range(k + p)])
+                       for s in range(S)]).astype(np.uint32)
+    corrupted = units.copy()
+    corrupted[:, erased] = 0x5A
+    bad = 1  # the corrupted stripe; 0 and 2 stay clean
+    spec = CASES[case]
+    if spec == "zero":  # both units' bytes of one range replaced by the same values (a shared stuck pattern)
+        corrupted[bad, read[2], 9000:9100] = 0
+        corrupted[bad, read[6], 9000:9100] = 0
+        corrupted[bad, read[2], 9000] ^= 0x40  # ensure the two ranges really changed
+        corrupted[bad, read[6], 9000] ^= 0x40
+    else:
+        for ui, pos, mask in spec:
+            corrupted[bad, read[ui], pos] ^= mask
+    lib = L.lib()
+    assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+    try:
+        d_out = torch.zeros((S, 4, n), dtype=torch.uint8, device=DEV)
+        d_crc = torch.zeros((S, 4, nwin), dtype=torch.int32, device=DEV)
+        mism = torch.zeros(S, dtype=torch.int32, device=DEV)
+        rc.RawErasureDecoder(rc.ECReplicationConfig(k, p)).reconstruct_crc_batch(
+            torch.from_numpy(corrupted).to(DEV), (k + p) * n, n, present, erased, d_out, 4 * n, n, S, n, ctype, bpc,
+            d_crc, d_expected=torch.from_numpy(stored.view(np.int32)).to(DEV), d_mismatch=mism)
+        torch.cuda.synchronize()
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+    m, out, oc = mism.cpu().numpy(), d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint32)
+    want = _first_failure(units[bad], corrupted[bad], read, nwin, bpc, otype)
+    assert m[0] == -1 and m[2] == -1, (case, m)
+    assert m[1] == want, (case, variant, m[1], want)
+    for s in (0, 2):
+        for i, e in enumerate(erased):
+            assert (out[s, i] == units[s, e]).all() and (oc[s, i] == stored[s, e]).all(), (case, s, e)
+    for i in range(4):  # the corrupted stripe's rebuilt CRCs describe what was written
+        assert (oc[bad, i] == oracle.crc_windows(otype, out[bad, i], bpc)).all()
+
+
+@pytest.mark.parametrize("variant", [230, 231])
+def test_combined_variants_without_expected_crcs_and_for_encode(variant):
+    """Without stored CRCs (decode + CRC of the rebuilt units only) and for encodes, the CV ids run their non-CV
+    geometry: same bytes and CRCs as the oracle."""
+    k, p, n, bpc, S = 6, 3, 1 << 18, 16384, 4
+    units = _units(k, p, n, S, 93000)
+    erased = [0, 5, 7]
+    present = [u for u in range(k + p) if u not in erased]
+    lib = L.lib()
+    assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+    try:
+        d_out = torch.zeros((S, 3, n), dtype=torch.uint8, device=DEV)
+        d_crc = torch.zeros((S, 3, n // bpc), dtype=torch.int32, device=DEV)
+        rc.RawErasureDecoder(rc.ECReplicationConfig(k, p)).reconstruct_crc_batch(
+            torch.from_numpy(units).to(DEV), (k + p) * n, n, present, erased, d_out, 3 * n, n, S, n,
+            ck.ChecksumType.CRC32C, bpc, d_crc)
+        enc_units = torch.from_numpy(units).to(DEV)
+        enc_units[:, k:] = 0
+        crcs = torch.zeros((S, k + p, n // bpc), dtype=torch.int32, device=DEV)
+        rc.RawErasureEncoder(rc.ECReplicationConfig(k, p)).encode_crc_batch(
+            enc_units, (k + p) * n, n, enc_units[:, k:], (k + p) * n, n, S, n, ck.ChecksumType.CRC32C, bpc, crcs)
+        torch.cuda.synchronize()
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+    out, oc = d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint32)
+    eu, c = enc_units.cpu().numpy(), crcs.cpu().numpy().view(np.uint32)
+    for s in range(S):
+        for i, e in enumerate(erased):
+            assert (out[s, i] == units[s, e]).all()
+            assert (oc[s, i] == oracle.crc_windows(oracle.CRC32C, units[s, e], bpc)).all()
+        assert (eu[s] == units[s]).all()
+        for u in range(k + p):
+            assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, units[s, u], bpc)).all()

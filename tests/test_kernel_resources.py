@@ -19,11 +19,11 @@ def _b(v):
     return f"Lb{int(v)}E"
 
 
-def _nb(K, R, D, NB, WPB, DYN, H, tail):
-    """Mangled template-argument list of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H, TAIL> (XO, EM
+def _nb(K, R, D, NB, WPB, DYN, H, tail, cv=False):
+    """Mangled template-argument list of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H, TAIL, CV> (XO, EM
     on), closed, so that it names exactly one instantiation."""
     return "encode_crc_nbI" + "".join([_i(K), _i(R), _i(D), _i(NB), _i(WPB), _i(4), _i(2), _b(1), _i(DYN), _b(1),
-                                       _b(1), _i(H), _b(tail)]) + "EEvN"
+                                       _b(1), _i(H), _b(tail), _b(cv)]) + "EEvN"
 
 
 def _defaults():

@@ -1,8 +1,9 @@
 """Same-process A/B of the fused reconstruction (verify the CRCs of the k units read + decode + CRC of the rebuilt unit)
 for a single lost unit of rs-6-3 and rs-3-2 -- the commonest datanode recovery (ECReconstructionCoordinator.java:240-352)
 -- device-resident, 1 MiB cells, CRC32C per 16 KiB.  Variant 0 (the nibble kernel, which takes one-output shapes since
-round 4) against 49 (the per-window kernel that took them before); interleaved rounds, HIP events.
-usage: python scripts/ab_single_erasure.py [ROUNDS]"""
+round 4) against 49 (the per-window kernel that took them before); interleaved rounds, HIP events.  VARIANTS (env,
+default 0,49) picks the crc_variant ids compared; SHAPES=all adds rs-6-3 with three units lost (round 5, CV).
+usage: [VARIANTS=0,231] [SHAPES=all] python scripts/ab_single_erasure.py [ROUNDS]"""
 import json
 import os
 import sys
@@ -18,7 +19,11 @@ from ozone_amd import rawcoder as rc  # noqa: E402
 ROUNDS = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 N, BPC = 1 << 20, 16384
 lib = L.lib()
-for k, p, erased, S in ((6, 3, [2], 3072), (3, 2, [1], 4096)):
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,49").split(",")]
+SHAPES = [(6, 3, [2], 3072), (3, 2, [1], 4096)]
+if os.environ.get("SHAPES") == "all":
+    SHAPES.append((6, 3, [0, 4, 7], 3072))
+for k, p, erased, S in SHAPES:
     nwin = N // BPC
     units = torch.empty((S, k + p, N), dtype=torch.uint8, device="cuda")
     for u in range(k):
@@ -34,7 +39,7 @@ for k, p, erased, S in ((6, 3, [2], 3072), (3, 2, [1], 4096)):
     dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
     e = len(erased)
     alg = S * (k + e) * N + S * (k + e) * nwin * 4 + S * 4  # k units + their stored CRCs read, e units + CRCs written
-    times = {0: [], 49: []}
+    times = {v: [] for v in VARIANTS}
 
     def launch():
         dec.reconstruct_crc_batch(units, (k + p) * N, N, present, erased, out, e * N, N, S, N, ck.ChecksumType.CRC32C,
@@ -54,9 +59,10 @@ for k, p, erased, S in ((6, 3, [2], 3072), (3, 2, [1], 4096)):
 
     try:
         for _ in range(ROUNDS):
-            for v in (0, 49):
+            for v in VARIANTS:
                 times[v].append(run(v))
-        ok = bool((mism == -1).all().item()) and bool((out[:, 0] == units[:, erased[0]]).all().item())
+        ok = bool((mism == -1).all().item()) and all(bool((out[:, i] == units[:, u]).all().item())
+                                                     for i, u in enumerate(erased))
     finally:
         lib.ozec_set_tuning(b"crc_variant", 0)
     for v, ts in times.items():

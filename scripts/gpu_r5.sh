@@ -84,6 +84,9 @@ for s in $STEPS; do
         done
       done
       python3 scripts/final_sq_summary.py "$OUT" > "$OUT/sq_summary.log" 2>&1 || exit 23 ;;
+    recab)  # fused reconstruction A/B of rs-6-3 / rs-3-2 shapes (scripts/ab_single_erasure.py, VARIANTS)
+      run "rec ab" 300 env SHAPES=all VARIANTS=${VARIANTS:-0,231} python -u scripts/ab_single_erasure.py ${ROUNDS:-6} \
+        > "$OUT/ab_rec.log" 2>&1 || { tail -20 "$OUT/ab_rec.log"; exit 24; } ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     tailnp)  # the same with the host batches' device unit pitch = the cell length (host_pitch16=0)

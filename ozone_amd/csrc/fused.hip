@@ -334,6 +334,10 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v, bool
   // a small batch: workgroups of 4 waves spread its units over many CUs (the 16-wave persistent workgroups put them on
   // a few, whose LDS pipes then serve all their waves; kernels.hpp TuneKnobs::nb_small_units)
   if (v == 0 && e.code.nstripes * e.crc.nwin < g_tune.nb_small_units.load(std::memory_order_relaxed)) v = 222;
+  // reconstructions that check stored CRCs: one combined input register (231, CV; nb_reverify after it).  Same-process
+  // A/Bs (profiles/r05/cv/): C3r 5.86-5.88 -> 5.70-5.71 ms on one box, 5.62 -> 5.34 ms on another; rs-6-3 lose 1 / lose
+  // 3 -2.5 / -2.2 %; rs-3-2 lose 1 even, so it keeps 172
+  if (v == 0 && ws && !tail && e.verify && e.crc.expected && k >= 6) v = 231;
   if (v == 0) v = k == 10 ? (ws ? 177 : 173) : !ws ? 174 : k == 6 ? 171 : 172;
   const bool used = ws && nb_variant_persistent(v);
   EncCrcArgs ed = e;

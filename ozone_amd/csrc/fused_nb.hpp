@@ -472,9 +472,9 @@ hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
 // whether variant v of the nibble kernel runs on the persistent WorkQueue grid (needs a leased counter slot)
 constexpr bool nb_variant_persistent(int v) { return v == 150 || v == 163 || v == 167 || v == 170 || v == 171 ||
                                                      v == 172 || v == 176 || v == 177 || v == 187 || (v >= 189 && v <= 194) ||
-                                                     v == 196 || (v >= 230 && v <= 234); }
+                                                     v == 196 || v == 231 || v == 234; }
 // whether variant v checks a reconstruction's inputs through one combined register (then nb_reverify follows it)
-constexpr bool nb_variant_cv(int v) { return v >= 230 && v <= 234; }
+constexpr bool nb_variant_cv(int v) { return v == 231 || v == 234; }
 
 // variant (g_tune.crc_variant, kernels.hpp kCrcVariants): the measured alternates of the nibble-table kernel
 template <int K, int R>
@@ -527,22 +527,13 @@ hipError_t launch_nb_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     case 220: return launch_nb<K, R, 1, kNB, 1, 4, 2, true, 0, true, true>(e, st);
     case 221: return launch_nb<K, R, 1, kNB, 2, 4, 2, true, 0, true, true>(e, st);
     case 222: return launch_nb<K, R, 1, kNB, 4, 4, 2, true, 0, true, true>(e, st);
-    // round 5, combined input verification (CV) for reconstructions that check stored CRCs: 230 = 170 (8-wave
-    // workgroups), 231 = 170 in 16-wave workgroups; anything else (encode, no expected CRCs) runs 170 itself
-    case 230:
-      if (!e.verify || !e.crc.expected) return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true>(e, st);
-      return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true, K, false, true>(e, st);
+    // round 5, combined input verification (CV) for reconstructions that check stored CRCs: 231 = 170's one-step groups
+    // in 16-wave workgroups (the default for rs-6-x / rs-10-x, fused.hip), 234 = 231 with a ring of 2 loads; for an
+    // encode or without stored CRCs either runs 170 itself.  (230 = 8-wave workgroups, 232 = two 10-wave and 233 = two
+    // 12-wave workgroups per CU measured 2-23 % slower than 231, profiles/r05/cv/, and were taken out.)
     case 231:
       if (!e.verify || !e.crc.expected) return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true>(e, st);
       return launch_nb<K, R, 1, kNB, 16, 4, 2, true, 1, true, true, K, false, true>(e, st);
-    // 232-234: 231's register file and workgroup shape -- two 10-wave workgroups per CU (5 waves per SIMD), two
-    // 12-wave ones (6 per SIMD), and 231 with a ring of 2 loads (fewer VGPRs)
-    case 232:
-      if (!e.verify || !e.crc.expected) return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true>(e, st);
-      return launch_nb<K, R, 1, kNB, 10, 5, 2, true, 1, true, true, K, false, true>(e, st);
-    case 233:
-      if (!e.verify || !e.crc.expected) return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true>(e, st);
-      return launch_nb<K, R, 1, kNB, 12, 6, 2, true, 1, true, true, K, false, true>(e, st);
     case 234:
       if (!e.verify || !e.crc.expected) return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 1, true, true>(e, st);
       return launch_nb<K, R, 1, 2, 16, 4, 2, true, 1, true, true, K, false, true>(e, st);

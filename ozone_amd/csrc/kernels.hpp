@@ -210,12 +210,12 @@ struct TuneKnobs {
 //       (the round-1 default), 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps
 //     fused RS (launch_encode_crc): 49 per-window kernel, 56 / 59 streamed-input kernel (fused.hip), 62 / 87 / 150 /
-//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 / 220-222 / 230-234 nibble-table kernel (fused_nb.hpp
+//       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 / 220-222 / 231 / 234 nibble-table kernel (fused_nb.hpp
 //       launch_nb_kr)
 constexpr int kGfVariants[] = {1, 5, 11};
 constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  49,  56,  59,  62,  87,  150, 163, 167, 170, 171,
                                  172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196, 220, 221, 222,
-                                 230, 231, 232, 233, 234};
+                                 231, 234};
 
 extern TuneKnobs g_tune;
 

@@ -1,4 +1,4 @@
-"""Combined input verification (fused_nb.hpp CV variants 230 / 231, round 5) vs the oracle (GPU).
+"""Combined input verification (fused_nb.hpp CV variants 231 / 234, round 5) vs the oracle (GPU).
 
 A reconstruction that checks the stored CRCs of the units it reads keeps one register for all of them, weighted per
 input (kernels.hpp kCv*), and re-verifies a failing stripe unit by unit (fused.hip nb_reverify).  The report must be
@@ -50,7 +50,7 @@ CASES = {
 }
 
 
-@pytest.mark.parametrize("variant", [230, 231, 0])
+@pytest.mark.parametrize("variant", [231, 234, 0])
 @pytest.mark.parametrize("case", sorted(CASES))
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
 def test_combined_verify_reports_the_first_failure(variant, case, ctype, otype):
@@ -97,7 +97,7 @@ def test_combined_verify_reports_the_first_failure(variant, case, ctype, otype):
         assert (oc[bad, i] == oracle.crc_windows(otype, out[bad, i], bpc)).all()
 
 
-@pytest.mark.parametrize("variant", [230, 231])
+@pytest.mark.parametrize("variant", [231, 234])
 def test_combined_variants_without_expected_crcs_and_for_encode(variant):
     """Without stored CRCs (decode + CRC of the rebuilt units only) and for encodes, the CV ids run their non-CV
     geometry: same bytes and CRCs as the oracle."""

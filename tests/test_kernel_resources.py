@@ -27,7 +27,8 @@ def _nb(K, R, D, NB, WPB, DYN, H, tail, cv=False):
 
 
 def _defaults():
-    """fused.hip: rs-10-x 177 (queue) / 173, rs-6-x 171 / 174, rs-3-x 172 / 174 (fused_nb.hpp launch_nb_kr), x = 1-4."""
+    """fused.hip: rs-10-x 177 (queue) / 173, rs-6-x 171 / 174, rs-3-x 172 / 174 (fused_nb.hpp launch_nb_kr), x = 1-4;
+    their byte-tail instantiations; 231 for verifying reconstructions."""
     out = []
     for t in (False, True):  # 16-B cells, and the byte-tail (TAIL) instantiation of the same variant
         out += [_nb(10, R, 2, 5, 16, 1, 5, t) for R in (1, 2, 3, 4)]     # 177
@@ -35,6 +36,9 @@ def _defaults():
         out += [_nb(6, R, 2, 3, 16, 1, 6, t) for R in (1, 2, 3)]   # 171
         out += [_nb(6, R, 2, 2, 12, 0, 6, t) for R in (1, 2, 3)]   # 174 (kD2 = 2 for K = 6)
         out += [_nb(3, R, 2, 2, 16, 1, 3, t) for R in (1, 2)] + [_nb(3, R, 2, 2, 12, 0, 3, t) for R in (1, 2)]
+    # 231: the combined-verify reconstruction default for rs-10-x and rs-6-x
+    out += [_nb(10, R, 1, 5, 16, 1, 10, False, True) for R in (1, 2, 3, 4)]
+    out += [_nb(6, R, 1, 3, 16, 1, 6, False, True) for R in (1, 2, 3)]
     return out
 
 

@@ -34,7 +34,7 @@ def test_every_variant_family_is_swept_by_a_gpu_test():
         assert re.search(r"parametrize\(\"variant\",[^)]*variants\." + fam + r"\b", src), fam
 
 
-@pytest.mark.parametrize("v", list(range(140, 150)) + [1, 11, 12, 13, 17, 23, 51, 61, 100, 151, 175, 178, 185, 186, 188, 195, 197, 199, 200, 202, 203, 210, 211, 212, 213, 999, -1])
+@pytest.mark.parametrize("v", list(range(140, 150)) + [1, 11, 12, 13, 17, 23, 51, 61, 100, 151, 175, 178, 185, 186, 188, 195, 197, 199, 200, 202, 203, 210, 211, 212, 213, 230, 232, 233, 999, -1])
 def test_removed_and_unknown_crc_variants_rejected(v):
     lib = L.lib()
     assert lib.ozec_set_tuning(b"crc_variant", v) == L.OZEC_EINVAL

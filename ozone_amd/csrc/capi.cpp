@@ -198,6 +198,7 @@ struct DevCtx {
   uint32_t *nib_tables[2] = {};                   // [type]
   uint32_t *xo_tables[2] = {};                    // [type]
   uint32_t *cv_tables[2] = {};                    // [type]
+  uint32_t *bshift_tables[2] = {};                // [type]
 
   int acquire(Slot **out) {
     std::unique_lock<std::mutex> lk(pool_mu);
@@ -272,6 +273,9 @@ int get_ctx(DevCtx **out) {
       const auto &cv = CrcMath::get(static_cast<CrcType>(t)).cv_tables();
       OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->cv_tables[t]), cv.size() * sizeof(uint32_t)));
       OZEC_HIP(hipMemcpy(c->cv_tables[t], cv.data(), cv.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+      const auto &bs = CrcMath::get(static_cast<CrcType>(t)).bshift_tables();
+      OZEC_HIP(hipMalloc(reinterpret_cast<void **>(&c->bshift_tables[t]), bs.size() * sizeof(uint32_t)));
+      OZEC_HIP(hipMemcpy(c->bshift_tables[t], bs.data(), bs.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     g_ctx[dev] = std::move(c);
   }
@@ -985,6 +989,9 @@ static int make_crc_args(DevCtx *ctx, int checksum_type, const uint8_t *d_base, 
   a->nib = ctx->nib_tables[static_cast<int>(t)];
   a->xo = ctx->xo_tables[static_cast<int>(t)];
   a->cv = ctx->cv_tables[static_cast<int>(t)];
+  a->bshift = nullptr;  // the run check's shift by bpc: bpc = 4 KiB << i only
+  for (int i = 0; i < ozec::kBshiftN; ++i)
+    if (bpc == (size_t{4096} << i)) a->bshift = ctx->bshift_tables[static_cast<int>(t)] + i * 224;
   a->init_full = cm.shift(0xffffffffu, bpc);
   a->init_last = cm.shift(0xffffffffu, len - (a->nwin ? (a->nwin - 1) * bpc : 0));
   a->big_endian = big_endian;

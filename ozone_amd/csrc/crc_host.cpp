@@ -111,6 +111,14 @@ CrcMath::CrcMath(uint32_t poly) : poly_(poly) {
       for (uint32_t v = 0; v < 32; ++v)
         cv_[kCvShift + j * 224 + g * 32 + v] = apply(wj, static_cast<uint32_t>(uint64_t{v} << (5 * g)));
   }
+  // bshift blob: register shift by 4 KiB << i bytes
+  bshift_.assign(kBshiftN * 224, 0);
+  for (int i = 0; i < kBshiftN; ++i) {
+    uint32_t m[32];
+    shift_matrix(uint64_t{4096} << i, m);
+    for (int g = 0; g < 7; ++g)
+      for (uint32_t v = 0; v < 32; ++v) bshift_[i * 224 + g * 32 + v] = apply(m, static_cast<uint32_t>(uint64_t{v} << (5 * g)));
+  }
 }
 
 // Block bit (0..127; dword d bit k = 32d + k, i.e. byte p/8 bit p%8) that index bit i of G26 table g reads,

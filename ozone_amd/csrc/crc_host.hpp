@@ -29,6 +29,8 @@ class CrcMath {
   const std::vector<uint32_t> &xo_tables() const { return xo_; }
   // the device CV blob (kernels.hpp kCv*)
   const std::vector<uint32_t> &cv_tables() const { return cv_; }
+  // the register shift by (4 KiB << i) bytes as 7 tables of 32 (the bshift blob of kernels.hpp), i < kBshiftN
+  const std::vector<uint32_t> &bshift_tables() const { return bshift_; }
   uint32_t byte_table(int v) const { return t0_[v]; }
   uint32_t poly() const { return poly_; }
   // x^(8n) mod P in CrcUtil's reversed representation (CrcUtil.getMonomial)
@@ -55,6 +57,7 @@ class CrcMath {
   std::vector<uint32_t> nib_;
   std::vector<uint32_t> xo_;
   std::vector<uint32_t> cv_;
+  std::vector<uint32_t> bshift_;
   std::vector<uint32_t> build_blob(int B) const;
   std::vector<uint32_t> build_g26(int B, int D) const;
 };

@@ -353,14 +353,23 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26(const CrcArgs a) {
 // XO: the register moves by one step with no shift lookups (kernels.hpp kXo*): it is XORed into the first dword of
 // its lane's next block, which is looked up in the XO set; the advance is undone once per window.  D then only sets
 // the unroll (the load ring NS divides it); the LDS holds the lane-tree shifts and the XO blob instead of D sets.
-template <int D, int NS, bool XO = false>
+// VR (round 5, verify with XO): the wave first checks its whole run of windows as ONE message -- the register is not
+// reset and not merged at window ends, so the lane tree and the XO inverse run once per run instead of once per
+// window -- against the stored window CRCs folded by Horner's rule (E = E x^(8 bpc) + raw_w, the shift by bpc from
+// a.bshift).  A run that matches is done (16 windows of 16 KiB: one tree instead of 16, 7 lookups per window for E);
+// one that does not is checked again window by window, so the first failing window recorded per cell is the
+// reference's.  Two windows of a run with the same error pattern k windows apart cancel only if
+// 1 + x^(8 bpc k) shares a factor with P beyond x + 1 (tests/test_cv_weights.py).
+template <int D, int NS, bool XO = false, bool VR = false>
 __global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int64_t nfull, int64_t per_wave) {
   static_assert(NS >= 2 && D % NS == 0, "the register ring must divide the unrolled group");
-  constexpr int kTree = XO ? 0 : g26_tree(D), kXoOff = 1344;
-  __shared__ __attribute__((aligned(16))) uint32_t s_t[XO ? 1344 + kXoWords : g26_words(D)];
+  static_assert(!VR || XO, "the run check folds through the XO blob");
+  constexpr int kTree = XO ? 0 : g26_tree(D), kXoOff = 1344, kBsOff = 1344 + kXoWords;
+  __shared__ __attribute__((aligned(16))) uint32_t s_t[XO ? 1344 + kXoWords + (VR ? 224 : 0) : g26_words(D)];
   if constexpr (XO) {
     load_tables(s_t, a.g26[g26_slot(1, D)] + g26_tree(D), 1344);
     load_tables(s_t + kXoOff, a.xo, kXoWords);
+    if constexpr (VR) load_tables(s_t + kBsOff, a.bshift, 224);
   } else {
     load_tables(s_t, a.g26[g26_slot(1, D)], g26_words(D));
   }
@@ -396,6 +405,38 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int6
     }
   };
   uint4 x[NS];
+  if constexpr (VR) {
+    if (a.expected) {  // (VR is launched for verify only)
+#pragma unroll
+      for (int i = 0; i + 1 < NS; ++i) load_next(x[i]);
+      int64_t cc = u0 / nfull, cw = u0 - cc * nfull;
+      uint32_t S = 0, E = 0;
+      for (int64_t u = u0; u < u1; ++u) {
+        const uint32_t ex0 = *(cu32 *)(a.expected + cc * a.out_cell_stride + cw);
+        E = g5_shift(s_t + kBsOff, E) ^ ~((a.expected_be ? __builtin_bswap32(ex0) : ex0) ^ a.init_full);
+        int32_t g = 0;
+        do {
+#pragma unroll
+          for (int rr = 0; rr < D; ++rr) {
+            load_next(x[(rr + NS - 1) % NS]);
+            uint4 xs = x[rr % NS];
+            xs.x ^= S;
+            S = g26_block(s_t + kXoOff, xs);
+          }
+        } while (++g < G);
+        if (++cw == nfull) {
+          cw = 0;
+          ++cc;
+        }
+      }
+      S = g5_lane_tree(s_t + kTree - kG5Tree, S, lane);
+      S = g5_shift(s_t + kXoOff + kXoInv, S);
+      if (S == E) return;  // wave-uniform: every lane holds the merged register
+      // the rare path: this run window by window (the cursor back at its start)
+      lu = u0, lc = u0 / nfull, lw = u0 - lc * nfull, lt = 0;
+      lbase = a.base + lc * a.cell_stride + lw * a.bpc + lane * 16;
+    }
+  }
 #pragma unroll
   for (int i = 0; i + 1 < NS; ++i) load_next(x[i]);
   int64_t cc = u0 / nfull, cw = u0 - cc * nfull;  // compute cursor: (cell, window) of u
@@ -955,13 +996,13 @@ int64_t stream_grid(int64_t total, int64_t per_wave) {
 
 // Full windows of every cell through the streaming kernel, the short last window of each cell (len % bpc)
 // through the per-window kernel.
-template <int D, int NS, bool XO = false>
+template <int D, int NS, bool XO = false, bool VR = false>
 hipError_t launch_crc_stream(const CrcArgs &a, hipStream_t st) {
   const int64_t nfull = a.len / a.bpc;
   const int64_t total = a.ncells * nfull;
   if (total > 0) {
     const int64_t per_wave = stream_per_wave(total, a.bpc);
-    hipLaunchKernelGGL((crc_windows_g26s<D, NS, XO>), dim3(static_cast<unsigned>(stream_grid(total, per_wave))),
+    hipLaunchKernelGGL((crc_windows_g26s<D, NS, XO, VR>), dim3(static_cast<unsigned>(stream_grid(total, per_wave))),
                        dim3(kBlock), 0, st, a, nfull, per_wave);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
@@ -997,6 +1038,9 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
     if (a.bpc % 4096 == 0) {
       if (v == 20) return launch_crc_stream<4, 2>(a, st);
       if (v == 22) return launch_crc_stream<4, 4>(a, st);
+      // verify with bpc = 4 KiB << i: a run of windows checked as one message (VR), window by window only when it
+      // fails; 24 pins the window-by-window check (round 4's default)
+      if (a.expected && a.bshift && v != 24) return launch_crc_stream<4, 2, true, true>(a, st);
       return launch_crc_stream<4, 2, true>(a, st);
     }
     // per-window kernel: G26 tables, B = 1 block per lane per step, groups of D = 4 steps, two steps of loads in

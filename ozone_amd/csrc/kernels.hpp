@@ -49,6 +49,7 @@ struct CrcArgs {
   const uint32_t *nib;        // device nibble table blob for this CRC type (kNib* layout)
   const uint32_t *xo;         // device XO table blob for this CRC type (kXo* layout)
   const uint32_t *cv;         // device CV table blob for this CRC type (kCv* layout)
+  const uint32_t *bshift;     // register shift by bpc bytes (7 tables of 32; kBshift*), null for other bpc
   uint32_t init_full;      // shift(0xFFFFFFFF, bpc bytes)
   uint32_t init_last;      // shift(0xFFFFFFFF, last window bytes)
   int32_t big_endian;
@@ -154,6 +155,11 @@ constexpr int kCvShift = kCvMaxK * 512;
 constexpr int kCvWords = kCvShift + kCvMaxK * 224;
 constexpr int32_t kMismatchSuspect = 0x7ffffffe;  // mismatch[s] while a stripe awaits its unit-by-unit re-verify
 
+// Device "bshift" blob: the register shift by bpc bytes for bpc = 4 KiB << i, i < kBshiftN (7 tables of 32 each), used by
+// the run check of the streaming verify kernel (kernels.hip crc_windows_g26s VR: the stored CRCs of a run of windows
+// folded by Horner's rule into the CRC the run has as one message)
+constexpr int kBshiftN = 9;  // 4 KiB .. 1 MiB
+
 // Runtime tuning knobs (ozec_set_tuning): 0 = built-in default.  Process-wide harness knobs for A/B and profiling
 // runs (bench.py --tune, scripts/ab.py): every field is an atomic, so setting one while other threads launch is not a
 // data race, but a set knob applies to every caller's next launch -- a production process leaves them at 0.
@@ -205,7 +211,8 @@ struct TuneKnobs {
 // ozec_tuning_variants); ozec_set_tuning rejects any other id.
 //   gf_variant (coding kernel gf_code_vec, kernels.hip launch_kr): 1, 5, 11
 //   crc_variant, by kernel family:
-//     streaming CRC (launch_crc_windows): 20, 22 -- D-step groups instead of the XO default
+//     streaming CRC (launch_crc_windows): 20, 22 -- D-step groups instead of the XO default; 24 -- verify without
+//       the run check (round 4's default)
 //     fused XOR codec (launch_enc_crc_kr, R = 1 all-ones): 2 no register shortcut, 3 D = 4 with loads one step ahead
 //       (the round-1 default), 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps
@@ -213,7 +220,7 @@ struct TuneKnobs {
 //       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 / 220-222 / 231 / 234 nibble-table kernel (fused_nb.hpp
 //       launch_nb_kr)
 constexpr int kGfVariants[] = {1, 5, 11};
-constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  49,  56,  59,  62,  87,  150, 163, 167, 170, 171,
+constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  24,  49,  56,  59,  62,  87,  150, 163, 167, 170, 171,
                                  172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196, 220, 221, 222,
                                  231, 234};
 

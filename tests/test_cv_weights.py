@@ -80,3 +80,18 @@ def test_gf2_helpers():
     p = POLYS["CRC32"]
     assert _xpow(32, p) == p ^ (1 << 32)          # x^32 = P - x^32
     assert _gcd(p, 1) == 1 and _gcd(0b110, 0b11) == 0b11  # x^2 + x = x (x + 1)
+
+
+@pytest.mark.parametrize("crc", sorted(POLYS))
+def test_run_check_window_distances(crc):
+    """The streaming verify kernel's run check (kernels.hip crc_windows_g26s VR) weights window w of a run by
+    x^(8 bpc (m - 1 - w)); two windows k apart with the same error pattern cancel only if 1 + x^(8 bpc k) shares a
+    factor with P: none for CRC-32, only x + 1 for CRC-32C (then only the one delta D = P / (x + 1)), for every bpc the
+    check runs with (4 KiB << i, i < kBshiftN) and runs of up to 256 windows."""
+    p = POLYS[crc]
+    want = 0b11 if crc == "CRC32C" else 1
+    for i in range(_hdr_int("kBshiftN")):
+        bpc = 4096 << i
+        for k in range(1, 256):
+            f = _xpow(8 * bpc * k, p) ^ 1
+            assert f != 0 and _gcd(p, f) == want, (crc, bpc, k)

@@ -130,3 +130,45 @@ def test_combined_variants_without_expected_crcs_and_for_encode(variant):
         assert (eu[s] == units[s]).all()
         for u in range(k + p):
             assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, units[s, u], bpc)).all()
+
+
+@pytest.mark.parametrize("variant", [0, 24])
+@pytest.mark.parametrize("bpc", [4096, 16384])
+@pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])
+def test_verify_run_check_reports_the_first_failing_window(variant, bpc, ctype, otype):
+    """ozec_checksum_verify_batch (the datanode scanner) checks a run of windows as one message (crc_windows_g26s VR,
+    the default) and re-checks a failing run window by window (24: always window by window).  Corruptions: one byte;
+    the same pattern in two windows of one run (the pair the run weights separate); in two cells whose windows share a
+    run; in a cell's last full window; none -- the per-cell first failing window vs the oracle."""
+    C, n = 24, 1 << 20  # 24 cells of 64 (bpc 16 KiB) or 256 windows
+    nwin = n // bpc
+    data = np.stack(cells(SEED, 95000, C, n))
+    exp = np.stack([oracle.crc_windows(otype, data[c], bpc) for c in range(C)]).astype(np.uint32)
+    bad = data.copy()
+    bad[1, 3 * bpc + 17] ^= 0x04                                   # one byte
+    bad[5, 2 * bpc + 100] ^= 0x81                                  # same pattern, two windows of one run
+    bad[5, 9 * bpc + 100] ^= 0x81
+    bad[7, n - 1] ^= 0x10                                          # the cell's last (full) window
+    bad[8, 0] ^= 0x01                                              # first window of a cell ...
+    bad[9, 5] ^= 0x01                                              # ... and of the next one (often one run)
+    want = np.full(C, -1)
+    for c in range(C):
+        diff = np.nonzero(np.asarray(oracle.crc_windows(otype, bad[c], bpc), np.uint32) != exp[c])[0]
+        if len(diff):
+            want[c] = int(diff[0])
+    lib = L.lib()
+    assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
+    try:
+        mism = torch.zeros(C, dtype=torch.int32, device=DEV)
+        ck.checksum_verify_batch(ctype, torch.from_numpy(bad).to(DEV), n, C, n, bpc,
+                                 torch.from_numpy(exp.view(np.int32)).to(DEV), mism)
+        torch.cuda.synchronize()
+        got = mism.cpu().numpy()
+        ck.checksum_verify_batch(ctype, torch.from_numpy(data).to(DEV), n, C, n, bpc,
+                                 torch.from_numpy(exp.view(np.int32)).to(DEV), mism)
+        torch.cuda.synchronize()
+        clean = mism.cpu().numpy()
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+    assert got.tolist() == want.tolist(), (variant, bpc)
+    assert clean.tolist() == [-1] * C

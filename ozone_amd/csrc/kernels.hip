@@ -360,10 +360,14 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26(const CrcArgs a) {
 // one that does not is checked again window by window, so the first failing window recorded per cell is the
 // reference's.  Two windows of a run with the same error pattern k windows apart cancel only if
 // 1 + x^(8 bpc k) shares a factor with P beyond x + 1 (tests/test_cv_weights.py).
-template <int D, int NS, bool XO = false, bool VR = false>
+// TB (round 5, compute with XO): the registers of TB consecutive windows go through ONE reduce-scatter lane tree
+// (g5_lane_tree_rs; TB - 1 + 6 - log2 TB shifts instead of 6 TB) and one XO inverse per lane, then lanes 0..TB-1 store
+// one window each.
+template <int D, int NS, bool XO = false, bool VR = false, int TB = 1>
 __global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int64_t nfull, int64_t per_wave) {
   static_assert(NS >= 2 && D % NS == 0, "the register ring must divide the unrolled group");
   static_assert(!VR || XO, "the run check folds through the XO blob");
+  static_assert(TB == 1 || (XO && (TB == 2 || TB == 4 || TB == 8)), "batched trees: XO, a power of two");
   constexpr int kTree = XO ? 0 : g26_tree(D), kXoOff = 1344, kBsOff = 1344 + kXoWords;
   __shared__ __attribute__((aligned(16))) uint32_t s_t[XO ? 1344 + kXoWords + (VR ? 224 : 0) : g26_words(D)];
   if constexpr (XO) {
@@ -439,6 +443,38 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int6
   }
 #pragma unroll
   for (int i = 0; i + 1 < NS; ++i) load_next(x[i]);
+  if constexpr (TB > 1) {
+    if (!a.expected) {
+      for (int64_t ub = u0; ub < u1; ub += TB) {
+        uint32_t Sw[TB];
+#pragma unroll
+        for (int q = 0; q < TB; ++q) {
+          uint32_t S = 0;
+          if (ub + q < u1) {  // wave-uniform
+            int32_t g = 0;
+            do {
+#pragma unroll
+              for (int rr = 0; rr < D; ++rr) {
+                load_next(x[(rr + NS - 1) % NS]);
+                uint4 xs = x[rr % NS];
+                xs.x ^= S;
+                S = g26_block(s_t + kXoOff, xs);
+              }
+            } while (++g < G);
+          }
+          Sw[q] = S;
+        }
+        int q = 0;
+        uint32_t v = g5_lane_tree_rs<TB>(s_t + kTree - kG5Tree, Sw, lane, q);
+        v = g5_shift(s_t + kXoOff + kXoInv, v);
+        if (lane < TB && ub + q < u1) {
+          const int64_t c = (ub + q) / nfull, w = ub + q - c * nfull;
+          a.out[c * a.out_cell_stride + w] = crc_finish(v, a.init_full, a.raw, a.big_endian);
+        }
+      }
+      return;
+    }
+  }
   int64_t cc = u0 / nfull, cw = u0 - cc * nfull;  // compute cursor: (cell, window) of u
   for (int64_t u = u0; u < u1; ++u) {
     uint32_t ex = 0;
@@ -996,13 +1032,13 @@ int64_t stream_grid(int64_t total, int64_t per_wave) {
 
 // Full windows of every cell through the streaming kernel, the short last window of each cell (len % bpc)
 // through the per-window kernel.
-template <int D, int NS, bool XO = false, bool VR = false>
+template <int D, int NS, bool XO = false, bool VR = false, int TB = 1>
 hipError_t launch_crc_stream(const CrcArgs &a, hipStream_t st) {
   const int64_t nfull = a.len / a.bpc;
   const int64_t total = a.ncells * nfull;
   if (total > 0) {
     const int64_t per_wave = stream_per_wave(total, a.bpc);
-    hipLaunchKernelGGL((crc_windows_g26s<D, NS, XO, VR>), dim3(static_cast<unsigned>(stream_grid(total, per_wave))),
+    hipLaunchKernelGGL((crc_windows_g26s<D, NS, XO, VR, TB>), dim3(static_cast<unsigned>(stream_grid(total, per_wave))),
                        dim3(kBlock), 0, st, a, nfull, per_wave);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
@@ -1041,6 +1077,9 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
       // verify with bpc = 4 KiB << i: a run of windows checked as one message (VR), window by window only when it
       // fails; 24 pins the window-by-window check (round 4's default)
       if (a.expected && a.bshift && v != 24) return launch_crc_stream<4, 2, true, true>(a, st);
+      // compute: the lane trees of 4 consecutive windows at once; 28 one tree per window (round 4), 29 8 windows
+      if (!a.expected && v == 29) return launch_crc_stream<4, 2, true, false, 8>(a, st);
+      if (!a.expected && v != 28) return launch_crc_stream<4, 2, true, false, 4>(a, st);
       return launch_crc_stream<4, 2, true>(a, st);
     }
     // per-window kernel: G26 tables, B = 1 block per lane per step, groups of D = 4 steps, two steps of loads in

@@ -212,7 +212,7 @@ struct TuneKnobs {
 //   gf_variant (coding kernel gf_code_vec, kernels.hip launch_kr): 1, 5, 11
 //   crc_variant, by kernel family:
 //     streaming CRC (launch_crc_windows): 20, 22 -- D-step groups instead of the XO default; 24 -- verify without
-//       the run check (round 4's default)
+//       the run check (round 4's default); 28 / 29 -- compute with one lane tree per window (round 4) / per 8 windows
 //     fused XOR codec (launch_enc_crc_kr, R = 1 all-ones): 2 no register shortcut, 3 D = 4 with loads one step ahead
 //       (the round-1 default), 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps
@@ -220,7 +220,7 @@ struct TuneKnobs {
 //       163 / 167 / 170-174 / 176 / 177 / 187 / 189-194 / 196 / 220-222 / 231 / 234 nibble-table kernel (fused_nb.hpp
 //       launch_nb_kr)
 constexpr int kGfVariants[] = {1, 5, 11};
-constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  24,  49,  56,  59,  62,  87,  150, 163, 167, 170, 171,
+constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  24,  28,  29,  49,  56,  59,  62,  87,  150, 163, 167, 170, 171,
                                  172, 173, 174, 176, 177, 187, 189, 190, 191, 192, 193, 194, 196, 220, 221, 222,
                                  231, 234};
 

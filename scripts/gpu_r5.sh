@@ -87,6 +87,11 @@ for s in $STEPS; do
     recab)  # fused reconstruction A/B of rs-6-3 / rs-3-2 shapes (scripts/ab_single_erasure.py, VARIANTS)
       run "rec ab" 300 env SHAPES=all VARIANTS=${VARIANTS:-0,231} python -u scripts/ab_single_erasure.py ${ROUNDS:-6} \
         > "$OUT/ab_rec.log" 2>&1 || { tail -20 "$OUT/ab_rec.log"; exit 24; } ;;
+    abcrc)  # same-process A/Bs of the streaming CRC kernel: compute (batched trees) and verify (run check)
+      run "ab crc" 300 python -u scripts/ab.py crc crc_variant ${CRC:-0,28,29} ${ROUNDS:-6} > "$OUT/ab_crc.log" 2>&1 \
+        || { tail -20 "$OUT/ab_crc.log"; exit 25; }
+      run "ab verify" 300 python -u scripts/ab.py verify crc_variant ${VERIFY:-0,24} ${ROUNDS:-6} > "$OUT/ab_verify.log" \
+        2>&1 || { tail -20 "$OUT/ab_verify.log"; exit 26; } ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     tailnp)  # the same with the host batches' device unit pitch = the cell length (host_pitch16=0)

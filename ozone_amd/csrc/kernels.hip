@@ -1077,9 +1077,10 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
       // verify with bpc = 4 KiB << i: a run of windows checked as one message (VR), window by window only when it
       // fails; 24 pins the window-by-window check (round 4's default)
       if (a.expected && a.bshift && v != 24) return launch_crc_stream<4, 2, true, true>(a, st);
-      // compute: the lane trees of 4 consecutive windows at once; 28 one tree per window (round 4), 29 8 windows
-      if (!a.expected && v == 29) return launch_crc_stream<4, 2, true, false, 8>(a, st);
-      if (!a.expected && v != 28) return launch_crc_stream<4, 2, true, false, 4>(a, st);
+      // compute: the lane trees of 8 consecutive windows at once (CRC32C 1.361 -> 1.285 ms for 8 GiB, 78.9 -> 83.6 %;
+      // 4 windows 1.293 ms, profiles/r05/crc/); 28 one tree per window (round 4), 29 four windows
+      if (!a.expected && v == 29) return launch_crc_stream<4, 2, true, false, 4>(a, st);
+      if (!a.expected && v != 28) return launch_crc_stream<4, 2, true, false, 8>(a, st);
       return launch_crc_stream<4, 2, true>(a, st);
     }
     // per-window kernel: G26 tables, B = 1 block per lane per step, groups of D = 4 steps, two steps of loads in

@@ -212,7 +212,7 @@ struct TuneKnobs {
 //   gf_variant (coding kernel gf_code_vec, kernels.hip launch_kr): 1, 5, 11
 //   crc_variant, by kernel family:
 //     streaming CRC (launch_crc_windows): 20, 22 -- D-step groups instead of the XO default; 24 -- verify without
-//       the run check (round 4's default); 28 / 29 -- compute with one lane tree per window (round 4) / per 8 windows
+//       the run check (round 4's default); 28 / 29 -- compute with one lane tree per window (round 4) / per 4 windows
 //     fused XOR codec (launch_enc_crc_kr, R = 1 all-ones): 2 no register shortcut, 3 D = 4 with loads one step ahead
 //       (the round-1 default), 4 / 5 XO with D = 4 / 2,
 //       20 / 21 streaming kernel with a ring of 2 / 4 steps

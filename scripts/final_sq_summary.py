@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 PAT = {"c3r": "encode_crc_nb", "c5dev": "encode_crc_nb", "c4": "encode_crc_g26", "c2": "gf_code_vec",
-       "c3": "gf_code_vec", "crc": "crc_windows_g26s"}
+       "c3": "gf_code_vec", "crc": "crc_windows_g26s", "verify": "crc_windows_g26s"}
 root = sys.argv[1]
 out = {}
 for w, pat in PAT.items():

@@ -162,7 +162,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
 }
 
 // Runtime k, R outputs (tables re-read from LDS per input). Used for schemas not instantiated above.
-template <int R>
+// BUF (round 5): cells at any byte offset -- raw buffer loads and stores (32-bit offsets from a rebased CodeArgs,
+// rebase32) instead of typed 16-B pointer accesses, which need 16-B alignment.
+template <int R, bool BUF = false>
 __global__ __launch_bounds__(kBlock) void gf_code_vec_generic(const CodeArgs a, int row0) {
   __shared__ PermTab s_tab[OZEC_MAX_ROWS * OZEC_MAX_K];
   const int k = a.k;
@@ -177,11 +179,18 @@ __global__ __launch_bounds__(kBlock) void gf_code_vec_generic(const CodeArgs a, 
     if (v >= nvec) continue;
     const uint8_t *ib = a.in + in_off(a, s) + static_cast<int64_t>(v) * 16;
     uint8_t *ob = a.out + out_off(a, s) + static_cast<int64_t>(v) * 16;
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, s)), rout = make_rsrc(a.out + out_off(a, s));
     uint4 acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = make_uint4(0, 0, 0, 0);
     for (int j = 0; j < k; ++j) {
-      const uint4 x = *reinterpret_cast<const uint4 *>(ib + a.in_off[j]);
+      uint4 x;
+      if constexpr (BUF) {
+        const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, v * 16u, static_cast<int>(a.in_off[j]), 0);
+        x = make_uint4(d[0], d[1], d[2], d[3]);
+      } else {
+        x = *reinterpret_cast<const uint4 *>(ib + a.in_off[j]);
+      }
       const Sel sx = make_sel(x.x), sy = make_sel(x.y), sz = make_sel(x.z), sw = make_sel(x.w);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -193,14 +202,21 @@ __global__ __launch_bounds__(kBlock) void gf_code_vec_generic(const CodeArgs a, 
       }
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) *reinterpret_cast<uint4 *>(ob + a.out_off[row0 + r]) = acc[r];
+    for (int r = 0; r < R; ++r) {
+      if constexpr (BUF) {
+        __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
+        __builtin_amdgcn_raw_buffer_store_b128(d, rout, v * 16u, static_cast<int>(a.out_off[row0 + r]), 0);
+      } else {
+        *reinterpret_cast<uint4 *>(ob + a.out_off[row0 + r]) = acc[r];
+      }
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) store_data_hold(acc[r]);
   }
 }
 
-// XOR of K inputs (XORRawEncoder / XORRawDecoder): one output.
-template <int K>
+// XOR of K inputs (XORRawEncoder / XORRawDecoder): one output.  BUF: any byte offset, as gf_code_vec_generic.
+template <int K, bool BUF = false>
 __global__ __launch_bounds__(kBlock) void xor_vec(const CodeArgs a) {
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
   const uint32_t cpc = (nvec + kBlock - 1) / kBlock;
@@ -211,18 +227,31 @@ __global__ __launch_bounds__(kBlock) void xor_vec(const CodeArgs a) {
     const uint32_t v = (u - s * cpc) * kBlock + threadIdx.x;
     if (v >= nvec) continue;
     const uint8_t *ib = a.in + in_off(a, s) + static_cast<int64_t>(v) * 16;
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(a.in + in_off(a, s));
     uint4 acc = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < (K > 0 ? K : OZEC_MAX_K); ++j) {
       if (K == 0 && j >= k) break;
-      const uint4 x = *reinterpret_cast<const uint4 *>(ib + a.in_off[j]);
+      uint4 x;
+      if constexpr (BUF) {
+        const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, v * 16u, static_cast<int>(a.in_off[j]), 0);
+        x = make_uint4(d[0], d[1], d[2], d[3]);
+      } else {
+        x = *reinterpret_cast<const uint4 *>(ib + a.in_off[j]);
+      }
       acc.x ^= x.x;
       acc.y ^= x.y;
       acc.z ^= x.z;
       acc.w ^= x.w;
     }
-    *reinterpret_cast<uint4 *>(a.out + out_off(a, s) + a.out_off[0] +
-                               static_cast<int64_t>(v) * 16) = acc;
+    if constexpr (BUF) {
+      __attribute__((ext_vector_type(4))) unsigned int d = {acc.x, acc.y, acc.z, acc.w};
+      __builtin_amdgcn_raw_buffer_store_b128(d, make_rsrc(a.out + out_off(a, s)), v * 16u,
+                                             static_cast<int>(a.out_off[0]), 0);
+      store_data_hold(acc);
+    } else {
+      *reinterpret_cast<uint4 *>(a.out + out_off(a, s) + a.out_off[0] + static_cast<int64_t>(v) * 16) = acc;
+    }
   }
 }
 
@@ -937,26 +966,34 @@ hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
 }
 
 template <int K>
-hipError_t launch_xor(const CodeArgs &a, hipStream_t st) {
+hipError_t launch_xor(const CodeArgs &a, hipStream_t st, bool buf) {
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
   const int64_t units = a.nstripes * ((nvec + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL((xor_vec<K>), dim3(grid_for(units, 1)), dim3(kBlock), 0, st, a);
+  if (buf) {
+    hipLaunchKernelGGL((xor_vec<K, true>), dim3(grid_for(units, 1)), dim3(kBlock), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((xor_vec<K>), dim3(grid_for(units, 1)), dim3(kBlock), 0, st, a);
+  }
   return hipGetLastError();
 }
 
+// aligned layouts keep the typed-pointer kernels measured in rounds 1-4; any other layout whose offsets fit a
+// 32-bit buffer offset after rebase32 runs the BUF instantiations (launch_code checks which applies)
 hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
-  if (a.all_ones && a.rows == 1) {
-    switch (a.k) {
-      case 2: return launch_xor<2>(a, st);
-      case 3: return launch_xor<3>(a, st);
-      case 4: return launch_xor<4>(a, st);
-      case 6: return launch_xor<6>(a, st);
-      case 10: return launch_xor<10>(a, st);
-      default: return launch_xor<0>(a, st);
-    }
-  }
   CodeArgs rb = a;
   const bool fits32 = rebase32(rb);
+  const bool buf = !vec_ok(a);
+  const CodeArgs &x = buf ? rb : a;
+  if (a.all_ones && a.rows == 1) {
+    switch (a.k) {
+      case 2: return launch_xor<2>(x, st, buf);
+      case 3: return launch_xor<3>(x, st, buf);
+      case 4: return launch_xor<4>(x, st, buf);
+      case 6: return launch_xor<6>(x, st, buf);
+      case 10: return launch_xor<10>(x, st, buf);
+      default: return launch_xor<0>(x, st, buf);
+    }
+  }
 #define OZEC_KR(KK, RR) \
   if (fits32 && a.k == KK && a.rows == RR) return launch_kr<KK, RR>(rb, st);
   OZEC_KR(3, 1) OZEC_KR(3, 2)
@@ -968,11 +1005,20 @@ hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
   const unsigned grid = grid_for(units, 1);
   for (int row0 = 0; row0 < a.rows; row0 += 4) {
     const int rr = a.rows - row0 < 4 ? a.rows - row0 : 4;
-    switch (rr) {
-      case 1: hipLaunchKernelGGL(gf_code_vec_generic<1>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
-      case 2: hipLaunchKernelGGL(gf_code_vec_generic<2>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
-      case 3: hipLaunchKernelGGL(gf_code_vec_generic<3>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
-      default: hipLaunchKernelGGL(gf_code_vec_generic<4>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+    if (buf) {
+      switch (rr) {
+        case 1: hipLaunchKernelGGL((gf_code_vec_generic<1, true>), dim3(grid), dim3(kBlock), 0, st, x, row0); break;
+        case 2: hipLaunchKernelGGL((gf_code_vec_generic<2, true>), dim3(grid), dim3(kBlock), 0, st, x, row0); break;
+        case 3: hipLaunchKernelGGL((gf_code_vec_generic<3, true>), dim3(grid), dim3(kBlock), 0, st, x, row0); break;
+        default: hipLaunchKernelGGL((gf_code_vec_generic<4, true>), dim3(grid), dim3(kBlock), 0, st, x, row0); break;
+      }
+    } else {
+      switch (rr) {
+        case 1: hipLaunchKernelGGL(gf_code_vec_generic<1>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+        case 2: hipLaunchKernelGGL(gf_code_vec_generic<2>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+        case 3: hipLaunchKernelGGL(gf_code_vec_generic<3>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+        default: hipLaunchKernelGGL(gf_code_vec_generic<4>, dim3(grid), dim3(kBlock), 0, st, a, row0); break;
+      }
     }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
@@ -980,14 +1026,12 @@ hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
   return hipSuccess;
 }
 
-// the instantiated gf_code_vec shapes read and write through raw buffer descriptors, which take any byte offset
-// (round 5: a packed batch of odd-length cells ran gf_code_bytes at ~5 GB/s, profiles/r05/small/)
-bool kr_any_offset(const CodeArgs &a) {
-  if (a.all_ones && a.rows == 1) return false;  // xor_vec: typed 16-B accesses
-  const bool kr = (a.k == 3 && a.rows >= 1 && a.rows <= 2) || (a.k == 6 && a.rows >= 1 && a.rows <= 3) ||
-                  (a.k == 10 && a.rows >= 1 && a.rows <= 4);
+// the vector kernels read and write through raw buffer descriptors (gf_code_vec; xor_vec and gf_code_vec_generic
+// with BUF), which take any byte offset once the offsets fit 32 bits (round 5: a packed batch of odd-length cells ran
+// gf_code_bytes at ~5 GB/s, profiles/r05/small/)
+bool vec_any_offset(const CodeArgs &a) {
   CodeArgs rb = a;
-  return kr && rebase32(rb);
+  return rebase32(rb);
 }
 
 }  // namespace
@@ -995,7 +1039,7 @@ bool kr_any_offset(const CodeArgs &a) {
 hipError_t launch_code(const CodeArgs &a, hipStream_t st) {
   if (a.len <= 0 || a.nstripes <= 0) return hipSuccess;
   int64_t start = 0;
-  if ((vec_ok(a) || kr_any_offset(a)) && a.len >= 16) {
+  if ((vec_ok(a) || vec_any_offset(a)) && a.len >= 16) {
     hipError_t err = launch_vec(a, st);
     if (err != hipSuccess) return err;
     start = a.len & ~static_cast<int64_t>(15);

@@ -92,6 +92,11 @@ for s in $STEPS; do
         || { tail -20 "$OUT/ab_crc.log"; exit 25; }
       run "ab verify" 300 python -u scripts/ab.py verify crc_variant ${VERIFY:-0,24} ${ROUNDS:-6} > "$OUT/ab_verify.log" \
         2>&1 || { tail -20 "$OUT/ab_verify.log"; exit 26; } ;;
+    oddshapes)  # XOR / generic RS coding at odd byte offsets: previous build (byte kernel) vs this one (BUF kernels)
+      run "odd shapes prev" 300 env OZEC_LIB_OVERRIDE=ab/libozec_prev.so python -u scripts/odd_shapes_ab.py prev \
+        > "$OUT/odd_shapes_prev.json" 2> "$OUT/odd_shapes.err" || exit 27
+      run "odd shapes new" 300 python -u scripts/odd_shapes_ab.py new > "$OUT/odd_shapes_new.json" \
+        2>> "$OUT/odd_shapes.err" || exit 28 ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     tailnp)  # the same with the host batches' device unit pitch = the cell length (host_pitch16=0)

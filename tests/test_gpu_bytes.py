@@ -135,3 +135,41 @@ def test_packed_odd_cells_coding_and_checksum_entry_points(k, p, n):
             assert (units[s, k + q] == ref[q]).all(), (k, p, n, s, q)
         for u, cell in enumerate(list(data[s]) + ref):
             assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (k, p, n, s, u)
+
+
+@pytest.mark.parametrize("codec,k,p", [("xor", 2, 1), ("xor", 3, 1), ("xor", 5, 1), ("rs", 4, 2), ("rs", 5, 6)])
+@pytest.mark.parametrize("n", [16, 1007, 16384 + 3, 700_001])
+def test_packed_odd_cells_xor_and_generic_shapes(codec, k, p, n):
+    """The shapes without a gf_code_vec instantiation -- XOR-k-1 (xor_vec) and RS schemas outside 3/6/10 data units
+    (gf_code_vec_generic; rs-5-6 in two row groups) -- on packed stripes at odd byte offsets run the BUF (raw buffer)
+    instantiations: encode + CRC32C and a decode of the last data unit, vs oracle.xor_* / rs_* and crc_windows,
+    guard bytes untouched."""
+    S, bpc, shift = 3, 16384, 3
+    rng = np.random.default_rng([k, p, n, 11])
+    data = rng.integers(0, 256, (S, k, n), dtype=np.uint8)
+    flat = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
+    flat[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)[:, :k] = data
+    d = torch.from_numpy(flat).to(DEV)
+    base = d[GUARD + shift:]
+    conf = rc.ECReplicationConfig(k, p, codec)
+    nwin = -(-n // bpc)
+    crcs = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    rc.RawErasureEncoder(conf).encode_crc_batch(base, (k + p) * n, n, base[k * n:], (k + p) * n, n, S, n,
+                                                ck.ChecksumType.CRC32C, bpc, crcs)
+    erased = [k - 1]
+    out = torch.zeros((S, 1, n), dtype=torch.uint8, device=DEV)
+    rc.RawErasureDecoder(conf).decode_batch(base, (k + p) * n, n, [u for u in range(k + p) if u != k - 1][:k], erased,
+                                            out, n, n, S, n)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    c = crcs.cpu().numpy().view(np.uint32)
+    o = out.cpu().numpy()
+    assert (got[:GUARD + shift] == 0xA5).all() and (got[GUARD + shift + S * (k + p) * n:] == 0xA5).all()
+    units = got[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
+    for s in range(S):
+        ref = [oracle.xor_encode(list(data[s]))] if codec == "xor" else oracle.rs_encode(k, p, list(data[s]))
+        for q in range(p):
+            assert (units[s, k + q] == ref[q]).all(), (codec, k, p, n, s, q)
+        for u, cell in enumerate(list(data[s]) + list(ref)):
+            assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (codec, k, p, n, s, u)
+        assert (o[s, 0] == data[s, k - 1]).all(), (codec, k, p, n, s)

@@ -3,7 +3,8 @@
 // gf_code_vec geometry), output r = XOR of the inputs (rotated by r): the C2 layout (rs-6-3, parity in place in the
 // 9-unit stripe) and the C3 layout (rs-10-4 decode: 10 of 14 units read, 4 written to a separate buffer), with
 // several block->chunk orders.  Prints one JSON line per case: fraction of 8 TB/s over the algorithmic bytes.
-//   hipcc --offload-arch=gfx950 -O3 scripts/stream_probe.hip -o scripts/stream_probe && scripts/stream_probe
+// With argument "r": read-only streaming over 24 GiB in contiguous chunks per workgroup (the CRC kernels' pattern).
+//   hipcc --offload-arch=gfx950 -O3 scripts/stream_probe.hip -o scripts/stream_probe && scripts/stream_probe [r]
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -73,6 +74,49 @@ __global__ __launch_bounds__(T) void stream(const Layout L) {
   }
 }
 
+// read-only streaming (the CRC kernels' side of the memory system): each workgroup reads CH contiguous bytes, U
+// 16-B loads per lane in flight, XOR-reduces them and stores nothing (a never-true compare keeps the loads live)
+template <int CH, int U>
+__global__ __launch_bounds__(256) void read_only(const uint8_t *p, uint64_t n, uint32_t magic, uint32_t *sink) {
+  const uint32_t q = gridDim.x >> 3;
+  const uint32_t b = blockIdx.x < (q << 3) ? (blockIdx.x & 7) * q + (blockIdx.x >> 3) : blockIdx.x;
+  const auto r = rsrc(p + uint64_t(b) * CH, CH);
+  uint32_t acc = 0;
+  for (int i = 0; i < CH / (256 * 16); i += U) {
+    __attribute__((ext_vector_type(4))) unsigned int d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) d[u] = __builtin_amdgcn_raw_buffer_load_b128(r, ((i + u) * 256 + threadIdx.x) * 16, 0, 2);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+  }
+  if (acc == magic) sink[threadIdx.x] = acc;
+}
+
+template <int CH, int U>
+void run_read(const uint8_t *p, uint64_t n, uint32_t *sink) {
+  const uint32_t grid = static_cast<uint32_t>(n / CH);
+  auto launch = [&]() { hipLaunchKernelGGL((read_only<CH, U>), dim3(grid), dim3(256), 0, 0, p, n, 0x9e3779b9u, sink); };
+  for (int i = 0; i < 3; ++i) launch();
+  CK(hipGetLastError());
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  const int it = 10;
+  CK(hipEventRecord(a));
+  for (int i = 0; i < it; ++i) launch();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  ms /= it;
+  const double bytes = double(grid) * CH;
+  std::printf("{\"case\": \"read only\", \"chunk\": %d, \"loads_in_flight\": %d, \"ms\": %.3f, \"TB/s\": %.3f, "
+              "\"frac_of_8TBps\": %.4f}\n", CH, U, ms, bytes / ms / 1e9, bytes / ms / 1e9 / 8.0);
+  std::fflush(stdout);
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+}
+
 template <int K, int R, int T = 256>
 void run(const char *name, Layout L, int order) {
   const uint32_t units = L.nstripes * (L.len / (T * 16));
@@ -103,8 +147,25 @@ void run(const char *name, Layout L, int order) {
   CK(hipEventDestroy(b));
 }
 
-int main() {
+int main(int argc, char **argv) {
   const uint32_t len = 1u << 20;
+  if (argc > 1 && argv[1][0] == 'r') {  // read-only cases: a 24 GiB buffer, the CRC leg's volume
+    const uint64_t n = uint64_t(24) << 30;
+    uint8_t *p;
+    uint32_t *sink;
+    CK(hipMalloc(&p, n));
+    CK(hipMalloc(&sink, 1024));
+    CK(hipMemset(p, 1, n));
+    run_read<16384, 4>(p, n, sink);
+    run_read<65536, 4>(p, n, sink);
+    run_read<65536, 8>(p, n, sink);
+    run_read<262144, 4>(p, n, sink);
+    run_read<262144, 8>(p, n, sink);
+    run_read<262144, 16>(p, n, sink);
+    CK(hipFree(p));
+    CK(hipFree(sink));
+    return 0;
+  }
   // C2 layout: 2048 stripes of 9 units, parity written in place
   {
     const uint32_t S = 2048;

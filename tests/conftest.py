@@ -34,8 +34,9 @@ def pytest_collection_modifyitems(config, items):
 def _fused_kernels_in_gpu_tests(request):
     """GPU tests run the fused kernels at every batch size: libozec's default sends batches of 16-B cells below
     fused_min_units (stripe x window units) to the unfused kernels, which would take the small parity batches away
-    from the fused kernels and variants they are written for.  tests/test_gpu_bytes.py covers both routes."""
-    if request.node.get_closest_marker("gpu") is None:
+    from the fused kernels and variants they are written for.  tests/test_gpu_bytes.py covers both routes.
+    OZEC_TEST_PRODUCTION_ROUTING=1 keeps libozec's own routing instead (a whole-suite run of the production defaults)."""
+    if request.node.get_closest_marker("gpu") is None or os.environ.get("OZEC_TEST_PRODUCTION_ROUTING") == "1":
         yield
         return
     from ozone_amd import _lib as L

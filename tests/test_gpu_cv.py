@@ -172,3 +172,40 @@ def test_verify_run_check_reports_the_first_failing_window(variant, bpc, ctype, 
         lib.ozec_set_tuning(b"crc_variant", 0)
     assert got.tolist() == want.tolist(), (variant, bpc)
     assert clean.tolist() == [-1] * C
+
+
+@pytest.mark.parametrize("k,p,erased", [(10, 4, [0, 1, 2, 3]), (6, 3, [2, 7])])
+def test_combined_verify_every_stripe_failing(k, p, erased):
+    """Every stripe of the batch fails its combined check (a whole corrupted replica): each is re-verified window by
+    window (nb_reverify, one wave per (input, window)) and reports its own first failing (unit, window), including a
+    corruption in a cell's short last window and one in a virtual-padded first step; the rebuilt units stay exact."""
+    n, bpc, S = 3 * 16384 + 4096, 16384, 6  # a short last window of 4 KiB
+    nwin = -(-n // bpc)
+    units = _units(k, p, n, S, 97000)
+    stored = np.stack([np.stack([oracle.crc_windows(oracle.CRC32C, units[s, u], bpc) for u in range(k + p)])
+                       for s in range(S)]).astype(np.uint32)
+    present = [u for u in range(k + p) if u not in erased]
+    read = present[:k]
+    corrupted = units.copy()
+    corrupted[:, erased] = 0x11
+    rng = np.random.default_rng([k, p, 5])
+    for s in range(S):
+        for _ in range(1 + s % 3):
+            corrupted[s, read[int(rng.integers(0, k))], int(rng.integers(0, n))] ^= int(rng.integers(1, 256))
+    corrupted[S - 1, read[k - 1], n - 1] ^= 0x80  # the short last window of the last read unit
+    lib = L.lib()
+    d_out = torch.zeros((S, len(erased), n), dtype=torch.uint8, device=DEV)
+    d_crc = torch.zeros((S, len(erased), nwin), dtype=torch.int32, device=DEV)
+    mism = torch.zeros(S, dtype=torch.int32, device=DEV)
+    assert lib.ozec_set_tuning(b"crc_variant", 231) == 0
+    try:
+        rc.RawErasureDecoder(rc.ECReplicationConfig(k, p)).reconstruct_crc_batch(
+            torch.from_numpy(corrupted).to(DEV), (k + p) * n, n, present, erased, d_out, len(erased) * n, n, S, n,
+            ck.ChecksumType.CRC32C, bpc, d_crc, d_expected=torch.from_numpy(stored.view(np.int32)).to(DEV),
+            d_mismatch=mism)
+        torch.cuda.synchronize()
+    finally:
+        lib.ozec_set_tuning(b"crc_variant", 0)
+    m = mism.cpu().numpy()
+    for s in range(S):
+        assert m[s] == _first_failure(units[s], corrupted[s], read, nwin, bpc, oracle.CRC32C), (s, m)

@@ -256,6 +256,9 @@ __global__ __launch_bounds__(256) void nb_reverify(const EncCrcArgs e) {
   __shared__ __attribute__((aligned(16))) uint32_t s_t[kG5Words];
   const CodeArgs &a = e.code;
   const CrcArgs &cr = e.crc;
+  bool any = false;  // the common case: no stripe of this block is suspect -- leave before loading the tables
+  for (int64_t s = blockIdx.x; s < a.nstripes && !any; s += gridDim.x) any = cr.mismatch[s] == kMismatchSuspect;
+  if (!any) return;
   load_tables(s_t, cr.tables[0], kG5Words);
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -263,7 +266,11 @@ __global__ __launch_bounds__(256) void nb_reverify(const EncCrcArgs e) {
   const int waves = blockDim.x >> 6;
   const int64_t nwin = cr.nwin;
   for (int64_t s = blockIdx.x; s < a.nstripes; s += gridDim.x) {
-    if (cr.mismatch[s] != kMismatchSuspect) continue;
+    // every wave reads the mark before any wave can lower it (atomicMin below): the barrier keeps a fast wave's first
+    // report from making a slower one skip the stripe
+    const bool suspect = cr.mismatch[s] == kMismatchSuspect;
+    __syncthreads();
+    if (!suspect) continue;
     for (int64_t t = wave; t < a.k * nwin; t += waves) {
       const int j = static_cast<int>(t / nwin);
       const int64_t w = t - j * nwin;

@@ -149,7 +149,62 @@ int main() {
       ++xo_checked;
     }
   }
-  printf("g26 emulation: %d windows bit-exact; nibble tables: %d blocks bit-exact; XO: %d windows bit-exact\n", checked,
-         nib_checked, xo_checked);
+  // G5 scheme of the combined-verify re-check (fused.hip nb_reverify): lane l folds blocks l, l+64, ... -- register
+  // shifted by the 1008-B gap (kG5Step), XORed into the block's first dword, block looked up in the kG5Blk tables --
+  // and the lane tree (kG5Tree, shifts by 16 * 2^m) merges the lanes; windows front-padded with zero blocks
+  int g5_checked = 0;
+  for (int ty = 0; ty < 2; ++ty) {
+    const CrcMath &cm = CrcMath::get(static_cast<CrcType>(ty));
+    const std::vector<uint32_t> &G = cm.device_tables(1);
+    if (static_cast<int>(G.size()) != kG5Words) {
+      printf("G5 blob size mismatch\n");
+      return 1;
+    }
+    auto g5_block = [&](const uint32_t w[4]) {
+      uint32_t r = 0;
+      for (int g = 0; g < 26; ++g) {
+        const int o = 5 * g, d = o >> 5, sh = o & 31;
+        const uint32_t v = (sh <= 27 || d == 3) ? (w[d] >> sh) : ((w[d] >> sh) | (w[d + 1] << (32 - sh)));
+        r ^= G[kG5Blk + g * 32 + (v & 31)];
+      }
+      return r;
+    };
+    for (int m : {1, 5, 63, 64, 65, 256, 257, 1024}) {  // 16-B blocks per window
+      std::vector<uint8_t> buf(static_cast<size_t>(m) * 16);
+      for (auto &x : buf) x = static_cast<uint8_t>(rand());
+      uint32_t ref = 0;
+      for (uint8_t x : buf) ref = (ref >> 8) ^ cm.byte_table((ref ^ x) & 0xff);
+      const long steps = (m + 63) / 64, pad = steps * 64 - m;
+      uint32_t S[64];
+      for (int l = 0; l < 64; ++l) {
+        S[l] = 0;
+        for (long q = 0; q < steps; ++q) {
+          const long vb = q * 64 + l - pad;
+          uint32_t w[4] = {0, 0, 0, 0};
+          if (vb >= 0) memcpy(w, &buf[vb * 16], 16);
+          if (q > 0) S[l] = shift7(G.data() + kG5Step, S[l]);
+          w[0] ^= S[l];
+          S[l] = g5_block(w);
+        }
+      }
+      for (int lv = 0; lv < 6; ++lv) {  // g5_lane_tree: lane l's registers precede lane l + 2^lv's
+        uint32_t nS[64];
+        for (int l = 0; l < 64; ++l) {
+          const int o = l ^ (1 << lv);
+          const bool upper = (l >> lv) & 1;
+          nS[l] = shift7(G.data() + kG5Tree + lv * 224, upper ? S[o] : S[l]) ^ (upper ? S[l] : S[o]);
+        }
+        memcpy(S, nS, sizeof(S));
+      }
+      for (int l = 0; l < 64; ++l)
+        if (S[l] != ref) {
+          printf("FAIL G5 re-check window crc type %d blocks %d lane %d: %08x vs %08x\n", ty, m, l, S[l], ref);
+          return 1;
+        }
+      ++g5_checked;
+    }
+  }
+  printf("g26 emulation: %d windows bit-exact; nibble tables: %d blocks bit-exact; XO: %d windows bit-exact; "
+         "G5 re-check: %d windows bit-exact\n", checked, nib_checked, xo_checked, g5_checked);
   return 0;
 }

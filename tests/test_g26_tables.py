@@ -19,4 +19,4 @@ def test_g26_host_emulation(tmp_path):
                            os.path.join(CSRC, "crc_host.cpp")])
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr
-    assert "bit-exact" in out.stdout and "XO:" in out.stdout
+    assert "bit-exact" in out.stdout and "XO:" in out.stdout and "G5 re-check:" in out.stdout

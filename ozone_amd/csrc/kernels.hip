@@ -541,25 +541,6 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int6
   }
 }
 
-// Scalar fallback: one thread per window, byte-at-a-time (any alignment, any bpc).
-__global__ __launch_bounds__(kBlock) void crc_windows_bytes(const CrcArgs a) {
-  __shared__ uint32_t s_t0[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_t0[i] = a.tables[0][kG5T0 + i];
-  __syncthreads();
-  const int64_t units = a.ncells * a.nwin;
-  for (int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; u < units;
-       u += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t c = u / a.nwin;
-    const int64_t w = u - c * a.nwin;
-    const bool last = w == a.nwin - 1;
-    const int64_t N = last ? a.len - w * a.bpc : a.bpc;
-    const uint8_t *win = a.base + c * a.cell_stride + w * a.bpc;
-    uint32_t S = 0;
-    for (int64_t i = 0; i < N; ++i) S = (S >> 8) ^ s_t0[(S ^ win[i]) & 0xff];
-    crc_emit(a, c, w, S, last);
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // Fused encode + CRC: one wave per (stripe, window); each step a lane takes the 16-B blocks of every data unit
 // (lanes interleaved, 64 blocks per step), produces the parity blocks and folds all K+R units into their CRC
@@ -1133,15 +1114,15 @@ hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t st) {
     const int64_t g = cg > 0 ? cg : 16384;
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
     hipLaunchKernelGGL((crc_windows_g26<1, 4, 2>), grid, block, 0, st, a);
-  } else if (aligned16(a.bpc)) {
-    // cells at unaligned offsets (a packed batch of odd-length cells): the per-window kernel with align-1 loads.  The
-    // byte-at-a-time kernel below ran 16 KiB windows one thread each
+  } else {
+    // cells at unaligned offsets (a packed batch of odd-length cells) and windows of any length (bpc not a multiple of
+    // 16: every window starts at its own byte offset): the per-window kernel with align-1 loads, each window's last
+    // 1-15 bytes folded bytewise after the lane tree.  (Until round 5 these ran a byte-at-a-time kernel, one thread
+    // per window.)
     const int64_t cg = g_tune.crc_grid;
     const int64_t g = cg > 0 ? cg : 16384;
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, (units + 3) / 4)))), block(kBlock);
     hipLaunchKernelGGL((crc_windows_g26<1, 4, 2, true>), grid, block, 0, st, a);
-  } else {
-    hipLaunchKernelGGL(crc_windows_bytes, dim3(grid_for(units, kBlock)), dim3(kBlock), 0, st, a);
   }
   return hipGetLastError();
 }

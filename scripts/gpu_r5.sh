@@ -97,6 +97,10 @@ for s in $STEPS; do
         > "$OUT/odd_shapes_prev.json" 2> "$OUT/odd_shapes.err" || exit 27
       run "odd shapes new" 300 python -u scripts/odd_shapes_ab.py new > "$OUT/odd_shapes_new.json" \
         2>> "$OUT/odd_shapes.err" || exit 28 ;;
+    oddbpc)  # CRC windows of any length / at odd offsets: previous build (byte kernel) vs this one (per-window kernel)
+      run "odd bpc prev" 300 env OZEC_LIB_OVERRIDE=ab/libozec_prev.so python -u scripts/odd_bpc_ab.py prev \
+        > "$OUT/odd_bpc_prev.json" 2> "$OUT/odd_bpc.err" || exit 29
+      run "odd bpc new" 300 python -u scripts/odd_bpc_ab.py new > "$OUT/odd_bpc_new.json" 2>> "$OUT/odd_bpc.err" || exit 30 ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     tailnp)  # the same with the host batches' device unit pitch = the cell length (host_pitch16=0)

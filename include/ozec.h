@@ -131,8 +131,8 @@ int ozec_decode_device(ozec_coder *dec, const uint8_t *const *d_inputs, const in
 
 /* Batched stripes, the layout the datanode/bench keeps in HBM: unit u (0 <= u < k+p) of stripe s lives at
  *   base + s * stripe_stride + u * unit_stride            (bytes; any strides and lengths.  Every schema and
- *   the XOR codec run their 16-B vector kernels at any byte offset -- raw buffer accesses, DESIGN.md §3 --
- *   while a batch's unit offsets span less than 2 GiB; the last 1-15 bytes of a cell go bytewise)
+ *   the XOR codec run their 16-B vector kernels at any byte offset and unit spacing; the last
+ *   1-15 bytes of a cell go bytewise)
  * encode reads units 0..k-1 of `d_in` and writes parity unit j to d_out + s*out_stripe_stride + j*out_unit_stride.
  * This is the batch entry SURVEY.md §7 "One stripe per call" asks for; the per-stripe semantics are exactly
  * RSUtil.encodeData's. */

@@ -39,7 +39,11 @@ namespace {
 // cache-policy bits of the loads/stores (0 = default, 2 = nt).
 // OPT bit 0: parity dwords in three-input XOR chains across the K inputs (1.5 VALU per coefficient and dword instead
 // of 2); bit 1: selector masks held in VGPRs (plain VOP2 AND instead of the literal-operand form).
-template <int K, int R, bool SREG, int VPT, int LAUX, int SAUX, int OPT = 0>
+// WIDE (round 5): one buffer descriptor per unit (its own 64-bit base, soffset 0) instead of one per stripe side with
+// 32-bit unit offsets -- for units 2 GiB or more apart (separately allocated cells, a stripe spread over a large HBM
+// pool), which rebase32 cannot bring into 32 bits.  The descriptors take the SGPRs the register-table form keeps its
+// tables in, so WIDE reads the tables from LDS.
+template <int K, int R, bool SREG, int VPT, int LAUX, int SAUX, int OPT = 0, bool WIDE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_WAVES, 8))) void gf_code_vec(
     const CodeArgs a, const TabArgs<K * R> tabs) {
   __shared__ __attribute__((aligned(16))) uint32_t s_w[5][K * R];
@@ -81,8 +85,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
       if (v < nvec) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, v * 16u, static_cast<int>(a.in_off[j]), LAUX);
-          x[q][j] = make_uint4(d[0], d[1], d[2], d[3]);
+          if constexpr (WIDE) {
+            const auto d = __builtin_amdgcn_raw_buffer_load_b128(
+                make_rsrc_n(a.in + in_off(a, s) + a.in_off[j], static_cast<uint32_t>(a.len)), v * 16u, 0, LAUX);
+            x[q][j] = make_uint4(d[0], d[1], d[2], d[3]);
+          } else {
+            const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, v * 16u, static_cast<int>(a.in_off[j]), LAUX);
+            x[q][j] = make_uint4(d[0], d[1], d[2], d[3]);
+          }
         }
       }
     }
@@ -155,7 +165,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OZEC_GF_
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
-        __builtin_amdgcn_raw_buffer_store_b128(d, rout, v * 16u, static_cast<int>(a.out_off[r]), SAUX);
+        if constexpr (WIDE) {
+          __builtin_amdgcn_raw_buffer_store_b128(
+              d, make_rsrc_n(a.out + out_off(a, s) + a.out_off[r], static_cast<uint32_t>(a.len)), v * 16u, 0, SAUX);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(d, rout, v * 16u, static_cast<int>(a.out_off[r]), SAUX);
+        }
       }
     }
   }
@@ -188,8 +203,8 @@ __global__ __launch_bounds__(kBlock) void gf_code_vec_generic(const CodeArgs a, 
       if constexpr (BUF) {
         const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, v * 16u, static_cast<int>(a.in_off[j]), 0);
         x = make_uint4(d[0], d[1], d[2], d[3]);
-      } else {
-        x = *reinterpret_cast<const uint4 *>(ib + a.in_off[j]);
+      } else {  // align-1 copy: global_load_dwordx4 at any byte address (gfx950 unaligned access mode)
+        __builtin_memcpy(&x, ib + a.in_off[j], 16);
       }
       const Sel sx = make_sel(x.x), sy = make_sel(x.y), sz = make_sel(x.z), sw = make_sel(x.w);
 #pragma unroll
@@ -207,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void gf_code_vec_generic(const CodeArgs a, 
         __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
         __builtin_amdgcn_raw_buffer_store_b128(d, rout, v * 16u, static_cast<int>(a.out_off[row0 + r]), 0);
       } else {
-        *reinterpret_cast<uint4 *>(ob + a.out_off[row0 + r]) = acc[r];
+        __builtin_memcpy(ob + a.out_off[row0 + r], &acc[r], 16);
       }
     }
 #pragma unroll
@@ -236,8 +251,8 @@ __global__ __launch_bounds__(kBlock) void xor_vec(const CodeArgs a) {
       if constexpr (BUF) {
         const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, v * 16u, static_cast<int>(a.in_off[j]), 0);
         x = make_uint4(d[0], d[1], d[2], d[3]);
-      } else {
-        x = *reinterpret_cast<const uint4 *>(ib + a.in_off[j]);
+      } else {  // align-1 copy: global_load_dwordx4 at any byte address (gfx950 unaligned access mode)
+        __builtin_memcpy(&x, ib + a.in_off[j], 16);
       }
       acc.x ^= x.x;
       acc.y ^= x.y;
@@ -250,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void xor_vec(const CodeArgs a) {
                                              static_cast<int>(a.out_off[0]), 0);
       store_data_hold(acc);
     } else {
-      *reinterpret_cast<uint4 *>(a.out + out_off(a, s) + a.out_off[0] + static_cast<int64_t>(v) * 16) = acc;
+      __builtin_memcpy(a.out + out_off(a, s) + a.out_off[0] + static_cast<int64_t>(v) * 16, &acc, 16);
     }
   }
 }
@@ -913,17 +928,21 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix64(uint8_t *base, int64_t
   }
 }
 
-template <int K, int R, int VPT, int LAUX, int SAUX, int OPT = 0>
+// WIDE instantiations: up to 18 coefficients (rs-3-x, rs-6-x, rs-10-1); rs-10-2..4 spilled 16-97 VGPRs in that form
+// and keep the typed-pointer kernel (aligned) or the byte kernel (odd offsets) for units 2 GiB apart
+constexpr int kWideMaxKR = 18;
+
+template <int K, int R, int VPT, int LAUX, int SAUX, int OPT = 0, bool WIDE = false>
 hipError_t launch_krv(const CodeArgs &a, hipStream_t st, int64_t default_grid) {
-  constexpr bool kSreg = K * R <= 18;
+  constexpr bool kSreg = K * R <= 18 && !WIDE;
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
   const int64_t units = a.nstripes * ((nvec + kBlock * VPT - 1) / (kBlock * VPT));
   const TabArgs<K * R> tabs = host_tabs<K * R>(a);
   const int64_t tg = g_tune.grid;
   int64_t grid = tg > 0 ? tg : default_grid;
   grid = std::max<int64_t>(1, std::min<int64_t>(grid, units));
-  hipLaunchKernelGGL((gf_code_vec<K, R, kSreg, VPT, LAUX, SAUX, OPT>), dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0,
-                     st, a, tabs);
+  hipLaunchKernelGGL((gf_code_vec<K, R, kSreg, VPT, LAUX, SAUX, OPT, WIDE>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
+                     0, st, a, tabs);
   return hipGetLastError();
 }
 
@@ -963,7 +982,7 @@ hipError_t launch_xor(const CodeArgs &a, hipStream_t st, bool buf) {
 hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
   CodeArgs rb = a;
   const bool fits32 = rebase32(rb);
-  const bool buf = !vec_ok(a);
+  const bool buf = fits32 && !vec_ok(a);  // BUF needs 32-bit offsets; the typed kernels (align-1 copies) take any
   const CodeArgs &x = buf ? rb : a;
   if (a.all_ones && a.rows == 1) {
     switch (a.k) {
@@ -975,8 +994,12 @@ hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
       default: return launch_xor<0>(x, st, buf);
     }
   }
-#define OZEC_KR(KK, RR) \
-  if (fits32 && a.k == KK && a.rows == RR) return launch_kr<KK, RR>(rb, st);
+#define OZEC_KR(KK, RR)                                                                                           \
+  if (a.k == KK && a.rows == RR) {                                                                                  \
+    if (fits32) return launch_kr<KK, RR>(rb, st);                                                                   \
+    if constexpr (KK * RR <= kWideMaxKR)                                                                           \
+      if (a.len < (int64_t{1} << 31)) return launch_krv<KK, RR, 1, 2, 2, 0, true>(a, st, int64_t{1} << 40);         \
+  }
   OZEC_KR(3, 1) OZEC_KR(3, 2)
   OZEC_KR(6, 1) OZEC_KR(6, 2) OZEC_KR(6, 3)
   OZEC_KR(10, 1) OZEC_KR(10, 2) OZEC_KR(10, 3) OZEC_KR(10, 4)
@@ -1007,20 +1030,15 @@ hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
   return hipSuccess;
 }
 
-// the vector kernels read and write through raw buffer descriptors (gf_code_vec; xor_vec and gf_code_vec_generic
-// with BUF), which take any byte offset once the offsets fit 32 bits (round 5: a packed batch of odd-length cells ran
-// gf_code_bytes at ~5 GB/s, profiles/r05/small/)
-bool vec_any_offset(const CodeArgs &a) {
-  CodeArgs rb = a;
-  return rebase32(rb);
-}
-
 }  // namespace
 
 hipError_t launch_code(const CodeArgs &a, hipStream_t st) {
   if (a.len <= 0 || a.nstripes <= 0) return hipSuccess;
   int64_t start = 0;
-  if ((vec_ok(a) || vec_any_offset(a)) && a.len >= 16) {
+  // every layout runs the 16-B vector kernels (round 5): buffer descriptors at any byte offset while the unit offsets
+  // fit 32 bits, gf_code_vec's WIDE form or the typed kernels' align-1 copies beyond (a packed batch of odd-length
+  // cells ran gf_code_bytes at ~5 GB/s, profiles/r05/small/); the byte kernel takes the last 1-15 bytes of a cell
+  if (a.len >= 16) {
     hipError_t err = launch_vec(a, st);
     if (err != hipSuccess) return err;
     start = a.len & ~static_cast<int64_t>(15);

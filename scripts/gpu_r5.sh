@@ -101,6 +101,10 @@ for s in $STEPS; do
       run "odd bpc prev" 300 env OZEC_LIB_OVERRIDE=ab/libozec_prev.so python -u scripts/odd_bpc_ab.py prev \
         > "$OUT/odd_bpc_prev.json" 2> "$OUT/odd_bpc.err" || exit 29
       run "odd bpc new" 300 python -u scripts/odd_bpc_ab.py new > "$OUT/odd_bpc_new.json" 2>> "$OUT/odd_bpc.err" || exit 30 ;;
+    wide)  # coding with units 2 GiB or more apart: previous build (typed / byte kernels) vs this one (WIDE)
+      run "wide prev" 300 env OZEC_LIB_OVERRIDE=ab/libozec_prev.so python -u scripts/wide_ab.py prev \
+        > "$OUT/wide_prev.json" 2> "$OUT/wide.err" || exit 31
+      run "wide new" 300 python -u scripts/wide_ab.py new > "$OUT/wide_new.json" 2>> "$OUT/wide.err" || exit 32 ;;
     tail)
       run tail 300 python -u bench.py --workload tail > "$OUT/bench_tail.json" 2> "$OUT/bench_tail.err" || exit 6 ;;
     tailnp)  # the same with the host batches' device unit pitch = the cell length (host_pitch16=0)

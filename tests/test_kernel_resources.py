@@ -64,8 +64,21 @@ def test_fused_defaults_no_scratch(kernels, pat):
 def test_coding_kernel_defaults_no_scratch(kernels, K, R):
     """gf_code_vec<K, R, K * R <= 18, 1, 2, 2, 0>: the coding kernel of C1-C3 (one vector per thread; coefficient
     tables in SGPRs up to 18 coefficients, kernels.hip launch_krv)."""
-    pat = "gf_code_vecI" + "".join([_i(K), _i(R), _b(K * R <= 18), _i(1), _i(2), _i(2), _i(0)])
+    pat = "gf_code_vecI" + "".join([_i(K), _i(R), _b(K * R <= 18), _i(1), _i(2), _i(2), _i(0), _b(0)]) + "EEvN"
     found = [k for k in kernels if pat in k["name"]]
     assert found, pat
     for k in found:
         assert k.get("private_segment_fixed_size") == 0 and k.get("vgpr_spill_count") == 0, k
+
+
+@pytest.mark.parametrize("K,R", [(3, 1), (3, 2), (6, 1), (6, 2), (6, 3), (10, 1)])
+def test_wide_coding_kernels_no_scratch(kernels, K, R):
+    """gf_code_vec<K, R, false, 1, 2, 2, 0, WIDE>: one descriptor per unit for units 2 GiB or more apart, instantiated
+    up to 18 coefficients (kernels.hip kWideMaxKR; rs-10-2..4 spilled in that form and are not instantiated)."""
+    pat = "gf_code_vecI" + "".join([_i(K), _i(R), _b(0), _i(1), _i(2), _i(2), _i(0), _b(1)]) + "EEvN"
+    found = [k for k in kernels if pat in k["name"]]
+    assert found, pat
+    for k in found:
+        assert k.get("private_segment_fixed_size") == 0 and k.get("vgpr_spill_count") == 0, k
+    assert not [k for k in kernels if "gf_code_vecI" + _i(10) + _i(4) in k["name"] and k["name"].endswith(
+        _b(1) + "EEvNS_8CodeArgsENS0_7TabArgsIXmlT_T0_EEE")], "rs-10-4 WIDE instantiated"

@@ -42,6 +42,9 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from devcopy import to_dev, to_host  # noqa: E402  (host <-> device through pinned staging, never a pageable DMA)
+
 MIB = 1 << 20
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 SEED = 0x00EC5EED
@@ -75,6 +78,9 @@ def parse(argv=None):
     ap.add_argument("--no-inproc", action="store_true",
                     help="skip the in-process multi-GPU C5 leg (one process, libozec's device list over all N GPUs)")
     ap.add_argument("--no-jni", action="store_true", help="skip the JNI per-call rows of the default line")
+    ap.add_argument("--full-line", action="store_true",
+                    help="print the whole record on stdout (default: a compact line, the record in gpurun_out/"
+                         "bench_full.json or $OZEC_BENCH_FULL)")
     ap.add_argument("--e2e-stripes", type=int, default=8192, help="C5 batch size (all GPUs together)")
     ap.add_argument("--e2e-steps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0, help="C5: stripes per pipelined chunk (0 = library default)")
@@ -607,10 +613,10 @@ def e2e_leg(args, rank, world, dist, dev, backend, cpu_group=None):
         ok = True
         if mine:
             last = np.frombuffer((ctypes.c_uint8 * sb).from_address(d0 + (mine - 1) * sb), np.uint8).reshape(9, n)
-            cells = torch.from_numpy(last[:k].copy()).cuda().unsqueeze(0)
+            cells = to_dev(last[:k], f"cuda:{dev}").unsqueeze(0)
             par = enc.encode_stripes(cells)
             torch.cuda.synchronize()
-            ok = bool((par[0].cpu().numpy() == last[k:]).all())
+            ok = bool((to_host(par[0]) == last[k:]).all())
         res = {"workload": "rs-6-3-1024k encode + CRC32C/16 KiB, one batch of %d stripes in shared host memory, "
                            "contiguous stripe range per GPU, pinned NUMA-local pages, H2D + fused kernel + D2H "
                            "(BASELINE configs[4])" % S,
@@ -714,10 +720,10 @@ def in_process_leg(args, hb, rank, world, dist, cpu_group, pc):
                 if hi > lo:
                     last = np.frombuffer((ctypes.c_uint8 * sb).from_address(base + (hi - 1) * sb), np.uint8).reshape(
                         hb.units, n)
-                    cells = torch.from_numpy(last[:k].copy()).cuda().unsqueeze(0)
+                    cells = to_dev(last[:k], f"cuda:{d}").unsqueeze(0)
                     par = enc.encode_stripes(cells)
                     torch.cuda.synchronize()
-                    ok = ok and bool((par[0].cpu().numpy() == last[k:]).all())
+                    ok = ok and bool((to_host(par[0]) == last[k:]).all())
         finally:
             rc.set_devices([devs[0]])
             L.ozec_set_device_policy(prev_policy)
@@ -1330,6 +1336,80 @@ def gather_per_rank(rec, dist):
     return {k: [r[k] for r in recs] for k in rec}
 
 
+def _r(v, nd=4):
+    return round(v, nd) if isinstance(v, float) else v
+
+
+def compact_line(full, full_path):
+    """The stdout line of the default run, kept well under the driver's 9 KB tail: every leg as
+    one short object (leg, erasure set, kernel, kernel_ms, frac, rocprof_avg_ms, traffic over algorithmic bytes), the
+    headline roofline without its PMC detail, the C5 legs, JNI per-call rows as us per stripe, the CPU baseline without
+    its host block.  The full record (PMC blocks, per-rank detail, every JNI row) goes to `full_path`."""
+    out = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "n_ranks", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data") if k in full}
+    cfg = full.get("config", {})
+    out["config"] = {k: cfg[k] for k in ("workload", "cell_bytes", "stripes", "global_stripes", "parallelism") if k in cfg}
+    rf = full.get("roofline", {})
+    out["roofline"] = {k: _r(rf[k]) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                             "kernel_ms", "alg_bytes_per_launch", "rocprof_avg_ms", "frac_rocprof_avg")
+                       if k in rf}
+    if isinstance(rf.get("pmc"), dict) and "traffic_over_algorithmic" in rf["pmc"]:
+        out["roofline"]["traffic_over_algorithmic"] = rf["pmc"]["traffic_over_algorithmic"]
+    if "per_rank" in full:
+        out["per_rank"] = {k: full["per_rank"][k] for k in ("elapsed_s", "kernel_ms", "numa_node") if k in full["per_rank"]}
+    legs = []
+    for lg in full.get("legs", []):
+        if "leg" not in lg:
+            legs.append({k: str(v)[:200] for k, v in lg.items()})
+            continue
+        c = {"leg": lg["leg"], "kernel": lg.get("kernel", "").split(" (")[0], "value": lg.get("value"),
+             "kernel_ms": lg.get("kernel_ms"), "frac": lg.get("frac"), "rocprof_avg_ms": lg.get("rocprof_avg_ms"),
+             "frac_rocprof_avg": lg.get("frac_rocprof_avg")}
+        pm = lg.get("pmc")
+        if isinstance(pm, dict) and "traffic_over_algorithmic" in pm:
+            c["traffic_over_algorithmic"] = pm["traffic_over_algorithmic"]
+        for k in ("verified", "error"):
+            if k in lg:
+                c[k] = lg[k]
+        legs.append(c)
+    if legs:
+        out["legs"] = legs
+    for key in ("e2e", "e2e_in_process"):
+        e = full.get(key)
+        if isinstance(e, dict):
+            c = {k: e[k] for k in ("value", "unit", "ms_per_step", "frac_of_duplex_h2d_link", "parity_spot_check",
+                                   "error") if k in e}
+            if isinstance(e.get("cpu_baseline"), dict):
+                c["cpu_baseline_GBps"] = e["cpu_baseline"].get("value")
+            out[key] = c
+    jp = full.get("jni_percall")
+    if isinstance(jp, dict) and "rows" in jp:
+        out["jni_percall_us"] = {f"{r['mode']} {r['cell_bytes'] >> 10}K x{r['threads']}": r["us_per_stripe"]
+                                 for r in jp["rows"]}
+        out["jni_percall_ok"] = all(r.get("round_trip_ok", True) for r in jp["rows"])
+    elif jp is not None:
+        out["jni_percall"] = str(jp)[:300]
+    cb = full.get("cpu_baseline")
+    if isinstance(cb, dict):
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "value_1_thread", "sample") if k in cb}
+    if "verified" in full:
+        out["verified"] = full["verified"]
+    out["full_record"] = full_path
+    return out
+
+
+def emit_default(result):
+    """rank 0 of the default (c2) run: the full record to a file, the compact line to stdout."""
+    path = os.environ.get("OZEC_BENCH_FULL", os.path.join(ROOT, "gpurun_out", "bench_full.json"))
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(result, f, indent=1)
+    except OSError as e:
+        path = f"(not written: {e})"
+    emit(compact_line(result, os.path.relpath(path, ROOT) if os.path.isabs(path) else path))
+
+
 def emit(obj):
     line = (json.dumps(obj) + "\n").encode()
     if _JSON_FD is None:
@@ -1515,7 +1595,10 @@ def main():
             if "e2e" in result and "value" in result["e2e"]:
                 result["e2e"]["cpu_baseline"] = cpu_baseline("c5", args.cpu_seconds)
     if rank == 0:
-        emit(result)
+        if args.workload == "c2" and not args.full_line:
+            emit_default(result)
+        else:
+            emit(result)
     if dist is not None:
         dist.destroy_process_group()
     return 0

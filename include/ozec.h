@@ -59,7 +59,10 @@ int ozec_version(void);
  * CodecUtil.createRawEncoderWithFallback, EC/rawcoder/util/CodecUtil.java:55-82) */
 int ozec_device_count(void);
 /* hipSetDevice for the calling thread: the device of its device-pointer calls, and under OZEC_DEVICE_POLICY_CURRENT of
- * the coders it creates and its host calls */
+ * the coders it creates and its host calls.  In a process that chose no device list or policy (ozec_set_devices,
+ * ozec_set_device_policy, OZEC_DEVICES, OZEC_DEVICE_POLICY), the first call also switches the PROCESS-WIDE policy to
+ * OZEC_DEVICE_POLICY_CURRENT (the one-process-per-GPU model): from then on every thread's new coders go to that
+ * thread's current device.  A device list or policy chosen later replaces that implicit policy. */
 int ozec_set_device(int device);
 /* ---- the GPUs of one drop-in process (one JVM per datanode / client drives every GPU of the node):
  * the device list is every visible GPU, or the OZEC_DEVICES environment variable ("0,2,5" / "all"), or this call
@@ -378,6 +381,9 @@ void ozec_stats_reset(void);
  * cached hipGraph of its H2D + kernel + D2H, default 256 KiB, 0 = off).  OZEC_EINVAL for an unknown key, a value out of range, or a kernel variant the library
  * does not hold. */
 int ozec_set_tuning(const char *key, int64_t value);
+/* the current value of a knob ozec_set_tuning sets (every key but "copy_threads" / "copy_stream"); OZEC_EINVAL for
+ * any other key */
+int ozec_get_tuning(const char *key, int64_t *value);
 /* the kernel variants "gf_variant" / "crc_variant" accept besides 0: writes up to cap ids, returns how many exist */
 int ozec_tuning_variants(const char *key, int *ids, int cap);
 /* fill n bytes with splitmix64 stream `stream_id` of `seed` (tests/golden/synth.py is the CPU twin) */

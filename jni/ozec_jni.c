@@ -34,6 +34,7 @@
 #define MAX_BUFS 256
 
 static void throw_status(JNIEnv *env, const ozm_status *st) {
+  if ((*env)->ExceptionCheck(env)) return;  /* the pending one (e.g. a refused array pin's OutOfMemoryError) stands */
   jclass c = (*env)->FindClass(env, st->exception_class);
   if (!c) { /* e.g. HadoopIllegalArgumentException absent from the class path: its superclass */
     (*env)->ExceptionClear(env);
@@ -252,20 +253,22 @@ static int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
  * NUMA node, as its own staging copies are -- instead of one GetByteArrayRegion after another on the calling thread:
  * one rs-6-3 stripe of 1 MiB heap cells spends ~150 us in that single-threaded copy-in (bench.py jni rows).  Nothing
  * in a critical section calls JNI or waits for a Java thread (the pool's workers are native threads).  An array the VM
- * will not hand out (NULL) falls back to Get/SetByteArrayRegion. */
-static void copy_regions(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl,
-                         const ozm_buf *stage, int in) {
+ * will not hand out (NULL) ends the pinning: the arrays already held are released, and with no exception pending every
+ * region is moved by Get/SetByteArrayRegion instead.  Returns 0, or -1 with a Java exception pending (typically the
+ * OutOfMemoryError of a refused pin): the caller then makes no further JNI call but returns to Java. */
+static int copy_regions(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl,
+                        const ozm_buf *stage, int in) {
   void *pin[MAX_BUFS] = {0};
   void *dst[MAX_BUFS];
   const void *src[MAX_BUFS];
   size_t nb[MAX_BUFS];
-  int n = 0, slow = 0;
-  for (int i = 0; i < as->n; ++i) {
+  int n = 0, refused = 0;
+  for (int i = 0; i < as->n && !refused; ++i) {
     if (!as->arr[i] || !stage[i].present) continue;
     pin[i] = (*env)->GetPrimitiveArrayCritical(env, as->arr[i], NULL);
     if (!pin[i]) {
-      slow = 1;
-      continue;
+      refused = 1;
+      break;
     }
     uint8_t *arr = (uint8_t *)pin[i] + bufs[i].offset + off;
     dst[n] = in ? (void *)stage[i].base : (void *)arr;
@@ -273,24 +276,27 @@ static void copy_regions(JNIEnv *env, const array_set *as, const ozm_buf *bufs, 
     nb[n] = (size_t)cl;
     ++n;
   }
-  const int rc = n ? ozec_host_copy(dst, src, nb, n, in) : 0;
-  for (int i = 0; i < as->n; ++i)
-    if (pin[i]) (*env)->ReleasePrimitiveArrayCritical(env, as->arr[i], pin[i], in ? JNI_ABORT : 0);
-  if (!slow && !rc) return;
-  for (int i = 0; i < as->n; ++i) {  /* the arrays not copied above, or all of them if the pool failed */
-    if (!as->arr[i] || !stage[i].present || (pin[i] && !rc)) continue;
+  const int rc = n && !refused ? ozec_host_copy(dst, src, nb, n, in) : 0;
+  for (int i = 0; i < as->n; ++i)  /* nothing was copied when a pin was refused: release without write-back */
+    if (pin[i]) (*env)->ReleasePrimitiveArrayCritical(env, as->arr[i], pin[i], in || refused ? JNI_ABORT : 0);
+  if (!refused && !rc) return 0;
+  if ((*env)->ExceptionCheck(env)) return -1;  /* no JNI call but the few allowed with an exception pending */
+  for (int i = 0; i < as->n; ++i) {  /* every array region, one JNI copy each */
+    if (!as->arr[i] || !stage[i].present) continue;
     if (in)
       (*env)->GetByteArrayRegion(env, as->arr[i], (jsize)(bufs[i].offset + off), (jsize)cl, (jbyte *)stage[i].base);
     else
       (*env)->SetByteArrayRegion(env, as->arr[i], (jsize)(bufs[i].offset + off), (jsize)cl,
                                  (const jbyte *)stage[i].base);
+    if ((*env)->ExceptionCheck(env)) return -1;
   }
+  return 0;
 }
 
 /* the present arrays' regions [offset + off, + cl) into consecutive arena slots of `stride` bytes from slot `first`
  * (absent ones take no slot); stage[i] describes the copy as a buffer at offset 0 */
-static void copy_in(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl, uint8_t *base,
-                    int64_t stride, int first, ozm_buf *stage) {
+static int copy_in(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl, uint8_t *base,
+                   int64_t stride, int first, ozm_buf *stage) {
   int slot = first;
   for (int i = 0; i < as->n; ++i) {
     memset(&stage[i], 0, sizeof(stage[i]));
@@ -299,7 +305,7 @@ static void copy_in(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64
     stage[i].base = base + (int64_t)slot++ * stride;
     stage[i].capacity = cl;
   }
-  copy_regions(env, as, bufs, off, cl, stage, 1);
+  return copy_regions(env, as, bufs, off, cl, stage, 1);
 }
 
 static void out_slots(const array_set *as, int64_t cl, uint8_t *base, int64_t stride, int first, ozm_buf *stage) {
@@ -311,9 +317,9 @@ static void out_slots(const array_set *as, int64_t cl, uint8_t *base, int64_t st
   }
 }
 
-static void copy_out(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl,
-                     const ozm_buf *stage) {
-  copy_regions(env, as, bufs, off, cl, stage, 0);
+static int copy_out(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl,
+                    const ozm_buf *stage) {
+  return copy_regions(env, as, bufs, off, cl, stage, 0);
 }
 
 static int present_count(const array_set *as) {
@@ -338,11 +344,14 @@ static int heap_code(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_
       rc = st->code;
       break;
     }
-    copy_in(env, ai, ib, off, cl, a, stride, 0, si);
+    if (copy_in(env, ai, ib, off, cl, a, stride, 0, si)) {
+      rc = ozm_fail(OZEC_ENOMEM, "a Java array could not be read", st);  /* its exception is pending */
+      break;
+    }
     out_slots(ao, cl, a, stride, nin, so);
     rc = erased ? ozm_decode(h, si, ai->n, erased, ne, so, ao->n, cl, st)
                 : ozm_encode(h, si, ai->n, so, ao->n, cl, st);
-    if (!rc) copy_out(env, ao, ob, off, cl, so);
+    if (!rc && copy_out(env, ao, ob, off, cl, so)) rc = ozm_fail(OZEC_ENOMEM, "a Java array could not be written", st);
   }
   arena_lease_end(&l);
   return rc;

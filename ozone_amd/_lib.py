@@ -146,6 +146,7 @@ _SIGS = {
     "ozec_stats": (ctypes.c_int, [ctypes.c_int, c_voidp]),
     "ozec_stats_reset": (None, []),
     "ozec_set_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
+    "ozec_get_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "ozec_tuning_variants": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "ozec_set_devices": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     "ozec_get_devices": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),

@@ -2022,6 +2022,32 @@ int ozec_set_tuning(const char *key, int64_t value) {
   return OZEC_OK;
 }
 
+int ozec_get_tuning(const char *key, int64_t *value) {
+  if (!key || !value) return fail(OZEC_EINVAL, "null argument");
+  const std::string k(key);
+  const auto &t = ozec::g_tune;
+  if (k == "gf_variant") *value = t.gf_variant.load();
+  else if (k == "crc_variant") *value = t.crc_variant.load();
+  else if (k == "grid") *value = t.grid.load();
+  else if (k == "crc_grid") *value = t.crc_grid.load();
+  else if (k == "crc_run") *value = t.crc_run.load();
+  else if (k == "unit_map") *value = t.unit_map.load();
+  else if (k == "host_chunk") *value = t.host_chunk.load();
+  else if (k == "host_chunk_shared") *value = t.host_chunk_shared.load();
+  else if (k == "host_slots") *value = t.host_slots.load();
+  else if (k == "queue_batches") *value = t.queue_batches.load();
+  else if (k == "e2e_chunk") *value = t.e2e_chunk.load();
+  else if (k == "e2e_rect") *value = t.e2e_rect.load();
+  else if (k == "host_graph") *value = t.host_graph.load();
+  else if (k == "host_duplex") *value = t.host_duplex.load();
+  else if (k == "host_pitch16") *value = t.host_pitch16.load();
+  else if (k == "fused_min_units") *value = t.fused_min_units.load();
+  else if (k == "rec_min_units") *value = t.rec_min_units.load();
+  else if (k == "nb_small_units") *value = t.nb_small_units.load();
+  else return fail(OZEC_EINVAL, "no readable tuning key " + k);
+  return OZEC_OK;
+}
+
 int ozec_tuning_variants(const char *key, int *ids, int cap) {
   if (!key) return fail(OZEC_EINVAL, "null key");
   const std::string k(key);

@@ -26,6 +26,9 @@ std::atomic<unsigned> g_gen{1};          // bumped by set_device_list (threads r
 // whether the process chose its devices itself (ozec_set_devices, ozec_set_device_policy, OZEC_DEVICES,
 // OZEC_DEVICE_POLICY): only a process that did not gets "current" from note_set_device
 std::atomic<bool> g_configured{false};
+// the "current" policy in force came from note_set_device, not from the process: a device list or policy chosen
+// afterwards replaces it
+std::atomic<bool> g_implicit_current{false};
 
 int visible() {
   int n = 0;
@@ -100,6 +103,7 @@ int set_device_list(const int *devs, int n) {
   g_list = n > 0 ? std::vector<int>(devs, devs + n) : default_list(vis);
   g_init = true;
   g_configured.store(true, std::memory_order_relaxed);
+  if (g_implicit_current.exchange(false)) g_policy.store(-1, std::memory_order_relaxed);  // the default again
   g_gen.fetch_add(1, std::memory_order_release);
   return OZEC_OK;
 }
@@ -118,6 +122,7 @@ int set_device_policy(int policy) {
   if (policy < 0 || policy > 2) return OZEC_EINVAL;
   g_policy.store(policy, std::memory_order_relaxed);
   g_configured.store(true, std::memory_order_relaxed);
+  g_implicit_current.store(false);
   return OZEC_OK;
 }
 
@@ -125,6 +130,7 @@ bool note_set_device() {
   if (g_configured.load(std::memory_order_relaxed) || env_set("OZEC_DEVICES") || env_set("OZEC_DEVICE_POLICY"))
     return false;
   g_policy.store(2, std::memory_order_relaxed);
+  g_implicit_current.store(true);
   return true;
 }
 

@@ -249,7 +249,8 @@ hipError_t launch_fill_splitmix64(uint8_t *base, int64_t cell_stride, int64_t nc
 // true when the fused kernel supports this (k, rows) pair with the given geometry
 bool encode_crc_supported(const CodeArgs &a, int64_t bpc);
 // whether a supported fused batch of nwin windows per stripe should run fused: at least min_units (stripe, window)
-// units (TuneKnobs::fused_min_units / rec_min_units); units at unaligned offsets always do
+// units (TuneKnobs::fused_min_units / rec_min_units), whatever the units' alignment (unaligned units follow the same
+// rule: their unfused kernels run at full rate too, kernels.hip encode_crc_fused_pays)
 bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin, int64_t min_units);
 // the streamed-input fused kernel (fused.hip): RS shapes with full windows, bpc % 4096 == 0; `e` already rebased
 bool encode_crc_lv_supported(const EncCrcArgs &e);

@@ -73,6 +73,15 @@ int main(int argc, char **argv) {
   // chose a list (here OZEC_DEVICES) or a policy keeps it
   CHECK(ozec::note_set_device() == (env == nullptr));
   CHECK(ozec::device_policy() == (env ? 0 : 2));
+  if (!env) {  // a device list chosen afterwards replaces that implicit "current" policy for every thread
+    const int two[2] = {1, 2};
+    CHECK(ozec::set_device_list(two, 2) == OZEC_OK && ozec::device_policy() == 0);
+    std::set<int> picked;
+    for (int i = 0; i < 4; ++i) picked.insert(ozec::pick_device());
+    CHECK((picked == std::set<int>{1, 2}));
+    CHECK(!ozec::note_set_device() && ozec::device_policy() == 0);  // configured now: later set_device calls leave it
+    CHECK(ozec::set_device_list(nullptr, 0) == OZEC_OK);
+  }
   CHECK(ozec::set_device_policy(0) == OZEC_OK);
   CHECK(!ozec::note_set_device() && ozec::device_policy() == 0);
   CHECK(ozec::device_list() == want);  // "3,x,1,9" -> invalid entries skipped

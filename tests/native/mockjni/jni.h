@@ -49,5 +49,6 @@ struct JNINativeInterface_ {
   void (*SetByteArrayRegion)(JNIEnv *, jbyteArray, jsize, jsize, const jbyte *);
   jintArray (*NewIntArray)(JNIEnv *, jsize);
   void (*SetIntArrayRegion)(JNIEnv *, jintArray, jsize, jsize, const jint *);
+  jboolean (*ExceptionCheck)(JNIEnv *);
 };
 #endif

@@ -25,10 +25,12 @@ struct mock_object {
 static int g_pins, g_local_refs;
 static char g_exc_class[96], g_exc_msg[512];
 static int g_exc_pending;
+static int g_calls_with_pending;  /* JNI calls other than the exception-safe ones made while an exception was pending */
 static char g_missing[96];
 
 static jclass find_class(JNIEnv *env, const char *name) {
   (void)env;
+  if (g_exc_pending) __atomic_add_fetch(&g_calls_with_pending, 1, __ATOMIC_RELAXED);
   if (g_missing[0] && !strcmp(name, g_missing)) {
     g_exc_pending = 1;
     snprintf(g_exc_class, sizeof g_exc_class, "java/lang/NoClassDefFoundError");
@@ -76,8 +78,21 @@ static void int_array_region(JNIEnv *env, jintArray a, jsize start, jsize n, jin
   memcpy(buf, (jint *)a->data + start, sizeof(jint) * (size_t)n);
 }
 
+/* test hook: the next `g_refuse_after` pins succeed, then GetPrimitiveArrayCritical returns NULL with an
+ * OutOfMemoryError pending (a JVM that cannot pin); -1 = never refuse */
+static int g_refuse_after = -1;
+
 static void *array_critical(JNIEnv *env, jarray a, jboolean *is_copy) {
   (void)env;
+  if (g_exc_pending) __atomic_add_fetch(&g_calls_with_pending, 1, __ATOMIC_RELAXED);
+  if (g_refuse_after == 0) {
+    g_refuse_after = -1;
+    g_exc_pending = 1;
+    snprintf(g_exc_class, sizeof g_exc_class, "java/lang/OutOfMemoryError");
+    snprintf(g_exc_msg, sizeof g_exc_msg, "could not pin the array");
+    return NULL;
+  }
+  if (g_refuse_after > 0) --g_refuse_after;
   if (is_copy) *is_copy = 0;
   __atomic_add_fetch(&g_pins, 1, __ATOMIC_RELAXED);
   return a->data;
@@ -122,8 +137,14 @@ static int region_ok(jarray a, jsize start, jsize n) {
 
 static int g_region_copies;
 
+static jboolean exception_check(JNIEnv *env) {
+  (void)env;
+  return (jboolean)(g_exc_pending != 0);
+}
+
 static void get_byte_region(JNIEnv *env, jbyteArray a, jsize start, jsize n, jbyte *buf) {
   (void)env;
+  if (g_exc_pending) __atomic_add_fetch(&g_calls_with_pending, 1, __ATOMIC_RELAXED);
   if (!region_ok(a, start, n)) return;
   memcpy(buf, (jbyte *)a->data + start, (size_t)n);
   __atomic_add_fetch(&g_region_copies, 1, __ATOMIC_RELAXED);
@@ -131,6 +152,7 @@ static void get_byte_region(JNIEnv *env, jbyteArray a, jsize start, jsize n, jby
 
 static void set_byte_region(JNIEnv *env, jbyteArray a, jsize start, jsize n, const jbyte *buf) {
   (void)env;
+  if (g_exc_pending) __atomic_add_fetch(&g_calls_with_pending, 1, __ATOMIC_RELAXED);
   if (!region_ok(a, start, n)) return;
   memcpy((jbyte *)a->data + start, buf, (size_t)n);
   __atomic_add_fetch(&g_region_copies, 1, __ATOMIC_RELAXED);
@@ -156,12 +178,14 @@ static const struct JNINativeInterface_ g_table = {
     find_class,           throw_new,      exception_clear,       delete_local_ref, array_length,
     object_array_element, int_array_region, array_critical,      release_array_critical,
     new_direct,           direct_address, direct_capacity,       get_byte_region,  set_byte_region,
-    new_int_array,        set_int_region,
+    new_int_array,        set_int_region, exception_check,
 };
 static JNIEnv g_env = &g_table;
 
 /* ---- driver API (ctypes) */
 JNIEnv *mock_env(void) { return &g_env; }
+void mock_refuse_pin_after(int n) { g_refuse_after = n; }
+int mock_calls_with_pending(void) { return __atomic_load_n(&g_calls_with_pending, __ATOMIC_RELAXED); }
 
 static struct mock_object *obj(int kind, void *data, int64_t len) {
   struct mock_object *o = calloc(1, sizeof *o);

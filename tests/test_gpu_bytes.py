@@ -13,6 +13,7 @@ import pytest
 import oracle
 
 torch = pytest.importorskip("torch")
+from devcopy import to_dev, to_host  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 from ozone_amd import checksum as ck  # noqa: E402
@@ -35,15 +36,15 @@ def _packed_case(k, p, n, S, bpc, ctype, shift, seed):
     flat = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
     body = flat[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
     body[:, :k] = data
-    d = torch.from_numpy(flat).to(DEV)
+    d = to_dev(flat)
     base = d[GUARD + shift:]
     nwin = -(-n // bpc)
     crcs = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
     rc.RawErasureEncoder(rc.ECReplicationConfig(k, p)).encode_crc_batch(
         base, (k + p) * n, n, base[k * n:], (k + p) * n, n, S, n, ctype, bpc, crcs)
     torch.cuda.synchronize()
-    got = d.cpu().numpy()
-    c = crcs.cpu().numpy().view(np.uint32)
+    got = to_host(d)
+    c = to_host(crcs).view(np.uint32)
     assert (got[:GUARD + shift] == 0xA5).all() and (got[GUARD + shift + S * (k + p) * n:] == 0xA5).all()
     units = got[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
     ot = _otype(ctype)
@@ -117,7 +118,7 @@ def test_packed_odd_cells_coding_and_checksum_entry_points(k, p, n):
     flat = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
     body = flat[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
     body[:, :k] = data
-    d = torch.from_numpy(flat).to(DEV)
+    d = to_dev(flat)
     base = d[GUARD + shift:]
     rc.RawErasureEncoder(rc.ECReplicationConfig(k, p)).encode_batch(base, (k + p) * n, n, base[k * n:], (k + p) * n,
                                                                      n, S, n)
@@ -125,8 +126,8 @@ def test_packed_odd_cells_coding_and_checksum_entry_points(k, p, n):
     crcs = torch.zeros((S * (k + p), nwin), dtype=torch.int32, device=DEV)
     ck.checksum_windows_batch(ck.ChecksumType.CRC32C, base, n, S * (k + p), n, bpc, crcs)
     torch.cuda.synchronize()
-    got = d.cpu().numpy()
-    c = crcs.cpu().numpy().view(np.uint32).reshape(S, k + p, nwin)
+    got = to_host(d)
+    c = to_host(crcs).view(np.uint32).reshape(S, k + p, nwin)
     assert (got[:GUARD + shift] == 0xA5).all() and (got[GUARD + shift + S * (k + p) * n:] == 0xA5).all()
     units = got[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
     for s in range(S):
@@ -149,7 +150,7 @@ def test_packed_odd_cells_xor_and_generic_shapes(codec, k, p, n):
     data = rng.integers(0, 256, (S, k, n), dtype=np.uint8)
     flat = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
     flat[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)[:, :k] = data
-    d = torch.from_numpy(flat).to(DEV)
+    d = to_dev(flat)
     base = d[GUARD + shift:]
     conf = rc.ECReplicationConfig(k, p, codec)
     nwin = -(-n // bpc)
@@ -161,9 +162,9 @@ def test_packed_odd_cells_xor_and_generic_shapes(codec, k, p, n):
     rc.RawErasureDecoder(conf).decode_batch(base, (k + p) * n, n, [u for u in range(k + p) if u != k - 1][:k], erased,
                                             out, n, n, S, n)
     torch.cuda.synchronize()
-    got = d.cpu().numpy()
-    c = crcs.cpu().numpy().view(np.uint32)
-    o = out.cpu().numpy()
+    got = to_host(d)
+    c = to_host(crcs).view(np.uint32)
+    o = to_host(out)
     assert (got[:GUARD + shift] == 0xA5).all() and (got[GUARD + shift + S * (k + p) * n:] == 0xA5).all()
     units = got[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
     for s in range(S):

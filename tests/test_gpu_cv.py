@@ -13,6 +13,7 @@ import oracle
 from synth import SEED, cells
 
 torch = pytest.importorskip("torch")
+from devcopy import to_dev, to_host  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 from ozone_amd import _lib as L  # noqa: E402
@@ -81,12 +82,12 @@ def test_combined_verify_reports_the_first_failure(variant, case, ctype, otype):
         d_crc = torch.zeros((S, 4, nwin), dtype=torch.int32, device=DEV)
         mism = torch.zeros(S, dtype=torch.int32, device=DEV)
         rc.RawErasureDecoder(rc.ECReplicationConfig(k, p)).reconstruct_crc_batch(
-            torch.from_numpy(corrupted).to(DEV), (k + p) * n, n, present, erased, d_out, 4 * n, n, S, n, ctype, bpc,
-            d_crc, d_expected=torch.from_numpy(stored.view(np.int32)).to(DEV), d_mismatch=mism)
+            to_dev(corrupted), (k + p) * n, n, present, erased, d_out, 4 * n, n, S, n, ctype, bpc,
+            d_crc, d_expected=to_dev(stored.view(np.int32)), d_mismatch=mism)
         torch.cuda.synchronize()
     finally:
         lib.ozec_set_tuning(b"crc_variant", 0)
-    m, out, oc = mism.cpu().numpy(), d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint32)
+    m, out, oc = to_host(mism), to_host(d_out), to_host(d_crc).view(np.uint32)
     want = _first_failure(units[bad], corrupted[bad], read, nwin, bpc, otype)
     assert m[0] == -1 and m[2] == -1, (case, m)
     assert m[1] == want, (case, variant, m[1], want)
@@ -111,9 +112,9 @@ def test_combined_variants_without_expected_crcs_and_for_encode(variant):
         d_out = torch.zeros((S, 3, n), dtype=torch.uint8, device=DEV)
         d_crc = torch.zeros((S, 3, n // bpc), dtype=torch.int32, device=DEV)
         rc.RawErasureDecoder(rc.ECReplicationConfig(k, p)).reconstruct_crc_batch(
-            torch.from_numpy(units).to(DEV), (k + p) * n, n, present, erased, d_out, 3 * n, n, S, n,
+            to_dev(units), (k + p) * n, n, present, erased, d_out, 3 * n, n, S, n,
             ck.ChecksumType.CRC32C, bpc, d_crc)
-        enc_units = torch.from_numpy(units).to(DEV)
+        enc_units = to_dev(units)
         enc_units[:, k:] = 0
         crcs = torch.zeros((S, k + p, n // bpc), dtype=torch.int32, device=DEV)
         rc.RawErasureEncoder(rc.ECReplicationConfig(k, p)).encode_crc_batch(
@@ -121,8 +122,8 @@ def test_combined_variants_without_expected_crcs_and_for_encode(variant):
         torch.cuda.synchronize()
     finally:
         lib.ozec_set_tuning(b"crc_variant", 0)
-    out, oc = d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint32)
-    eu, c = enc_units.cpu().numpy(), crcs.cpu().numpy().view(np.uint32)
+    out, oc = to_host(d_out), to_host(d_crc).view(np.uint32)
+    eu, c = to_host(enc_units), to_host(crcs).view(np.uint32)
     for s in range(S):
         for i, e in enumerate(erased):
             assert (out[s, i] == units[s, e]).all()
@@ -160,14 +161,14 @@ def test_verify_run_check_reports_the_first_failing_window(variant, bpc, ctype, 
     assert lib.ozec_set_tuning(b"crc_variant", variant) == 0
     try:
         mism = torch.zeros(C, dtype=torch.int32, device=DEV)
-        ck.checksum_verify_batch(ctype, torch.from_numpy(bad).to(DEV), n, C, n, bpc,
-                                 torch.from_numpy(exp.view(np.int32)).to(DEV), mism)
+        ck.checksum_verify_batch(ctype, to_dev(bad), n, C, n, bpc,
+                                 to_dev(exp.view(np.int32)), mism)
         torch.cuda.synchronize()
-        got = mism.cpu().numpy()
-        ck.checksum_verify_batch(ctype, torch.from_numpy(data).to(DEV), n, C, n, bpc,
-                                 torch.from_numpy(exp.view(np.int32)).to(DEV), mism)
+        got = to_host(mism)
+        ck.checksum_verify_batch(ctype, to_dev(data), n, C, n, bpc,
+                                 to_dev(exp.view(np.int32)), mism)
         torch.cuda.synchronize()
-        clean = mism.cpu().numpy()
+        clean = to_host(mism)
     finally:
         lib.ozec_set_tuning(b"crc_variant", 0)
     assert got.tolist() == want.tolist(), (variant, bpc)
@@ -200,12 +201,12 @@ def test_combined_verify_every_stripe_failing(k, p, erased):
     assert lib.ozec_set_tuning(b"crc_variant", 231) == 0
     try:
         rc.RawErasureDecoder(rc.ECReplicationConfig(k, p)).reconstruct_crc_batch(
-            torch.from_numpy(corrupted).to(DEV), (k + p) * n, n, present, erased, d_out, len(erased) * n, n, S, n,
-            ck.ChecksumType.CRC32C, bpc, d_crc, d_expected=torch.from_numpy(stored.view(np.int32)).to(DEV),
+            to_dev(corrupted), (k + p) * n, n, present, erased, d_out, len(erased) * n, n, S, n,
+            ck.ChecksumType.CRC32C, bpc, d_crc, d_expected=to_dev(stored.view(np.int32)),
             d_mismatch=mism)
         torch.cuda.synchronize()
     finally:
         lib.ozec_set_tuning(b"crc_variant", 0)
-    m = mism.cpu().numpy()
+    m = to_host(mism)
     for s in range(S):
         assert m[s] == _first_failure(units[s], corrupted[s], read, nwin, bpc, oracle.CRC32C), (s, m)

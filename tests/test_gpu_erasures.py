@@ -15,6 +15,7 @@ import oracle
 from synth import SEED, cells
 
 torch = pytest.importorskip("torch")
+from devcopy import to_dev, to_host  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 from ozone_amd import checksum as ck  # noqa: E402
@@ -36,7 +37,7 @@ def _sets(k, p):
 def test_decode_every_recoverable_set(k, p):
     n, S = 3001, 2
     units = _units(k, p, n, S, 600000 + k)
-    d_in = torch.from_numpy(units).to(DEV)
+    d_in = to_dev(units)
     dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
     sets = _sets(k, p)
     d_out = torch.empty((S, p, n), dtype=torch.uint8, device=DEV)
@@ -44,7 +45,7 @@ def test_decode_every_recoverable_set(k, p):
         present = [u for u in range(k + p) if u not in erased]
         d_out.fill_(0xA5)
         dec.decode_batch(d_in, (k + p) * n, n, present, erased, d_out, p * n, n, S, n)
-        got = d_out.cpu().numpy()
+        got = to_host(d_out)
         for i, e in enumerate(erased):
             assert (got[:, i] == units[:, e]).all(), (k, p, erased, e)
     assert len(sets) == sum(len(list(itertools.combinations(range(k + p), ne))) for ne in range(1, p + 1))
@@ -63,8 +64,8 @@ def test_reconstruct_every_recoverable_set_with_crcs(k, p, bpc):
     nwin = -(-n // bpc)
     stored = np.stack([np.stack([oracle.crc_windows(oracle.CRC32C, units[s, u], bpc) for u in range(k + p)])
                        for s in range(S)]).astype(np.uint32)
-    d_in = torch.from_numpy(units).to(DEV)
-    d_exp = torch.from_numpy(stored.view(np.int32)).to(DEV)
+    d_in = to_dev(units)
+    d_exp = to_dev(stored.view(np.int32))
     dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p))
     d_out = torch.empty((S, p, n), dtype=torch.uint8, device=DEV)
     mism = torch.empty(S, dtype=torch.int32, device=DEV)
@@ -74,7 +75,7 @@ def test_reconstruct_every_recoverable_set_with_crcs(k, p, bpc):
         d_crc = torch.empty((S, len(erased), nwin), dtype=torch.int32, device=DEV)  # [stripe][rebuilt unit][window]
         dec.reconstruct_crc_batch(d_in, (k + p) * n, n, present, erased, d_out, p * n, n, S, n,
                                   ck.ChecksumType.CRC32C, bpc, d_crc, d_expected=d_exp, d_mismatch=mism)
-        got, crcs, m = d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint32), mism.cpu().numpy()
+        got, crcs, m = to_host(d_out), to_host(d_crc).view(np.uint32), to_host(mism)
         assert (m == -1).all(), (k, p, erased, m)
         for i, e in enumerate(erased):
             assert (got[:, i] == units[:, e]).all(), (k, p, erased, e)

@@ -8,6 +8,7 @@ from synth import SEED, cells
 import variants
 
 torch = pytest.importorskip("torch")
+from devcopy import to_dev, to_host  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 from ozone_amd import checksum as ck  # noqa: E402
@@ -18,12 +19,11 @@ DEV = "cuda:0"
 
 
 def t(a):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return to_dev(a)  # pinned staging, never a pageable DMA (devcopy.py)
 
 
 def h(x):
-    torch.cuda.synchronize()
-    return x.cpu().numpy()
+    return to_host(x)
 
 
 @pytest.mark.parametrize("ctype,otype", [(ck.ChecksumType.CRC32C, oracle.CRC32C), (ck.ChecksumType.CRC32, oracle.CRC32)])

@@ -13,6 +13,7 @@ from synth import SEED, cells, splitmix64_bytes
 import variants
 
 torch = pytest.importorskip("torch")
+from devcopy import to_dev, to_host  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 from ozone_amd import _lib as L  # noqa: E402
@@ -31,12 +32,11 @@ def dec(codec, k, p):
 
 
 def t(a):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return to_dev(a)  # pinned staging, never a pageable DMA (devcopy.py)
 
 
 def h(x):
-    torch.cuda.synchronize()
-    return x.cpu().numpy()
+    return to_host(x)
 
 
 # ------------------------------------------------------------------------------------------ golden
@@ -881,6 +881,7 @@ def test_host_path_pinned_buffers_dma_in_place(codec, k, p, n):
     cd = ck.Checksum(ck.ChecksumType.CRC32C, bpc).compute_checksum(ins[1])
     got = [int.from_bytes(b, "big") for b in cd.get_checksums()]
     assert got == [int(x) for x in oracle.crc_windows(oracle.CRC32C, data[1], bpc)]
+    del views, ins, par, units, dins, outs  # no view into the pool outlives it (its range is retired on free)
     pool.free()
 
 

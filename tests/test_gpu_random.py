@@ -16,6 +16,7 @@ import pytest
 import oracle
 
 torch = pytest.importorskip("torch")
+from devcopy import to_dev, to_host  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 from ozone_amd import checksum as ck  # noqa: E402
@@ -93,23 +94,23 @@ def test_random_device_encode_decode(i):
     off = [int(x) for x in r.integers(0, 16, k + p + 8)]
     raw = [torch.zeros(n + 32, dtype=torch.uint8, device=DEV) for _ in range(k)]
     for j in range(k):
-        raw[j][off[j]:off[j] + n] = torch.from_numpy(data[j]).to(DEV)
+        raw[j][off[j]:off[j] + n] = to_dev(data[j])
     out = [torch.full((n + 32,), 0xA5, dtype=torch.uint8, device=DEV) for _ in range(p)]
     rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec)).encode_device(
         [raw[j][off[j]:] for j in range(k)], [out[q][off[k + q]:] for q in range(p)], n)
     torch.cuda.synchronize()
     ref = _parity(codec, k, p, data)
     for q in range(p if codec == "rs" else 1):
-        o = out[q].cpu().numpy()
+        o = to_host(out[q])
         assert (o[off[k + q]:off[k + q] + n] == ref[q]).all(), (codec, k, p, n, q)
         assert (o[:off[k + q]] == 0xA5).all() and (o[off[k + q] + n:] == 0xA5).all()  # nothing outside the cell
     units = data + ref
     erased, present = _erasure(r, codec, k, p)
-    d_in = [torch.from_numpy(units[u]).to(DEV) if u in present else None for u in range(k + p)]
+    d_in = [to_dev(units[u]) if u in present else None for u in range(k + p)]
     d_out = [torch.zeros(n, dtype=torch.uint8, device=DEV) for _ in erased]
     rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec)).decode_device(d_in, erased, d_out, n)
     torch.cuda.synchronize()
-    assert all((x.cpu().numpy() == units[e]).all() for x, e in zip(d_out, erased)), (codec, k, p, n, erased)
+    assert all((to_host(x) == units[e]).all() for x, e in zip(d_out, erased)), (codec, k, p, n, erased)
 
 
 FUSED = [("rs", 6, 3), ("rs", 6, 2), ("rs", 6, 1), ("rs", 3, 2), ("rs", 3, 1), ("rs", 10, 4), ("rs", 10, 3),
@@ -137,13 +138,13 @@ def test_random_fused_encode_crc(i):
     rows = p if codec == "rs" else 1
     data = np.stack([np.stack(_cells(r, k, n)) for _ in range(S)])              # [S][k][n]
     units = torch.full((S, k + p, n), 0xA5, dtype=torch.uint8, device=DEV)
-    units[:, :k] = torch.from_numpy(data).to(DEV)
+    units[:, :k] = to_dev(data)
     nwin = -(-n // bpc)
     crcs = torch.zeros((S, k + rows, nwin), dtype=torch.int32, device=DEV)
     rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec)).encode_crc_batch(
         units, (k + p) * n, n, units[:, k:], (k + p) * n, n, S, n, ctype, bpc, crcs)
     torch.cuda.synchronize()
-    got, c = units.cpu().numpy(), crcs.cpu().numpy().view(np.uint32)
+    got, c = to_host(units), to_host(crcs).view(np.uint32)
     for s in range(S):
         ref = _parity(codec, k, p, list(data[s]))
         for q in range(p):
@@ -177,11 +178,11 @@ def test_random_fused_reconstruction(i):
     d_crc = torch.zeros((S, len(erased), nwin), dtype=torch.int32, device=DEV)
     mism = torch.zeros(S, dtype=torch.int32, device=DEV)
     dec = rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec))
-    dec.reconstruct_crc_batch(torch.from_numpy(corrupted).to(DEV), (k + p) * n, n, present, erased, d_out,
+    dec.reconstruct_crc_batch(to_dev(corrupted), (k + p) * n, n, present, erased, d_out,
                               len(erased) * n, n, S, n, ctype, bpc, d_crc,
-                              d_expected=torch.from_numpy(stored.view(np.int32)).to(DEV), d_mismatch=mism)
+                              d_expected=to_dev(stored.view(np.int32)), d_mismatch=mism)
     torch.cuda.synchronize()
-    out, crcs, m = d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint32), mism.cpu().numpy()
+    out, crcs, m = to_host(d_out), to_host(d_crc).view(np.uint32), to_host(mism)
     for s in range(S):
         if s == bad_s:
             assert m[s] == bad_u * nwin + pos // bpc, (codec, k, p, n, bpc, erased, bad_u, pos)

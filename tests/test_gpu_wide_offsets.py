@@ -12,6 +12,7 @@ import pytest
 import oracle
 
 torch = pytest.importorskip("torch")
+from devcopy import to_dev, to_host  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 from ozone_amd import checksum as ck  # noqa: E402
@@ -59,13 +60,13 @@ def test_units_more_than_2gib_apart(codec, k, p, shift, n):
     wcrc = torch.zeros((k + p, nwin), dtype=torch.int32, device=DEV)  # every unit of stripe 1, cell stride US
     ck.checksum_windows_batch(ck.ChecksumType.CRC32, base[ss:], US, k + p, n, bpc, wcrc)
     torch.cuda.synchronize()
-    c, o, w = crcs.cpu().numpy().view(np.uint32), out.cpu().numpy(), wcrc.cpu().numpy().view(np.uint32)
-    ro, rcc, m = rout.cpu().numpy(), rcrc.cpu().numpy().view(np.uint32), mism.cpu().numpy()
+    c, o, w = to_host(crcs).view(np.uint32), to_host(out), to_host(wcrc).view(np.uint32)
+    ro, rcc, m = to_host(rout), to_host(rcrc).view(np.uint32), to_host(mism)
     for s in range(S):
         ref = [oracle.xor_encode(list(data[s]))] if codec == "xor" else oracle.rs_encode(k, p, list(data[s]))
         units = list(data[s]) + list(ref)
         for q in range(p):
-            assert (at(s, k + q).cpu().numpy() == ref[q]).all(), (codec, k, p, shift, n, s, q)
+            assert (to_host(at(s, k + q)) == ref[q]).all(), (codec, k, p, shift, n, s, q)
         for u in range(k + p):
             assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, units[u], bpc)).all(), (codec, s, u)
         for i, e in enumerate(erased):

@@ -42,7 +42,8 @@ def J():
         ("mock_pins_at_device_call", ctypes.c_int, []), ("mock_device_calls", ctypes.c_int, []),
         ("mock_reset_device_calls", None, []), ("mock_region_copies", ctypes.c_int, []),
         ("mock_set_missing_class", None, [ctypes.c_char_p]), ("mock_host_allocs", ctypes.c_int, []),
-        ("mock_host_live", ctypes.c_int, []),
+        ("mock_host_live", ctypes.c_int, []), ("mock_refuse_pin_after", None, [ctypes.c_int]),
+        ("mock_calls_with_pending", ctypes.c_int, []),
         ("mock_take_exception", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
         (P + "deviceCount", i32, [vp, vp]),
         (P + "setDevices", None, [vp, vp, vp]), (P + "getDevices", vp, [vp, vp]),
@@ -446,6 +447,35 @@ def test_heap_arrays_never_pinned_across_device_work(J, java, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("refuse_after", [0, 2, 3])  # the first input pin, the last one, the first output pin
+def test_refused_array_pin_leaves_its_exception_and_no_further_jni_call(J, java, refuse_after):
+    """a JVM that cannot pin an array (GetPrimitiveArrayCritical -> NULL, OutOfMemoryError pending) ends the
+    copy: the arrays already pinned are released without write-back, the exception stays the pending one (no JNI call
+    but ExceptionCheck / Release / DeleteLocalRef runs while it is pending), outputs stay untouched, and the next call
+    works."""
+    k, p, n = 3, 2, 1 << 16
+    h = call(J, "coderCreate", 0, 0, k, p)
+    try:
+        d = cells(SEED, 743000 + refuse_after, k, n)
+        outs = [np.full(n, 0xA5, np.uint8) for _ in range(p)]
+        pending0 = J.mock_calls_with_pending()
+        J.mock_refuse_pin_after(refuse_after)
+        call(J, "encodeArrays", h, java.array([java.bytes(x) for x in d]), java.ints([0] * k), n,
+             java.array([java.bytes(x) for x in outs]), java.ints([0] * p))
+        assert java.exception() == ("java/lang/OutOfMemoryError", "could not pin the array")
+        assert J.mock_calls_with_pending() == pending0, "a JNI call ran with the exception pending"
+        assert J.mock_pins() == 0
+        assert all((o == 0xA5).all() for o in outs)
+        call(J, "encodeArrays", h, java.array([java.bytes(x) for x in d]), java.ints([0] * k), n,
+             java.array([java.bytes(x) for x in outs]), java.ints([0] * p))
+        assert java.exception() is None
+        assert all((o == r).all() for o, r in zip(outs, oracle.rs_encode(k, p, d)))
+    finally:
+        J.mock_refuse_pin_after(-1)
+        call(J, "coderRelease", h)
+
+
+@pytest.mark.gpu
 def test_heap_arenas_are_pooled_across_threads(J, java):
     """The pinned arenas heap-array calls copy through come from a bounded pool, not one per Java thread: 24 threads
     calling one after another reuse one arena (no new pinned allocation after the first), and the results stay exact."""
@@ -480,17 +510,18 @@ def test_compose_windows_batch_through_jni(J, java):
     """composeWindowsBatch on device pointers (a GPU pipeline's window CRCs): the composite CRC of every cell equals
     the CRC of the whole cell."""
     import torch
+    from devcopy import to_dev, to_host
     n, bpc, C = 100_000, 4096, 5
     nwin = (n + bpc - 1) // bpc
     data = np.stack(cells(SEED, 747000, C, n))
     win = np.stack([oracle.crc_windows(oracle.CRC32C, data[c], bpc) for c in range(C)]).astype(np.uint32)
-    d_win = torch.from_numpy(win.view(np.int32)).cuda()
+    d_win = to_dev(win.view(np.int32))
     d_out = torch.zeros(C, dtype=torch.int32, device="cuda")
     call(J, "composeWindowsBatch", 3, d_win.data_ptr(), nwin, C, nwin, bpc, n - (nwin - 1) * bpc, 0, d_out.data_ptr(),
          0, 0)
     assert java.exception() is None
     torch.cuda.synchronize()
-    got = d_out.cpu().numpy().view(np.uint32)
+    got = to_host(d_out).view(np.uint32)
     assert [int(v) for v in got] == [oracle.crc_windows(oracle.CRC32C, data[c], n)[0] for c in range(C)]
     call(J, "composeWindowsBatch", 3, d_win.data_ptr(), nwin, -1, nwin, bpc, 1, 0, d_out.data_ptr(), 0, 0)
     assert java.exception()[0] == "org/apache/hadoop/HadoopIllegalArgumentException"

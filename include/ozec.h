@@ -85,9 +85,8 @@ int ozec_synchronize(void);
 /* give back the host-batch pipeline's chunk buffers (4 device + 4 pinned buffers of one chunk each: about 1.1 GiB
  * of HBM and, for pageable callers, of pinned memory with rs-6-3 1 MiB cells and 32-stripe chunks) and the staging
  * buffers of the idle host-call slots, on every GPU the process has used; the next call allocates again.  Device
- * memory goes back to HIP; pinned blocks up to 4 GiB in all stay registered in libozec's own cache for the next
- * allocation (ozec_host_free likewise), so a registered host range is not handed back to the kernel in normal
- * operation ("GPU faults") */
+ * memory goes back to HIP; pinned blocks are unregistered and their pages returned, their address ranges retired as
+ * ozec_host_free does ("GPU faults") */
 int ozec_release_staging(void);
 
 /* ---- coder lifecycle: RawErasureCoderFactory.createEncoder/createDecoder
@@ -268,7 +267,12 @@ uint32_t ozec_crc_combine(int checksum_type, uint32_t crc_a, uint32_t crc_b, uin
  * never crosses the inter-socket fabric; every staging buffer libozec allocates itself is placed the same way. */
 int ozec_host_alloc(size_t bytes, void **out);
 int ozec_host_alloc_on(size_t bytes, int device, void **out);
+/* unregister the block and retire its address range: its pages go back to the kernel, but the range is never used for
+ * a later block ("GPU faults").  OZEC_EINVAL for a pointer ozec_host_alloc did not return; OZEC_EDEVICE
+ * when the HIP runtime refuses to unregister it -- the block is then left mapped and registered (a leak, counted by
+ * ozec_host_free_failures) rather than changed under a registration HIP still holds. */
 int ozec_host_free(void *p);
+uint64_t ozec_host_free_failures(void);
 /* host NUMA node closest to `device` (-1: unknown / not a NUMA host) */
 int ozec_device_numa_node(int device, int *node);
 /* NUMA node holding the (touched) page at p, -1 if unknown -- placement diagnostics */

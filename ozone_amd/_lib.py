@@ -110,6 +110,7 @@ _SIGS = {
     "ozec_host_alloc": (ctypes.c_int, [c_size, ctypes.POINTER(c_voidp)]),
     "ozec_host_alloc_on": (ctypes.c_int, [c_size, ctypes.c_int, ctypes.POINTER(c_voidp)]),
     "ozec_host_free": (ctypes.c_int, [c_voidp]),
+    "ozec_host_free_failures": (ctypes.c_uint64, []),
     "ozec_device_numa_node": (ctypes.c_int, [ctypes.c_int, c_intp]),
     "ozec_host_page_node": (ctypes.c_int, [c_voidp, c_intp]),
     "ozec_host_copy": (ctypes.c_int, [c_voidp, c_voidp, c_voidp, ctypes.c_int, ctypes.c_int]),

@@ -18,6 +18,8 @@
 #include <sstream>
 #include <string>
 #include <algorithm>
+#include <atomic>
+#include <deque>
 #include <unordered_map>
 #include <vector>
 
@@ -34,45 +36,43 @@ constexpr size_t kHuge = 2u << 20;
 
 std::mutex g_mu;
 std::unordered_map<void *, size_t> g_allocs;  // pinned_alloc'ed regions -> mapped length
-// Address ranges of freed pinned blocks.  A freed block is unregistered at once and its pages go back to the kernel,
-// but its address range does not: it is replaced by an inaccessible reservation (PROT_NONE, mmap MAP_FIXED over the
-// block, so the range is never unmapped in between) and reused only for later pinned blocks.  No range libozec ever
-// registered with HIP can therefore come back from the kernel as an unrelated pageable buffer, which is the pattern the
-// round-4 faults shared ("GPU faults").  Adjacent reservations are merged; a block is carved from the
-// smallest one it fits.
+// Retired address ranges of freed pinned blocks ("GPU faults").  A freed block is unregistered at once and its
+// pages go back to the kernel, but its address range does not come back into use: it is replaced by an inaccessible
+// mapping (PROT_NONE, mmap MAP_FIXED over the block, so the range is never unmapped in between) and no later block,
+// libozec's or anyone's, is placed there.  Nothing libozec registered with HIP is therefore ever registered again at the
+// same address, nor handed out by the kernel as a caller's pageable buffer, while the runtime might still hold state for
+// it.  The retired ranges are returned to the kernel oldest first only past kRetiredMax ranges or kRetiredBytes of
+// address space (bounded VMAs and VA for a process that allocates and frees pinned memory for months).
 struct Range {
   uint8_t *p;
   size_t len;
 };
-std::vector<Range> g_reserved;  // guarded by g_mu
+std::deque<Range> g_retired;  // guarded by g_mu, oldest first
+size_t g_retired_bytes = 0;   // guarded by g_mu
+std::atomic<uint64_t> g_unregister_failures{0};
+constexpr size_t kRetiredMax = 4096;
+constexpr size_t kRetiredBytes = size_t{4} << 40;  // 4 TiB of address space, no memory behind it
 constexpr int kRw = PROT_READ | PROT_WRITE;
 constexpr int kAnon = MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE;
 
-// caller holds g_mu
-void reserve_locked(uint8_t *p, size_t len) {
-  for (size_t i = 0; i < g_reserved.size();) {
-    Range &r = g_reserved[i];
-    if (r.p + r.len == p || p + len == r.p) {  // merge the neighbour into [p, p + len) and look again
-      p = std::min(p, r.p);
-      len += r.len;
-      g_reserved.erase(g_reserved.begin() + static_cast<std::ptrdiff_t>(i));
-      i = 0;
-      continue;
-    }
-    ++i;
-  }
-  g_reserved.push_back({p, len});
-}
-
-// turn a block back into a reservation; false when the kernel refused (the range is then simply unmapped)
-bool quarantine(void *p, size_t len) {
+// retire a block's range (its pages are released by the PROT_NONE mapping); munmap when the kernel refuses
+void retire(void *p, size_t len) {
   if (mmap(p, len, PROT_NONE, kAnon | MAP_FIXED, -1, 0) == MAP_FAILED) {
     munmap(p, len);
-    return false;
+    return;
   }
-  std::lock_guard<std::mutex> lk(g_mu);
-  reserve_locked(static_cast<uint8_t *>(p), len);
-  return true;
+  std::vector<Range> release;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_retired.push_back({static_cast<uint8_t *>(p), len});
+    g_retired_bytes += len;
+    while (g_retired.size() > kRetiredMax || g_retired_bytes > kRetiredBytes) {
+      release.push_back(g_retired.front());
+      g_retired_bytes -= g_retired.front().len;
+      g_retired.pop_front();
+    }
+  }
+  for (const Range &r : release) munmap(r.p, r.len);
 }
 
 size_t page_size() {
@@ -166,40 +166,14 @@ int pinned_alloc(size_t bytes, int device, void **out) {
   if (bytes == 0) return 0;
   const size_t len = (bytes + kHuge - 1) / kHuge * kHuge;
   const int node = device >= 0 ? device_numa_node(device) : -1;
-  uint8_t *reused = nullptr;
-  {  // carve the block from the smallest reservation it fits
-    std::lock_guard<std::mutex> lk(g_mu);
-    size_t best = g_reserved.size();
-    for (size_t i = 0; i < g_reserved.size(); ++i)
-      if (g_reserved[i].len >= len && (best == g_reserved.size() || g_reserved[i].len < g_reserved[best].len)) best = i;
-    if (best < g_reserved.size()) {
-      const Range r = g_reserved[best];
-      g_reserved.erase(g_reserved.begin() + static_cast<std::ptrdiff_t>(best));
-      if (r.len > len) g_reserved.push_back({r.p + len, r.len - len});
-      reused = r.p;
-    }
-  }
-  void *p = nullptr;
-  if (reused) {  // fresh zero pages over the reservation (MAP_FIXED replaces it in place)
-    p = mmap(reused, len, kRw, kAnon | MAP_FIXED, -1, 0);
-    if (p == MAP_FAILED) {
-      std::lock_guard<std::mutex> lk(g_mu);
-      reserve_locked(reused, len);
-      p = nullptr;
-    }
-  }
-  if (!p) {
-    p = mmap(nullptr, len, kRw, kAnon, -1, 0);
-    if (p == MAP_FAILED) return -ENOMEM;
-    reused = nullptr;
-  }
+  void *p = mmap(nullptr, len, kRw, kAnon, -1, 0);  // always a fresh range (retired ones are never reused)
+  if (p == MAP_FAILED) return -ENOMEM;
   (void)madvise(p, len, MADV_HUGEPAGE);  // fewer translations per DMA; best effort
   // placement first (pages are allocated on the first touch, which hipHostRegister does while pinning)
   (void)bind_to_node(p, len, node, false, false);
   if (hipHostRegister(p, len, hipHostRegisterPortable) != hipSuccess) {
     (void)hipGetLastError();
-    if (reused) (void)quarantine(p, len);  // it stays reserved: never handed to the kernel
-    else munmap(p, len);
+    munmap(p, len);  // never registered: nothing can refer to it
     return -ENOMEM;
   }
   {
@@ -221,19 +195,23 @@ int pinned_free(void *p) {
     g_allocs.erase(it);
   }
   // the callers have drained every stream that used the block (capi.cpp Slot / E2E, stripe_queue.cpp); hipHostUnregister
-  // waits for the device besides
-  (void)hipHostUnregister(p);
-  (void)hipGetLastError();
-  (void)quarantine(p, len);
+  // waits for the device besides.  If the runtime does not release the registration, the block is left exactly as it
+  // is -- mapped, registered, its pages in place -- rather than changing pages HIP may still reach (a leak, counted).
+  if (hipHostUnregister(p) != hipSuccess) {
+    (void)hipGetLastError();
+    g_unregister_failures.fetch_add(1, std::memory_order_relaxed);
+    return -EBUSY;
+  }
+  retire(p, len);
   return 0;
 }
 
-size_t pinned_reserved_bytes() {
+size_t pinned_retired_bytes() {
   std::lock_guard<std::mutex> lk(g_mu);
-  size_t n = 0;
-  for (const Range &r : g_reserved) n += r.len;
-  return n;
+  return g_retired_bytes;
 }
+
+uint64_t pinned_unregister_failures() { return g_unregister_failures.load(std::memory_order_relaxed); }
 
 const void *pinned_alloc_base(const void *p) {
   void *base = nullptr;

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -247,9 +248,14 @@ int ozec_host_alloc(size_t bytes, void **out) {
 
 int ozec_host_free(void *p) {
   if (!p) return OZEC_OK;
-  if (ozec::pinned_free(p) != 0) return set_error(OZEC_EINVAL, "pointer was not allocated by ozec_host_alloc");
+  const int rc = ozec::pinned_free(p);
+  if (rc == -EBUSY)
+    return set_error(OZEC_EDEVICE, "the HIP runtime did not unregister the pinned block (left mapped and registered)");
+  if (rc != 0) return set_error(OZEC_EINVAL, "pointer was not allocated by ozec_host_alloc");
   return OZEC_OK;
 }
+
+uint64_t ozec_host_free_failures(void) { return ozec::pinned_unregister_failures(); }
 
 int ozec_device_numa_node(int device, int *node) {
   if (!node) return set_error(OZEC_EINVAL, "null output");

@@ -1,8 +1,8 @@
 """libozec's pinned blocks (ozone_amd/csrc/numa.cpp pinned_alloc / pinned_free) on the CPU, against a fake HIP runtime
 that counts registrations (tests/native/pinned_cache.cpp), under TSan: a freed block is unregistered and its pages
-returned at once, its address range stays reserved (PROT_NONE) and is reused only for later pinned blocks (carved,
-merged); a refused registration leaves the range reserved; foreign / double frees are refused; concurrent cycles never
-share a block.  Why the ranges are kept: DESIGN.md §4, "GPU faults"."""
+returned at once, its address range is retired (PROT_NONE, never reused for a later block, bounded); a refused
+unregistration leaves the block untouched and is counted; foreign / double frees are refused; concurrent cycles never
+share a block.  Why: DESIGN.md §4, "GPU faults"."""
 import os
 import subprocess
 import tempfile

@@ -374,6 +374,9 @@ typedef struct {
 } ozec_op_stats;
 int ozec_stats(int op, ozec_op_stats *out);
 void ozec_stats_reset(void);
+/* fused batch calls (ozec_encode_crc_batch, ozec_reconstruct_crc_batch) since the process started, by the route they
+ * took: one fused kernel, or the unfused kernels (coding, then CRC passes) -- which kernels a workload reaches */
+int ozec_fused_routes(uint64_t *fused, uint64_t *unfused);
 
 /* ---- harness utilities ------------------------------------------------------------------------------- */
 /* process-wide tuning knobs for A/B and profiling runs (a production process leaves them at their defaults; a set

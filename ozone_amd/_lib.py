@@ -146,6 +146,7 @@ _SIGS = {
                                                       ctypes.c_int, c_voidp, ctypes.c_int, c_voidp]),
     "ozec_stats": (ctypes.c_int, [ctypes.c_int, c_voidp]),
     "ozec_stats_reset": (None, []),
+    "ozec_fused_routes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "ozec_set_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
     "ozec_get_tuning": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "ozec_tuning_variants": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),

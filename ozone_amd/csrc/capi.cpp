@@ -1106,6 +1106,15 @@ uint32_t ozec_crc_value(int, uint32_t state) { return ~state; }
 
 // ---- fused encode + CRC --------------------------------------------------------------------------
 
+// fused batch calls by route: one fused kernel, or the unfused kernels (ozec_fused_routes)
+static std::atomic<uint64_t> g_route_fused{0}, g_route_unfused{0};
+
+int ozec_fused_routes(uint64_t *fused, uint64_t *unfused) {
+  if (fused) *fused = g_route_fused.load(std::memory_order_relaxed);
+  if (unfused) *unfused = g_route_unfused.load(std::memory_order_relaxed);
+  return OZEC_OK;
+}
+
 int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_stripe_stride, int64_t in_unit_stride,
                           uint8_t *d_out, int64_t out_stripe_stride, int64_t out_unit_stride, size_t num_stripes,
                           size_t len, int checksum_type, size_t bpc, uint32_t *d_crcs, int big_endian, void *stream) {
@@ -1139,7 +1148,9 @@ int ozec_encode_crc_batch(ozec_coder *enc, const uint8_t *d_in, int64_t in_strip
   if (ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) &&
       ozec::encode_crc_fused_pays(a, nwin, ozec::g_tune.fused_min_units.load(std::memory_order_relaxed))) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
+    g_route_fused.fetch_add(1, std::memory_order_relaxed);
   } else {
+    g_route_unfused.fetch_add(1, std::memory_order_relaxed);
     // unfused: encode, then the CRC pass (crcs[s][u][w] layout kept): one launch over all S x units cells when they
     // sit at one stride (the host batches' device layout [S][k + p][unit pitch]), else one per unit
     OZEC_HIP(ozec::launch_code(a, st));
@@ -1514,7 +1525,9 @@ int ozec_reconstruct_crc_batch(ozec_coder *dec, const uint8_t *d_in, int64_t in_
   if (nrows && n_erased == nrows && ozec::encode_crc_supported(a, static_cast<int64_t>(bpc)) &&
       ozec::encode_crc_fused_pays(a, nwin, ozec::g_tune.rec_min_units.load(std::memory_order_relaxed))) {
     OZEC_HIP(ozec::launch_encode_crc(e, st));
+    g_route_fused.fetch_add(1, std::memory_order_relaxed);
   } else {
+    g_route_unfused.fetch_add(1, std::memory_order_relaxed);
     // unfused: verify the read units, decode, CRC the rebuilt units
     if (d_expected) {
       for (int j = 0; j < nin; ++j) {

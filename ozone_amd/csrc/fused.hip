@@ -318,24 +318,28 @@ bool encode_crc_nb_bytes_supported(const CodeArgs &a, int64_t bpc) {
 
 namespace {
 
-hipError_t launch_nb_shape(const EncCrcArgs &e, hipStream_t st, int v, bool tail) {
+hipError_t launch_nb_shape(const EncCrcArgs &e, hipStream_t st, int v, bool tail, bool wide) {
   const int k = e.code.k, r = e.code.rows;
-  if (k == 6 && r == 3) return launch_nb_6_3(e, st, v, tail);
-  if (k == 6 && r == 2) return launch_nb_6_2(e, st, v, tail);
-  if (k == 6 && r == 1) return launch_nb_6_1(e, st, v, tail);
-  if (k == 3 && r == 2) return launch_nb_3_2(e, st, v, tail);
-  if (k == 3 && r == 1) return launch_nb_3_1(e, st, v, tail);
-  if (k == 10 && r == 4) return launch_nb_10_4(e, st, v, tail);
-  if (k == 10 && r == 3) return launch_nb_10_3(e, st, v, tail);
-  if (k == 10 && r == 2) return launch_nb_10_2(e, st, v, tail);
-  if (k == 10 && r == 1) return launch_nb_10_1(e, st, v, tail);
+  if (k == 6 && r == 3) return launch_nb_6_3(e, st, v, tail, wide);
+  if (k == 6 && r == 2) return launch_nb_6_2(e, st, v, tail, wide);
+  if (k == 6 && r == 1) return launch_nb_6_1(e, st, v, tail, wide);
+  if (k == 3 && r == 2) return launch_nb_3_2(e, st, v, tail, wide);
+  if (k == 3 && r == 1) return launch_nb_3_1(e, st, v, tail, wide);
+  if (k == 10 && r == 4) return launch_nb_10_4(e, st, v, tail, wide);
+  if (k == 10 && r == 3) return launch_nb_10_3(e, st, v, tail, wide);
+  if (k == 10 && r == 2) return launch_nb_10_2(e, st, v, tail, wide);
+  if (k == 10 && r == 1) return launch_nb_10_1(e, st, v, tail, wide);
   return hipErrorInvalidValue;
 }
 
 }  // namespace
 
-hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v, bool tail) {
+hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v, bool tail, bool wide) {
   const int k = e.code.k, r = e.code.rows;
+  if (wide) {  // units 2 GiB or more apart: one descriptor per unit, the one geometry instantiated for it (fused_nb.hpp)
+    (void)hipGetLastError();
+    return launch_nb_shape(e, st, 0, tail, true);
+  }
   if (!tail && (v == 56 || v == 59)) {
     if (k == 6 && r == 3) return launch_lv_kr<6, 3>(e, st, v);
     if (k == 6 && r == 2) return launch_lv_kr<6, 2>(e, st, v);
@@ -369,7 +373,7 @@ hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t st, int v, bool
   const bool used = ws && nb_variant_persistent(v);
   EncCrcArgs ed = e;
   ed.work = used ? ws->ctr : nullptr;
-  hipError_t err = launch_nb_shape(ed, st, v, tail);
+  hipError_t err = launch_nb_shape(ed, st, v, tail, false);
   if (err == hipSuccess && !tail && nb_variant_cv(v) && e.verify && e.crc.expected) {
     const int64_t g = std::min<int64_t>(e.code.nstripes, 4096);
     hipLaunchKernelGGL(nb_reverify, dim3(static_cast<unsigned>(g)), dim3(256), 0, st, e);

@@ -9,7 +9,8 @@ namespace ozec {
 
 
 #define OZEC_NB_SHAPES(X) X(6, 3) X(6, 2) X(6, 1) X(3, 2) X(3, 1) X(10, 4) X(10, 3) X(10, 2) X(10, 1)
-#define OZEC_NB_DECL(K, R) hipError_t launch_nb_##K##_##R(const EncCrcArgs &e, hipStream_t st, int v, bool tail);
+#define OZEC_NB_DECL(K, R) \
+  hipError_t launch_nb_##K##_##R(const EncCrcArgs &e, hipStream_t st, int v, bool tail, bool wide);
 OZEC_NB_SHAPES(OZEC_NB_DECL)
 
 namespace {
@@ -142,6 +143,40 @@ __device__ __forceinline__ uint32_t nb_tail(const EncCrcArgs &e, __amdgpu_buffer
   return v;
 }
 
+// nb_tail for units 2 GiB or more apart (WIDE): the unit's bytes through 64-bit pointers (its base is per lane, and a
+// buffer descriptor must be uniform), ib / ob = the stripe's window bases
+template <int K, int R>
+__device__ __forceinline__ uint32_t nb_tail_wide(const EncCrcArgs &e, const uint8_t *ib, uint8_t *ob,
+                                                 const uint32_t *s_gf, int q, uint32_t v, uint32_t o0, int32_t tb) {
+  const CodeArgs &a = e.code;
+  const uint32_t poly = e.crc.poly;
+  int64_t uoff = a.in_off[0];
+#pragma unroll
+  for (int j = 1; j < K; ++j) uoff = q == j ? a.in_off[j] : uoff;
+#pragma unroll
+  for (int r = 0; r < R; ++r) uoff = q == K + r ? a.out_off[r] : uoff;
+  for (int32_t b = 0; b < tb; ++b) {
+    const int64_t o = static_cast<int64_t>(o0) + b;
+    uint32_t byte;
+    if (q < K) {
+      byte = ib[uoff + o];
+    } else {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint32_t x = ib[a.in_off[j] + o];
+        acc ^= s_gf[j * 32 + (x & 15)] ^ s_gf[j * 32 + 16 + (x >> 4)];
+      }
+      byte = (acc >> (8 * (q - K))) & 0xffu;
+      ob[uoff + o] = static_cast<uint8_t>(byte);
+    }
+    v ^= byte;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = (v >> 1) ^ (poly & (0u - (v & 1u)));
+  }
+  return v;
+}
+
 // CV: the combined check of one window, by the whole wave.  `have` marks the lane holding the combined register's total
 // v (XOR_j x^(8 w_j) raw_j after the lane tree); lanes 0..K-1 turn input j's stored CRC back into its raw register
 // (crc_finish inverted: ~ex ^ init), weight it by x^(8 w_j) (table s_cvs + 224 j) and the 16-lane XOR gives the
@@ -185,10 +220,12 @@ __device__ __forceinline__ void nb_check_combined(const EncCrcArgs &e, const uin
 // stored CRCs; a failing stripe is marked kMismatchSuspect and re-verified unit by unit (nb_reverify).  Saves the
 // shifts and lane trees of K - 1 registers: for rs-10-4 one shift per step instead of ~7.5 (H = 5, D = 2) and 5
 // registers through the lane tree instead of 14.
+// WIDE (round 6): units 2 GiB or more apart (no 32-bit unit offsets after rebase32): one buffer descriptor per unit
+// (64-bit base, soffset 0) instead of one per stripe side, the byte tail through 64-bit pointers (nb_tail_wide)
 // (Round-3 probes -- output-register groups, VALU / LDS pads, far-addressing without the index OR, late lane-tree
 // tables, guided and static persistent orders -- are measured in DESIGN 2.3 and were taken out of the library.)
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
-          bool EM = false, int H = K, bool TAIL = false, bool CV = false>
+          bool EM = false, int H = K, bool TAIL = false, bool CV = false, bool WIDE = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_nb(
     const EncCrcArgs e) {
   static_assert(R >= 1 && R <= 4, "one GF byte per output in the entry dword");
@@ -272,8 +309,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     // runs in the VALU, and without this the buffer accesses were wrapped in waterfall loops)
     const int64_t s = uniform64(u / nwin);
     const int64_t w = uniform64(u - s * nwin);
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(a.out + out_off(a, s) + w * cr.bpc, out_extent);
+    const uint8_t *const ib = a.in + in_off(a, s) + w * cr.bpc;
+    uint8_t *const ob = a.out + out_off(a, s) + w * cr.bpc;
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(ib, in_extent);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(ob, out_extent);
     // steps of this window: a cell's last window may be short (its whole 16-B blocks here, its last 1-15 bytes in
     // nb_tail).  It is run as whole D-step groups with Pb virtual zero blocks in front, as the per-window kernel
     // does: a zero block leaves a zero CRC register at zero and has zero GF products, and the blocks after it keep
@@ -292,8 +331,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
       return t < Tu && o >= 0 ? static_cast<uint32_t>(o) : 0x80000000u;
     };
     auto load = [&](uint32_t vo, int j) {
-      const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, vo, static_cast<int>(a.in_off[j]), 2);
-      return make_uint4(d[0], d[1], d[2], d[3]);
+      if constexpr (WIDE) {
+        const auto d = __builtin_amdgcn_raw_buffer_load_b128(make_rsrc_n(ib + a.in_off[j], static_cast<uint32_t>(wmax)),
+                                                             vo, 0, 2);
+        return make_uint4(d[0], d[1], d[2], d[3]);
+      } else {
+        const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, vo, static_cast<int>(a.in_off[j]), 2);
+        return make_uint4(d[0], d[1], d[2], d[3]);
+      }
     };
     uint32_t S[K + R];
 #pragma unroll
@@ -360,7 +405,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         for (int r = 0; r < R; ++r) {
           const uint4 p = make_uint4(o[r][0], o[r][1], o[r][2], o[r][3]);
           __attribute__((ext_vector_type(4))) unsigned int dv = {p.x, p.y, p.z, p.w};
-          __builtin_amdgcn_raw_buffer_store_b128(dv, rout, vcur, static_cast<int>(a.out_off[r]), 2);
+          if constexpr (WIDE) {
+            __builtin_amdgcn_raw_buffer_store_b128(dv, make_rsrc_n(ob + a.out_off[r], static_cast<uint32_t>(wmax)), vcur,
+                                                   0, 2);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b128(dv, rout, vcur, static_cast<int>(a.out_off[r]), 2);
+          }
           store_data_hold(p);
           if constexpr (XO) {
             uint4 px = p;
@@ -407,9 +457,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         uint32_t vt = v;
         if constexpr (TAIL) {  // the cell's last 1-15 bytes (nb_tail)
           const int32_t tb = last ? static_cast<int32_t>((a.len - w * cr.bpc) & 15) : 0;
-          if (tb != 0 && lane < tree_np(K + R) && q < K + R)
-            vt = nb_tail<K, R>(e, rin, rout, s_gf, q, v, static_cast<uint32_t>((a.len - w * cr.bpc) & ~int64_t{15}),
-                               tb);
+          if (tb != 0 && lane < tree_np(K + R) && q < K + R) {
+            const uint32_t o0 = static_cast<uint32_t>((a.len - w * cr.bpc) & ~int64_t{15});
+            if constexpr (WIDE) vt = nb_tail_wide<K, R>(e, ib, ob, s_gf, q, v, o0, tb);
+            else vt = nb_tail<K, R>(e, rin, rout, s_gf, q, v, o0, tb);
+          }
         }
         if (lane < tree_np(K + R) && q < K + R) nb_emit_lane<K, R>(e, s, w, q, vt, init);
       } else if (lane < tree_np(K + R)) {  // each unit's total once; static unit index (kernarg arrays stay SGPR-indexed)
@@ -430,16 +482,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 template <int K, int R, int D, int NB, int WPB, int WAVES, int FENCE = 2, bool RS = true, int DYN = 0, bool XO = false,
-          bool EM = false, int H = K, bool TAIL = false, bool CV = false>
+          bool EM = false, int H = K, bool TAIL = false, bool CV = false, bool WIDE = false>
 hipError_t launch_nb(const EncCrcArgs &e, hipStream_t st) {
   if constexpr ((D * K) % NB != 0) {  // the ring must divide the unrolled group: fall back to one that does
     // NB = 2 with an odd group once made this launcher call itself with the same arguments (a host stack overflow,
     // SIGSEGV in the caller: DESIGN 2.3); the fallback must differ from NB and divide the group
     constexpr int kNB = (D * K) % 2 == 0 ? 2 : (D * K <= K + 1 ? D * K : 1);
     static_assert(kNB != NB && (D * K) % kNB == 0 && kNB - 1 <= K, "fallback ring must differ and divide the group");
-    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL, CV>(e, st);
+    return launch_nb<K, R, D, kNB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL, CV, WIDE>(e, st);
   } else {
-    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL, CV>;
+    auto kern = encode_crc_nb<K, R, D, NB, WPB, WAVES, FENCE, RS, DYN, XO, EM, H, TAIL, CV, WIDE>;
     const int64_t units = e.code.nstripes * e.crc.nwin;
     const int64_t blocks = (units + WPB - 1) / WPB;
     int64_t g = blocks;
@@ -567,6 +619,14 @@ hipError_t launch_nb_tail_kr(const EncCrcArgs &e, hipStream_t st, int v) {
     default: break;
   }
   return hipErrorInvalidValue;
+}
+// units 2 GiB or more apart (round 6): the one-step geometry of 173 with one descriptor per unit, for 16-B-multiple
+// cells and (TAIL) any length; a rare layout (a caller's cells scattered over a large HBM pool), so one form only
+template <int K, int R>
+hipError_t launch_nb_wide_kr(const EncCrcArgs &e, hipStream_t st, bool tail) {
+  constexpr int kNB = K % 2 == 0 && K > 2 ? K / 2 : K;
+  if (tail) return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, true, true, K, true, false, true>(e, st);
+  return launch_nb<K, R, 1, kNB, 8, 4, 2, true, 0, true, true, K, false, false, true>(e, st);
 }
 }  // namespace
 }  // namespace ozec

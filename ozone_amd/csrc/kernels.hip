@@ -570,11 +570,65 @@ __global__ __launch_bounds__(kBlock) void crc_windows_g26s(const CrcArgs a, int6
 // LDS too (ds_read_b32 broadcast).
 // XO (XOR codec only): the input registers move by one step with no shift lookups (kernels.hpp kXo*; as
 // crc_windows_g26s), the parity's register is still the XOR of theirs, and the advance is undone once per window.
-template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false, bool HV = false, bool XO = false>
+// TAIL (round 6, the XOR codec only): cells of any length at any byte offset.  The window loop takes the whole 16-B
+// blocks of the last window (buffer accesses at any byte address); after the lane tree, the lane of unit q extends its
+// register bytewise over the window's last 1-15 bytes, the parity lane XORing the K inputs' bytes and storing them
+// (xor_tail).  The raw register update is GF(2)-linear in (register, byte), so the parity's register stays the XOR of
+// the inputs' registers through the tail as well.
+template <int K>
+__device__ __forceinline__ uint32_t xor_tail(const EncCrcArgs &e, __amdgpu_buffer_rsrc_t rin,
+                                             __amdgpu_buffer_rsrc_t rout, int q, uint32_t v, uint32_t o0, int32_t tb) {
+  const CodeArgs &a = e.code;
+  const uint32_t poly = e.crc.poly;
+  for (int32_t b = 0; b < tb; ++b) {
+    const uint32_t ob = o0 + static_cast<uint32_t>(b);
+    uint32_t byte = 0;
+    if (q < K) {
+      byte = __builtin_amdgcn_raw_buffer_load_b8(rin, ob, static_cast<int>(a.in_off[q]), 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) byte ^= __builtin_amdgcn_raw_buffer_load_b8(rin, ob, static_cast<int>(a.in_off[j]), 0);
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(byte), rout, ob, static_cast<int>(a.out_off[0]), 0);
+    }
+    v ^= byte;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = (v >> 1) ^ (poly & (0u - (v & 1u)));
+  }
+  return v;
+}
+
+// WIDE (round 6, the XOR codec only): units 2 GiB or more apart -- one buffer descriptor per unit (64-bit base), the tail
+// through 64-bit pointers (xor_tail_wide).
+template <int K>
+__device__ __forceinline__ uint32_t xor_tail_wide(const EncCrcArgs &e, const uint8_t *ib, uint8_t *ob, int q, uint32_t v,
+                                                  uint32_t o0, int32_t tb) {
+  const CodeArgs &a = e.code;
+  const uint32_t poly = e.crc.poly;
+  for (int32_t b = 0; b < tb; ++b) {
+    const int64_t o = static_cast<int64_t>(o0) + b;
+    uint32_t byte = 0;
+    if (q < K) {
+      byte = ib[a.in_off[q] + o];
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) byte ^= ib[a.in_off[j] + o];
+      ob[a.out_off[0] + o] = static_cast<uint8_t>(byte);
+    }
+    v ^= byte;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = (v >> 1) ^ (poly & (0u - (v & 1u)));
+  }
+  return v;
+}
+
+template <int K, int R, int D, bool XORC, int TM, int WAVES = 4, bool PF = false, bool HV = false, bool XO = false,
+          bool TAIL = false, bool WIDE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void encode_crc_g26(const EncCrcArgs e, const TabArgs<K * R> tabs) {
   constexpr int E = D;
   static_assert(D >= 1, "group of at least one step");
   static_assert(!XO || XORC, "XO only where every CRC register belongs to an input (the XOR codec)");
+  static_assert(!TAIL || (XORC && R == 1 && !XO), "byte tails: the XOR codec's default form");
+  static_assert(!WIDE || (XORC && R == 1 && !XO), "one descriptor per unit: the XOR codec's default form");
   constexpr int kXoOff = g26_words(E);  // XO: the XO blob after the G26 blob
   __shared__ __attribute__((aligned(16))) uint32_t s_t[g26_words(E) + (XO ? kXoWords : 0)];
   __shared__ __attribute__((aligned(16))) uint4 s_q[K * R];
@@ -606,17 +660,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
     const int64_t m = N >> 4;
     const int32_t G = static_cast<int32_t>((m + 64 * D - 1) / (64 * D));
     const int32_t P = G * 64 * D - static_cast<int32_t>(m);  // window <= 2 GiB: 32-bit block indices
-    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(a.in + in_off(a, s) + w * cr.bpc, in_extent);
-    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(a.out + out_off(a, s) + w * cr.bpc, out_extent);
+    const uint8_t *const ib = a.in + in_off(a, s) + w * cr.bpc;
+    uint8_t *const ob = a.out + out_off(a, s) + w * cr.bpc;
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc_n(ib, in_extent);
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc_n(ob, out_extent);
     uint32_t S[K + R];
 #pragma unroll
     for (int q = 0; q < K + R; ++q) S[q] = 0;
     auto load_x = [&](int32_t t, uint4 (&dst)[K]) {
       const int32_t vb = t * 64 + lane - P;
       auto ld = [&](int j) {
-        const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<uint32_t>(vb) * 16u,
-                                                             static_cast<int>(a.in_off[j]), 2);
-        return make_uint4(d[0], d[1], d[2], d[3]);
+        if constexpr (WIDE) {
+          const auto d = __builtin_amdgcn_raw_buffer_load_b128(make_rsrc_n(ib + a.in_off[j], static_cast<uint32_t>(wmax)),
+                                                               static_cast<uint32_t>(vb) * 16u, 0, 2);
+          return make_uint4(d[0], d[1], d[2], d[3]);
+        } else {
+          const auto d = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<uint32_t>(vb) * 16u,
+                                                               static_cast<int>(a.in_off[j]), 2);
+          return make_uint4(d[0], d[1], d[2], d[3]);
+        }
       };
       if (__builtin_expect(t * 64 >= P, 1)) {  // wave-uniform: only the first steps hold virtual blocks
 #pragma unroll
@@ -690,8 +752,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             __attribute__((ext_vector_type(4))) unsigned int d = {acc[r].x, acc[r].y, acc[r].z, acc[r].w};
-            __builtin_amdgcn_raw_buffer_store_b128(d, rout, static_cast<uint32_t>(vb) * 16u,
-                                                   static_cast<int>(a.out_off[r]), 2);
+            if constexpr (WIDE) {
+              __builtin_amdgcn_raw_buffer_store_b128(d, make_rsrc_n(ob + a.out_off[r], static_cast<uint32_t>(wmax)),
+                                                     static_cast<uint32_t>(vb) * 16u, 0, 2);
+            } else {
+              __builtin_amdgcn_raw_buffer_store_b128(d, rout, static_cast<uint32_t>(vb) * 16u,
+                                                     static_cast<int>(a.out_off[r]), 2);
+            }
           }
         }
         if constexpr (XORC) store_data_hold(acc[0]);
@@ -722,10 +789,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES, 8
       for (int q = 0; q <= K; ++q) S[q] = g5_shift(s_t + kXoOff + kXoInv, S[q]);
     }
     const uint32_t init = last ? cr.init_last : cr.init_full;
+    int32_t tb = 0;
+    if constexpr (TAIL) tb = last ? static_cast<int32_t>(N & 15) : 0;
 #pragma unroll
     for (int q = 0; q < K + R; ++q) {
-      const uint32_t v = g5_lane_tree(s_t + g26_tree(E) - kG5Tree, S[q], lane);
+      uint32_t v = g5_lane_tree(s_t + g26_tree(E) - kG5Tree, S[q], lane);
       if (lane == q) {
+        if constexpr (TAIL) {
+          if (tb != 0) {
+            if constexpr (WIDE) v = xor_tail_wide<K>(e, ib, ob, q, v, static_cast<uint32_t>(m * 16), tb);
+            else v = xor_tail<K>(e, rin, rout, q, v, static_cast<uint32_t>(m * 16), tb);
+          }
+        }
         if (!e.verify) {
           cr.out[(s * (K + R) + q) * nwin + w] = crc_finish(v, init, cr.raw, cr.big_endian);
         } else if (q >= K) {
@@ -1157,7 +1232,7 @@ hipError_t launch_xor_stream(const EncCrcArgs &e, hipStream_t st) {
 }
 
 template <int K, int R>
-hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
+hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st, bool wide = false) {
   const int64_t units = e.code.nstripes * e.crc.nwin;
   const TabArgs<K * R> tabs = host_tabs<K * R>(e.code);
   // defaults measured on MI355X (scripts/tune_crc.py, profiles/r01/session2/tune_g26*.log): one wave per window
@@ -1180,6 +1255,19 @@ hipError_t launch_enc_crc_kr(const EncCrcArgs &e, hipStream_t st) {
     }
   }
   if constexpr (R == 1) {
+    if (wide && e.code.all_ones) {  // units 2 GiB or more apart (WIDE; TAIL for any length)
+      if (aligned16(e.code.len))
+        hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1, 4, false, false, false, false, true>), grid, block, 0, st, e,
+                           tabs);
+      else
+        hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1, 4, false, false, false, true, true>), grid, block, 0, st, e,
+                           tabs);
+      return hipGetLastError();
+    }
+    if (e.code.all_ones && (!aligned16(e.code.len) || !vec_ok(e.code))) {  // any length, any byte offset (TAIL)
+      hipLaunchKernelGGL((encode_crc_g26<K, R, 2, true, 1, 4, false, false, false, true>), grid, block, 0, st, e, tabs);
+      return hipGetLastError();
+    }
     if (e.code.all_ones && v != 2) {
       // XOR codec: groups of D = 2 steps, loads issued at the step (45 VGPRs for xor-2-1, 8 waves per SIMD).  Round 1
       // chose D = 4 with the next step's loads in flight (67 VGPRs; variant 3 now): C4 77.9 % vs 75.8 % then
@@ -1214,8 +1302,11 @@ bool encode_crc_supported(const CodeArgs &a, int64_t bpc) {
   OZEC_FUSED_SHAPES(OZEC_SHAPE_OK)
 #undef OZEC_SHAPE_OK
   CodeArgs rb = a;
-  if (!kr || bpc <= 0 || !aligned16(bpc) || !rebase32(rb)) return false;
-  return (aligned16(a.len) && vec_ok(a)) || encode_crc_nb_bytes_supported(a, bpc);
+  if (!kr || bpc <= 0 || !aligned16(bpc)) return false;
+  if (!rebase32(rb))  // units 2 GiB or more apart: the WIDE forms, one buffer descriptor per unit (round 6)
+    return a.len < (int64_t{1} << 31) && (encode_crc_nb_bytes_supported(a, bpc) || (a.all_ones && a.rows == 1));
+  // the XOR codec's per-window kernel takes any length and byte offset (encode_crc_g26 TAIL, round 6)
+  return (aligned16(a.len) && vec_ok(a)) || encode_crc_nb_bytes_supported(a, bpc) || (a.all_ones && a.rows == 1);
 }
 
 bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin, int64_t min_units) {
@@ -1228,15 +1319,29 @@ bool encode_crc_fused_pays(const CodeArgs &a, int64_t nwin, int64_t min_units) {
 hipError_t launch_encode_crc(const EncCrcArgs &e0, hipStream_t st) {
   if (e0.code.nstripes * e0.crc.nwin <= 0) return hipSuccess;
   EncCrcArgs e = e0;
-  if (!rebase32(e.code)) return hipErrorInvalidValue;
+  if (!rebase32(e.code)) {  // units 2 GiB or more apart: one buffer descriptor per unit (WIDE, round 6)
+    if (e0.code.len >= (int64_t{1} << 31)) return hipErrorInvalidValue;
+    const int k = e0.code.k, r = e0.code.rows;
+    if (e0.code.all_ones && r == 1) {
+      if (k == 2) return launch_enc_crc_kr<2, 1>(e0, st, true);
+      if (k == 3) return launch_enc_crc_kr<3, 1>(e0, st, true);
+      if (k == 6) return launch_enc_crc_kr<6, 1>(e0, st, true);
+      if (k == 10) return launch_enc_crc_kr<10, 1>(e0, st, true);
+      return hipErrorInvalidValue;
+    }
+    if (!encode_crc_nb_bytes_supported(e0.code, e0.crc.bpc)) return hipErrorInvalidValue;
+    return launch_encode_crc_lv(e0, st, 0, !aligned16(e0.code.len), true);
+  }
   // the RS shapes with whole windows and a short last window of any whole number of blocks: the nibble-table kernel
   // (fused_nb.hpp); 56 / 59 the streamed-input kernel (full windows only); variant 49 pins the per-window kernel
   const int v = g_tune.crc_variant.load(std::memory_order_relaxed);
   if (!aligned16(e.code.len) || !vec_ok(e.code)) {
     // byte-granular cells (a key's last stripe, odd unit strides): the nibble kernel's TAIL instantiations (nb_tail);
-    // a pinned variant without one falls back to the default
-    if (!encode_crc_nb_bytes_supported(e.code, e.crc.bpc)) return hipErrorInvalidValue;
-    return launch_encode_crc_lv(e, st, v, true);
+    // a pinned variant without one falls back to the default.  The XOR codec: its per-window kernel's TAIL form
+    if (!(e.code.all_ones && e.code.rows == 1)) {
+      if (!encode_crc_nb_bytes_supported(e.code, e.crc.bpc)) return hipErrorInvalidValue;
+      return launch_encode_crc_lv(e, st, v, true);
+    }
   }
   if (v == 0 || (v >= 50 && v < 300)) {
     const bool lv = v == 56 || v == 59;

@@ -257,7 +257,9 @@ bool encode_crc_lv_supported(const EncCrcArgs &e);
 // the nibble-table kernel (fused_nb.hpp): the same shapes, and a short last window of any whole number of 16-B blocks
 bool encode_crc_nb_supported(const EncCrcArgs &e);
 bool encode_crc_nb_bytes_supported(const CodeArgs &a, int64_t bpc);
-hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant, bool tail = false);
+// tail: cells of any length (nb_tail); wide: units 2 GiB or more apart (`e` NOT rebased; one descriptor per unit)
+hipError_t launch_encode_crc_lv(const EncCrcArgs &e, hipStream_t stream, int variant, bool tail = false,
+                                bool wide = false);
 
 // WorkQueue counter slots of the persistent kernels (device.hpp WorkQueue; pool in work_slots.cpp).  work_lease gives a
 // zeroed slot of the current device, not in use by any launch still running, or null (capturing stream, pool full,

@@ -25,6 +25,10 @@ run() {
       step "bench default"
       OZEC_BENCH_FULL=$OUT/bench_full.json timeout -k 10 900 python -u bench.py > "$OUT/bench.json" \
         2> "$OUT/bench.err" ;;
+    percall)
+      step "percall probe"
+      { timeout -k 10 120 scripts/percall_probe 1048576 200 && timeout -k 10 120 scripts/percall_probe 65536 500; } \
+        > "$OUT/percall.json" 2> "$OUT/percall.err" ;;
     *)
       step "unknown step $what"
       return 2 ;;

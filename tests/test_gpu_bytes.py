@@ -7,6 +7,8 @@ nb_tail (bytewise CRC register update, GF products from the s_gf nibble products
 accesses for the blocks.  Checked bit-exact against oracle.rs_encode / oracle.crc_windows (Checksum.java:157-200,
 RSRawEncoder), with guard bytes around the batch that must stay untouched.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -21,6 +23,7 @@ from ozone_amd import _lib as L  # noqa: E402
 from ozone_amd import rawcoder as rc  # noqa: E402
 
 DEV = "cuda:0"
+PRODUCTION_ROUTING = os.environ.get("OZEC_TEST_PRODUCTION_ROUTING") == "1"
 GUARD = 64
 
 
@@ -174,3 +177,76 @@ def test_packed_odd_cells_xor_and_generic_shapes(codec, k, p, n):
         for u, cell in enumerate(list(data[s]) + list(ref)):
             assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, cell, bpc)).all(), (codec, k, p, n, s, u)
         assert (o[s, 0] == data[s, k - 1]).all(), (codec, k, p, n, s)
+
+
+def _routes():
+    import ctypes
+    f, u = ctypes.c_uint64(), ctypes.c_uint64()
+    assert L.lib().ozec_fused_routes(ctypes.byref(f), ctypes.byref(u)) == 0
+    return f.value, u.value
+
+
+@pytest.mark.parametrize("k", [2, 3, 6, 10])
+@pytest.mark.parametrize("n", [1, 15, 1007, 16384 + 3, 50001, 3 * 16384 + 15])
+@pytest.mark.parametrize("shift", [0, 3])
+def test_xor_fused_any_length_and_offset(k, n, shift):
+    """the XOR codec's fused kernel (encode_crc_g26 TAIL) takes cells of any length at any byte
+    offset -- packed stripes of xor-k-1 (unit stride n) -- in ONE launch for encode + CRC32C and for the fused
+    reconstruction (verify + decode + CRC), where round 5 ran coding and CRC as two kernels.  Parity, window CRCs,
+    the rebuilt unit, its CRCs and the first failing (unit, window) of a planted corruption vs the oracle
+    (XORRawEncoder.java:39-85, XORRawDecoder.java:45-61, Checksum.java:157-200); guard bytes untouched; both calls
+    counted on the fused route."""
+    p, S, bpc = 1, 3, 16384
+    rng = np.random.default_rng([k, n, shift, 13])
+    data = rng.integers(0, 256, (S, k, n), dtype=np.uint8)
+    flat = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
+    flat[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)[:, :k] = data
+    d = to_dev(flat)
+    base = d[GUARD + shift:]
+    nwin = -(-n // bpc)
+    crcs = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    conf = rc.ECReplicationConfig(k, p, "xor")
+    f0, u0 = _routes()
+    rc.RawErasureEncoder(conf).encode_crc_batch(base, (k + p) * n, n, base[k * n:], (k + p) * n, n, S, n,
+                                                ck.ChecksumType.CRC32C, bpc, crcs)
+    f1, u1 = _routes()
+    assert PRODUCTION_ROUTING or (f1 - f0, u1 - u0) == (1, 0), "the encode did not take the fused kernel"
+    got, c = to_host(d), to_host(crcs).view(np.uint32)
+    assert (got[:GUARD + shift] == 0xA5).all() and (got[GUARD + shift + S * (k + p) * n:] == 0xA5).all()
+    units = got[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n).copy()
+    for s in range(S):
+        ref = oracle.xor_encode(list(data[s]))
+        assert (units[s, k] == ref).all(), (k, n, shift, s)
+        for u in range(k + 1):
+            assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, units[s, u], bpc)).all(), (k, n, shift, s, u)
+    # reconstruction of data unit 1 from the other k units, stored CRCs checked; stripe 1 has one corrupted byte in
+    # the last unit read
+    erased = [1]
+    present = [u for u in range(k + 1) if u not in erased]
+    stored = c.copy()
+    bad = units.copy()
+    bad[:, 1] = 0xEE
+    pos = n // 2
+    bad[1, present[-1], pos] ^= 0x10
+    flat2 = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
+    flat2[GUARD + shift:GUARD + shift + S * (k + p) * n] = bad.reshape(-1)
+    d2 = to_dev(flat2)
+    out = torch.zeros((S, 1, n + 5), dtype=torch.uint8, device=DEV)
+    ocrc = torch.zeros((S, 1, nwin), dtype=torch.int32, device=DEV)
+    mism = torch.zeros(S, dtype=torch.int32, device=DEV)
+    ob = out.view(-1)[shift:]  # outputs at odd offsets too
+    f0, u0 = _routes()
+    rc.RawErasureDecoder(conf).reconstruct_crc_batch(
+        d2[GUARD + shift:], (k + p) * n, n, present, erased, ob, n + 5, n, S, n, ck.ChecksumType.CRC32C, bpc, ocrc,
+        d_expected=to_dev(stored.view(np.int32)), d_mismatch=mism)
+    f1, u1 = _routes()
+    assert PRODUCTION_ROUTING or (f1 - f0, u1 - u0) == (1, 0), "the reconstruction did not take the fused kernel"
+    o = to_host(out).reshape(-1)[shift:shift + S * (n + 5)]
+    oc, m = to_host(ocrc).view(np.uint32), to_host(mism)
+    for s in range(S):
+        rebuilt = o[s * (n + 5):s * (n + 5) + n]
+        if s != 1:
+            assert (rebuilt == data[s, 1]).all(), (k, n, shift, s)
+            assert m[s] == -1
+        assert (oc[s, 0] == oracle.crc_windows(oracle.CRC32C, rebuilt, bpc)).all(), (k, n, shift, s)
+    assert m[1] == present[-1] * nwin + pos // bpc

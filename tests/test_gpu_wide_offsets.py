@@ -2,10 +2,13 @@
 
 The vector kernels address a stripe through 32-bit buffer offsets after rebase32 (device.hpp); a layout whose units
 lie further apart -- a caller's stripes scattered over a large HBM pool, unit stride 768 MiB here -- must take the
-64-bit paths (typed-pointer kernels when 16-B aligned, the byte kernels otherwise) and still produce the oracle's
+64-bit paths (one buffer descriptor per unit: gf_code_vec WIDE, and since round 6 the fused kernels' WIDE forms, in
+ONE launch for the fused shapes; typed-pointer / byte kernels for the other schemas) and still produce the oracle's
 parity, decoded units and CRCs (RSUtil.encodeData, XORRawEncoder, Checksum.computeChecksum) and a clean verified
 reconstruction (ChecksumData.java:118-150), aligned and at odd byte offsets, with the bytes after the units untouched.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -19,7 +22,16 @@ from ozone_amd import checksum as ck  # noqa: E402
 from ozone_amd import rawcoder as rc  # noqa: E402
 
 DEV = "cuda:0"
+PRODUCTION_ROUTING = os.environ.get("OZEC_TEST_PRODUCTION_ROUTING") == "1"
 US = 768 << 20  # unit stride: 768 MiB
+
+
+def _routes():
+    import ctypes
+    from ozone_amd import _lib as L
+    f, u = ctypes.c_uint64(), ctypes.c_uint64()
+    assert L.lib().ozec_fused_routes(ctypes.byref(f), ctypes.byref(u)) == 0
+    return f.value, u.value
 
 
 @pytest.mark.parametrize("codec,k,p", [("rs", 6, 3), ("xor", 2, 1), ("rs", 4, 2), ("rs", 10, 4)])
@@ -38,15 +50,21 @@ def test_units_more_than_2gib_apart(codec, k, p, shift, n):
         return base[off:off + n]
     for s in range(S):
         for u in range(k):
-            at(s, u).copy_(torch.from_numpy(data[s, u]))
+            at(s, u).copy_(to_dev(data[s, u]))
         for u in range(k, k + p):
             at(s, u).fill_(0x3C)
     guard_after = [base[s * ss + u * US + n:s * ss + u * US + n + 16].clone() for s in range(S) for u in range(k + p)]
     conf = rc.ECReplicationConfig(k, p, codec)
     nwin = -(-n // bpc)
     crcs = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    fused_shape = (codec, k, p) in (("rs", 6, 3), ("xor", 2, 1), ("rs", 10, 4))
+    r0 = _routes()
     rc.RawErasureEncoder(conf).encode_crc_batch(base, ss, US, base[k * US:], ss, US, S, n, ck.ChecksumType.CRC32C,
                                                 bpc, crcs)
+    r1 = _routes()
+    # round 6: the fused shapes take ONE fused launch (one buffer descriptor per unit, WIDE), any length and offset
+    if not PRODUCTION_ROUTING:  # (libozec's own routing sends batches this small to the unfused kernels)
+        assert (r1[0] - r0[0], r1[1] - r0[1]) == ((1, 0) if fused_shape else (0, 1)), (codec, k, p, r0, r1)
     erased = [0] if codec == "xor" else [0, k]
     present = [u for u in range(k + p) if u not in erased][:k]
     out = torch.zeros((S, len(erased), n), dtype=torch.uint8, device=DEV)
@@ -54,9 +72,14 @@ def test_units_more_than_2gib_apart(codec, k, p, shift, n):
     rout = torch.zeros((S, len(erased), n), dtype=torch.uint8, device=DEV)
     rcrc = torch.zeros((S, len(erased), nwin), dtype=torch.int32, device=DEV)
     mism = torch.zeros(S, dtype=torch.int32, device=DEV)
+    r0 = _routes()
     rc.RawErasureDecoder(conf).reconstruct_crc_batch(base, ss, US, present, erased, rout, len(erased) * n, n, S, n,
                                                      ck.ChecksumType.CRC32C, bpc, rcrc, d_expected=crcs,
                                                      d_mismatch=mism)
+    r1 = _routes()
+    rec_fused = (codec, k, p) in (("rs", 6, 3), ("xor", 2, 1), ("rs", 10, 4))  # rs-6-3 erasing 2: shape (6, 2)
+    if not PRODUCTION_ROUTING:
+        assert (r1[0] - r0[0], r1[1] - r0[1]) == ((1, 0) if rec_fused else (0, 1)), (codec, k, p, r0, r1)
     wcrc = torch.zeros((k + p, nwin), dtype=torch.int32, device=DEV)  # every unit of stripe 1, cell stride US
     ck.checksum_windows_batch(ck.ChecksumType.CRC32, base[ss:], US, k + p, n, bpc, wcrc)
     torch.cuda.synchronize()

@@ -19,11 +19,11 @@ def _b(v):
     return f"Lb{int(v)}E"
 
 
-def _nb(K, R, D, NB, WPB, DYN, H, tail, cv=False):
-    """Mangled template-argument list of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H, TAIL, CV> (XO, EM
-    on), closed, so that it names exactly one instantiation."""
+def _nb(K, R, D, NB, WPB, DYN, H, tail, cv=False, wide=False):
+    """Mangled template-argument list of encode_crc_nb<K, R, D, NB, WPB, 4, 2, true, DYN, XO, EM, H, TAIL, CV, WIDE>
+    (XO, EM on), closed, so that it names exactly one instantiation."""
     return "encode_crc_nbI" + "".join([_i(K), _i(R), _i(D), _i(NB), _i(WPB), _i(4), _i(2), _b(1), _i(DYN), _b(1),
-                                       _b(1), _i(H), _b(tail), _b(cv)]) + "EEvN"
+                                       _b(1), _i(H), _b(tail), _b(cv), _b(wide)]) + "EEvN"
 
 
 def _defaults():
@@ -39,6 +39,11 @@ def _defaults():
     # 231: the combined-verify reconstruction default for rs-10-x and rs-6-x
     out += [_nb(10, R, 1, 5, 16, 1, 10, False, True) for R in (1, 2, 3, 4)]
     out += [_nb(6, R, 1, 3, 16, 1, 6, False, True) for R in (1, 2, 3)]
+    # round 6: units 2 GiB or more apart (WIDE, one descriptor per unit), 16-B cells and byte tails
+    for t in (False, True):
+        out += [_nb(10, R, 1, 5, 8, 0, 10, t, False, True) for R in (1, 2, 3, 4)]
+        out += [_nb(6, R, 1, 3, 8, 0, 6, t, False, True) for R in (1, 2, 3)]
+        out += [_nb(3, R, 1, 3, 8, 0, 3, t, False, True) for R in (1, 2)]
     return out
 
 

@@ -1169,6 +1169,7 @@ def _jni_percall_bin():
                     os.path.join(ROOT, "jni", "ozec_marshal.c"), os.path.join(mock, "mockjni.c"),
                     os.path.join(ROOT, "tests", "native", "jni_percall.c"), "-L", lib, "-lozec", "-lpthread",
                     "-Wl,--wrap=ozec_encode,--wrap=ozec_decode,--wrap=ozec_crc_update,--wrap=ozec_checksum_windows,"
+                    "--wrap=ozec_encode_cb,--wrap=ozec_decode_cb,"
                     "--wrap=ozec_host_alloc,--wrap=ozec_host_free", f"-Wl,-rpath,{lib}", "-o", out],
                    check=True, capture_output=True, timeout=120)
     _JNI_BIN = out

@@ -124,6 +124,20 @@ int ozec_encode(ozec_coder *enc, const uint8_t *const *inputs, uint8_t *const *o
  *      ascending index order are used (RSRawDecoder.java:79-82).  erased[i] <-> outputs[i]. ----------- */
 int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased, int num_erased,
                 uint8_t *const *outputs, size_t len);
+/* The same two calls with the caller moving the bytes (round 6; the JNI glue's byte[] arrays, which it may hold
+ * pinned only while it copies, AbstractNativeRawEncoder.java:75-86 copying them likewise): libozec runs its staged
+ * pipeline in column chunks and calls fill(user, off, len, dst) to copy bytes [off, off + len) of every input into
+ * dst[i] (its pinned staging; encode: the k inputs in order; decode: one slot per unit, k + p of them, NULL for the
+ * units the decoder does not read) and drain(user, off, len, src) to copy the outputs' bytes [off, off + len) out of
+ * src[r] (encode: the p outputs; decode: the n_erased outputs in erasedIndexes order; XOR outputs past the coded one
+ * are zero) -- so the caller's copies of one chunk overlap the GPU's work on the other.  Both run on the calling
+ * thread, never while a device call of this thread is being made; a nonzero return ends the call with that value.
+ * present_units[u] != 0: the caller has unit u (ozec_decode's non-null inputs). */
+typedef int (*ozec_fill_fn)(void *user, size_t off, size_t len, uint8_t *const *dst);
+typedef int (*ozec_drain_fn)(void *user, size_t off, size_t len, const uint8_t *const *src);
+int ozec_encode_cb(ozec_coder *encoder, size_t len, ozec_fill_fn fill, ozec_drain_fn drain, void *user);
+int ozec_decode_cb(ozec_coder *decoder, const uint8_t *present_units, const int *erased, int n_erased, size_t len,
+                   ozec_fill_fn fill, ozec_drain_fn drain, void *user);
 
 /* ---- device-resident forms (same semantics, device pointers, async on `stream`) ---------------------- */
 int ozec_encode_device(ozec_coder *enc, const uint8_t *const *d_inputs, uint8_t *const *d_outputs,

@@ -109,15 +109,14 @@ static void refs_free(JNIEnv *env, array_set *as) {
 }
 
 /* ---------------------------------------------------------------- heap arrays: copied, never pinned across the GPU
- * A byte[] pinned with GetPrimitiveArrayCritical for the whole call would hold the VM's GC locker through staging, H2D,
- * kernel and D2H (~0.3 ms per rs-6-3 stripe of 1 MiB cells; every ECKeyOutputStream writer passes heap buffers,
- * ECKeyOutputStream.java:701).  Instead each call copies the regions it reads into a pinned arena (ozec_host_alloc:
- * pinned, on a listed GPU's NUMA node; the arrays held critical for that copy only, copy_regions), runs on the arena --
- * libozec DMAs pinned memory in place, one rectangular copy each way for cells at one stride -- and copies the outputs
- * back the same way: the two host copies libozec's own staging would make, with no JNI pin while libozec works, as the
- * reference's bridge
- * copies heap arrays into direct buffers (AbstractNativeRawEncoder.java:80-93).  Calls are cut in column chunks of
- * HEAP_CHUNK bytes per cell (coding is byte-position-wise), so an arena holds at most (k + p) x 4 MiB.
+ * A byte[] pinned with GetPrimitiveArrayCritical for the whole call would hold the VM's GC locker through staging, the
+ * PCIe transfers and the kernel (~0.2 ms per rs-6-3 stripe of 1 MiB cells; every ECKeyOutputStream writer passes heap
+ * buffers, ECKeyOutputStream.java:701).  Instead the regions a call reads are copied into pinned memory and its outputs
+ * back, the arrays held critical for each copy only, as the reference's bridge copies heap arrays into direct buffers
+ * (AbstractNativeRawEncoder.java:80-93).  Coder calls (round 6) copy into libozec's own pinned staging through the
+ * ozec_encode_cb / ozec_decode_cb callbacks, chunk by chunk while the GPU works on the previous chunk (heap_code);
+ * checksum calls copy into a pinned arena leased for the call.  Calls are cut in column pieces of HEAP_CHUNK bytes per
+ * cell (coding and window CRCs are position-wise), so a call's staging is at most (k + p) x 4 MiB.
  * Arenas come from a process-wide pool of ARENA_POOL, leased for one call: pinned memory stays bounded however many
  * Java threads call at once; a call that finds every arena leased gets a pageable one of its own (libozec then stages
  * it through its pinned slots), so no call waits for another. */
@@ -293,68 +292,65 @@ static int copy_regions(JNIEnv *env, const array_set *as, const ozm_buf *bufs, i
   return 0;
 }
 
-/* the present arrays' regions [offset + off, + cl) into consecutive arena slots of `stride` bytes from slot `first`
- * (absent ones take no slot); stage[i] describes the copy as a buffer at offset 0 */
-static int copy_in(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl, uint8_t *base,
-                   int64_t stride, int first, ozm_buf *stage) {
-  int slot = first;
+
+
+
+
+
+
+/* encode (erased == NULL) or decode of heap arrays already validated by ozm_*_check (round 6): libozec's staged
+ * pipeline with the glue moving the bytes (ozec_encode_cb / ozec_decode_cb).  libozec cuts each HEAP_CHUNK piece of the
+ * call into column chunks and asks for chunk c's inputs (heap_fill: the arrays held critical for that copy only,
+ * copy_regions) while its kernel works on chunk c - 1 straight from its pinned staging, and hands back each chunk's
+ * outputs (heap_drain) -- the copies overlap the GPU instead of preceding and following it.  No array is pinned while
+ * libozec waits for the device: the callbacks run between its device operations and release every pin before they
+ * return. */
+typedef struct {
+  JNIEnv *env;
+  const array_set *ai, *ao;
+  const ozm_buf *ib, *ob;
+  int64_t base; /* this piece's offset within the call */
+} heap_job;
+
+static void staging_bufs(const array_set *as, const void *const *p, size_t len, ozm_buf *stage) {
   for (int i = 0; i < as->n; ++i) {
     memset(&stage[i], 0, sizeof(stage[i]));
-    if (!as->arr[i]) continue;
-    stage[i].present = 1;
-    stage[i].base = base + (int64_t)slot++ * stride;
-    stage[i].capacity = cl;
-  }
-  return copy_regions(env, as, bufs, off, cl, stage, 1);
-}
-
-static void out_slots(const array_set *as, int64_t cl, uint8_t *base, int64_t stride, int first, ozm_buf *stage) {
-  for (int i = 0; i < as->n; ++i) {
-    memset(&stage[i], 0, sizeof(stage[i]));
-    stage[i].present = as->arr[i] != NULL;
-    stage[i].base = base + (int64_t)(first + i) * stride;
-    stage[i].capacity = cl;
+    stage[i].present = p[i] != NULL;
+    stage[i].base = p[i];
+    stage[i].capacity = (int64_t)len;
   }
 }
 
-static int copy_out(JNIEnv *env, const array_set *as, const ozm_buf *bufs, int64_t off, int64_t cl,
-                    const ozm_buf *stage) {
-  return copy_regions(env, as, bufs, off, cl, stage, 0);
+static int heap_fill(void *user, size_t off, size_t len, uint8_t *const *dst) {
+  heap_job *j = (heap_job *)user;
+  ozm_buf stage[MAX_BUFS];
+  staging_bufs(j->ai, (const void *const *)dst, len, stage);
+  return copy_regions(j->env, j->ai, j->ib, j->base + (int64_t)off, (int64_t)len, stage, 1) ? -1 : 0;
 }
 
-static int present_count(const array_set *as) {
-  int n = 0;
-  for (int i = 0; i < as->n; ++i) n += as->arr[i] != NULL;
-  return n;
+static int heap_drain(void *user, size_t off, size_t len, const uint8_t *const *src) {
+  heap_job *j = (heap_job *)user;
+  ozm_buf stage[MAX_BUFS];
+  staging_bufs(j->ao, (const void *const *)src, len, stage);
+  return copy_regions(j->env, j->ao, j->ob, j->base + (int64_t)off, (int64_t)len, stage, 0) ? -1 : 0;
 }
 
-/* encode (erased == NULL) or decode of heap arrays already validated by ozm_*_check */
 static int heap_code(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_buf *ib, const array_set *ao,
                      const ozm_buf *ob, const int *erased, int ne, int64_t len, ozm_status *st) {
-  ozm_buf si[MAX_BUFS], so[MAX_BUFS];
-  const int nin = present_count(ai);
-  arena_lease l;
-  arena_lease_begin(&l);
-  int rc = 0;
-  for (int64_t off = 0; off < len && !rc; off += HEAP_CHUNK) {
+  heap_job j = {env, ai, ao, ib, ob, 0};
+  uint8_t present[MAX_BUFS];
+  for (int i = 0; i < ai->n; ++i) present[i] = ai->arr[i] != NULL;
+  for (int64_t off = 0; off < len; off += HEAP_CHUNK) {
     const int64_t cl = len - off < HEAP_CHUNK ? len - off : HEAP_CHUNK;
-    const int64_t stride = round_up(cl, ARENA_ALIGN);
-    uint8_t *a = arena(&l, (size_t)((int64_t)(nin + ao->n) * stride), st);
-    if (!a) {
-      rc = st->code;
-      break;
+    j.base = off;
+    const int rc = erased ? ozec_decode_cb(h, present, erased, ne, (size_t)cl, heap_fill, heap_drain, &j)
+                          : ozec_encode_cb(h, (size_t)cl, heap_fill, heap_drain, &j);
+    if (rc) {
+      if ((*env)->ExceptionCheck(env)) return ozm_fail(OZEC_ENOMEM, "a Java array could not be copied", st);
+      return ozm_fail(rc, NULL, st);
     }
-    if (copy_in(env, ai, ib, off, cl, a, stride, 0, si)) {
-      rc = ozm_fail(OZEC_ENOMEM, "a Java array could not be read", st);  /* its exception is pending */
-      break;
-    }
-    out_slots(ao, cl, a, stride, nin, so);
-    rc = erased ? ozm_decode(h, si, ai->n, erased, ne, so, ao->n, cl, st)
-                : ozm_encode(h, si, ai->n, so, ao->n, cl, st);
-    if (!rc && copy_out(env, ao, ob, off, cl, so)) rc = ozm_fail(OZEC_ENOMEM, "a Java array could not be written", st);
   }
-  arena_lease_end(&l);
-  return rc;
+  return 0;
 }
 
 static int int_array(JNIEnv *env, jintArray a, int *out, int max, int *n, ozm_status *st) {

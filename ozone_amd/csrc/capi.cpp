@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -109,8 +110,8 @@ struct Slot {
     return OZEC_OK;
   }
 
-  int reserve(size_t bytes, size_t nevents) {
-    if (bytes > pinned_cap || bytes > dbuf_cap) drop_graphs();
+  int reserve(size_t bytes, size_t nevents, bool with_device = true) {
+    if (bytes > pinned_cap || (with_device && bytes > dbuf_cap)) drop_graphs();
     if (bytes > pinned_cap) {
       if (pinned) (void)ozec::pinned_free(pinned);
       pinned = nullptr;
@@ -120,7 +121,7 @@ struct Slot {
         return fail(OZEC_ENOMEM, "cannot pin " + std::to_string(cap) + " bytes of staging memory");
       pinned_cap = cap;
     }
-    if (bytes > dbuf_cap) {
+    if (with_device && bytes > dbuf_cap) {
       if (dbuf) (void)hipFree(dbuf);
       dbuf = nullptr;
       dbuf_cap = 0;
@@ -436,10 +437,31 @@ bool range_pinned(const void *p, size_t n) {
 //   gkey (optional): the bytes the launch depends on besides the slot's buffers and the chunk geometry; with it, a
 //   call of one staged chunk up to host_graph bytes per unit replays a cached graph of its three stream operations
 //   (one graph launch instead of three operations: 45 -> 34 us for a 64 KiB-cell rs-6-3 stripe)
+// the address at which the GPU reaches pinned host memory p (registered or hipHostMalloc'ed; the same address on ROCm),
+// null when p is not GPU-mapped
+uint8_t *dev_view(const void *p) {
+  void *dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, const_cast<void *>(p), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return static_cast<uint8_t *>(dp);
+}
+
+// caller-moved bytes (ozec_encode_cb / ozec_decode_cb): fill puts input bytes [off, off + cl) of every input into the
+// staging pointers, drain takes output bytes [off, off + cl) of every output from them; nonzero ends the call
+struct HostCopies {
+  std::function<int(size_t off, size_t cl, uint8_t *const *dst)> fill;
+  std::function<int(size_t off, size_t cl, const uint8_t *const *src)> drain;
+};
+
+//   zc: the launch may read and write pinned host memory in place (zero copy, TuneKnobs::host_zero_copy): the kernel
+//   reaches the caller's pinned buffers, or the slot's pinned staging, over PCIe, with no H2D / D2H operation
+//   cb: the caller moves the bytes (in / out unused): the staged path with its copies replaced by cb's
 template <class Launch, class OutBytes, class OutPos>
 int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, size_t gran, int nout,
                     uint8_t *const *out, OutBytes out_bytes, OutPos out_pos, Launch launch,
-                    const std::vector<uint8_t> *gkey = nullptr) {
+                    const std::vector<uint8_t> *gkey = nullptr, bool zc = false, const HostCopies *cb = nullptr) {
   constexpr size_t kMaxChunks = 64;
   SlotLease lease(ctx);
   if (int rc = ctx->acquire(&lease.slot)) return rc;
@@ -454,6 +476,13 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
   size_t chunk = static_cast<size_t>(std::max<int64_t>(1, want));
   chunk = std::max(chunk, (len + kMaxChunks - 1) / kMaxChunks);
   chunk = std::max(gran, chunk / gran * gran);
+  // zero copy for a call alone on the GPU's slots: concurrent callers keep the SDMA copies, which together fill the link
+  // (four JNI threads: 52 GB/s through copies, 43 with every call zero-copy, profiles/r06/zero_copy/)
+  const int64_t zc_grid = zc && ctx->leased.load() <= 1 ? ozec::g_tune.host_zero_copy.load(std::memory_order_relaxed) : 0;
+  // zero copy, one call in one chunk of at least 2 x 256 KiB per unit: two chunks, so the staging copies of one half
+  // overlap the kernel on the other (1 MiB-cell rs-6-3 stripe from pageable cells 289 -> 239 us; four chunks 360,
+  // profiles/r06/percall/)
+  if (zc_grid > 0 && chunk >= len && len >= 2 * (size_t{256} << 10)) chunk = std::max(gran, round_up((len + 1) / 2, gran));
   if (chunk >= len) chunk = len;
   const size_t nch = (len + chunk - 1) / chunk;
   const size_t cp = round_up(chunk, kStageAlign), op = round_up(out_bytes(chunk), kStageAlign);
@@ -482,15 +511,30 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
   int64_t sin = 0, sout = 0;
   const size_t obytes = out_bytes(len);
   std::vector<const uint8_t *> obase(nout);
-  for (int r = 0; r < nout; ++r) obase[r] = out[r] + out_pos(0);
-  const bool rect = stride_of(in, nin, len, &sin) && stride_of(obase.data(), nout, obytes, &sout);
-  bool direct = rect || len >= (256u << 10);
-  if (rect && direct) {
-    direct = range_pinned(in[0], static_cast<size_t>(sin) * (nin - 1) + len) &&
-             range_pinned(obase[0], static_cast<size_t>(sout) * (nout - 1) + obytes);
-  } else {
-    for (int j = 0; j < nin && direct; ++j) direct = range_pinned(in[j], len);
-    for (int r = 0; r < nout && direct; ++r) direct = range_pinned(obase[r], obytes);
+  bool rect = false, direct = false;
+  if (!cb) {
+    for (int r = 0; r < nout; ++r) obase[r] = out[r] + out_pos(0);
+    rect = stride_of(in, nin, len, &sin) && stride_of(obase.data(), nout, obytes, &sout);
+    direct = rect || len >= (256u << 10);
+    if (rect && direct) {
+      direct = range_pinned(in[0], static_cast<size_t>(sin) * (nin - 1) + len) &&
+               range_pinned(obase[0], static_cast<size_t>(sout) * (nout - 1) + obytes);
+    } else {
+      for (int j = 0; j < nin && direct; ++j) direct = range_pinned(in[j], len);
+      for (int r = 0; r < nout && direct; ++r) direct = range_pinned(obase[r], obytes);
+    }
+  }
+  if (direct && rect && zc_grid > 0) {
+    // zero copy (round 6): the kernel reads the caller's pinned inputs and writes its pinned outputs over PCIe -- one
+    // launch, no copy operation (HIP's SDMA engines run a copy at the link rate on some streams and at a third of it
+    // on others, profiles/r06/engines/)
+    uint8_t *din = dev_view(in[0]), *dout = dev_view(obase[0]);
+    if (din && dout) {
+      ozec::GridCap cap(zc_grid);
+      OZEC_HIP(launch(din, sin, dout, sout, 0, len, s->stream));
+      OZEC_HIP(hipStreamSynchronize(s->stream));
+      return OZEC_OK;
+    }
   }
   if (direct) {
     const size_t dcp = round_up(len, kStageAlign), dop = round_up(obytes, kStageAlign);
@@ -548,18 +592,55 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     OZEC_HIP(hipStreamSynchronize(s->stream));
     return OZEC_OK;
   }
-  if (int rc = s->reserve(per_chunk * nch, nch)) return rc;
+  if (int rc = s->reserve(per_chunk * nch, nch, zc_grid <= 0)) return rc;
   // other calls in flight: their copies and DMA share host DRAM with this call's staging copies (copy_pool.hpp)
   const bool shared = ctx->leased.load() > 1 || nch > 1;
   auto unstage = [&](size_t c) -> int {
     OZEC_HIP(hipEventSynchronize(s->events[c]));
     const size_t off = c * chunk, cl = std::min(chunk, len - off);
     const uint8_t *src = s->pinned + c * per_chunk + nin * cp;
+    if (cb) {
+      std::vector<const uint8_t *> srcs(nout);
+      for (int r = 0; r < nout; ++r) srcs[r] = src + r * op;
+      return cb->drain(off, cl, srcs.data());
+    }
     std::vector<ozec::CopyTask> tasks;
     for (int r = 0; r < nout; ++r) tasks.push_back({out[r] + out_pos(off), src + r * op, out_bytes(cl)});
     ozec::parallel_copy(tasks, ozec::CopyDir::kFromStaging, shared, ctx->numa);
     return OZEC_OK;
   };
+  // chunk c's inputs into the staging at h
+  auto stage = [&](size_t c, uint8_t *h) -> int {
+    const size_t off = c * chunk, cl = std::min(chunk, len - off);
+    if (cb) {
+      std::vector<uint8_t *> dsts(nin);
+      for (int j = 0; j < nin; ++j) dsts[j] = h + j * cp;
+      return cb->fill(off, cl, dsts.data());
+    }
+    std::vector<ozec::CopyTask> tasks;
+    for (int j = 0; j < nin; ++j) tasks.push_back({h + j * cp, in[j] + off, cl});
+    ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, shared, ctx->numa);
+    return OZEC_OK;
+  };
+  if (zc_grid > 0) {
+    // zero copy from the slot's pinned staging: stage chunk c, one kernel launch on it in place, unstage chunk c - 1
+    // while the kernel runs
+    uint8_t *hz = dev_view(s->pinned);
+    if (hz) {
+      ozec::GridCap cap(zc_grid);
+      for (size_t c = 0; c < nch; ++c) {
+        const size_t off = c * chunk, cl = std::min(chunk, len - off);
+        uint8_t *h = s->pinned + c * per_chunk, *hd = hz + c * per_chunk;
+        if (int rc = stage(c, h)) return rc;
+        OZEC_HIP(launch(hd, static_cast<int64_t>(cp), hd + nin * cp, static_cast<int64_t>(op), off, cl, s->stream));
+        OZEC_HIP(hipEventRecord(s->events[c], s->stream));
+        if (c > 0)
+          if (int rc = unstage(c - 1)) return rc;
+      }
+      return unstage(nch - 1);
+    }
+    if (int rc = s->reserve(per_chunk * nch, nch, true)) return rc;  // not GPU-mapped: the copy path below
+  }
   const int64_t graph_max = ozec::g_tune.host_graph.load(std::memory_order_relaxed);
   if (gkey && nch == 1 && graph_max > 0 && len <= static_cast<size_t>(graph_max)) {
     std::vector<uint8_t> key = *gkey;
@@ -586,9 +667,7 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
       }
     }
     if (ex) {
-      std::vector<ozec::CopyTask> tasks;
-      for (int j = 0; j < nin; ++j) tasks.push_back({h + j * cp, in[j], len});
-      ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, shared, ctx->numa);
+      if (int rc = stage(0, h)) return rc;
       OZEC_HIP(hipGraphLaunch(ex, s->stream));
       OZEC_HIP(hipEventRecord(s->events[0], s->stream));
       return unstage(0);
@@ -597,9 +676,7 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
   for (size_t c = 0; c < nch; ++c) {
     const size_t off = c * chunk, cl = std::min(chunk, len - off);
     uint8_t *h = s->pinned + c * per_chunk, *d = s->dbuf + c * per_chunk;
-    std::vector<ozec::CopyTask> tasks;
-    for (int j = 0; j < nin; ++j) tasks.push_back({h + j * cp, in[j] + off, cl});
-    ozec::parallel_copy(tasks, ozec::CopyDir::kToStaging, shared, ctx->numa);
+    if (int rc = stage(c, h)) return rc;
     OZEC_HIP(hipMemcpyAsync(d, h, nin * cp, hipMemcpyHostToDevice, s->stream));
     OZEC_HIP(launch(d, static_cast<int64_t>(cp), d + nin * cp, static_cast<int64_t>(op), off, cl, s->stream));
     OZEC_HIP(hipMemcpyAsync(h + nin * cp, d + nin * cp, nout * op, hipMemcpyDeviceToHost, s->stream));
@@ -611,7 +688,8 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
 }
 
 // host-buffer coding job (encode / decode): rows outputs from nin inputs
-int staged_code(DevCtx *ctx, const CodeArgs &tmpl, const uint8_t *const *in, uint8_t *const *out, size_t len) {
+int staged_code(DevCtx *ctx, const CodeArgs &tmpl, const uint8_t *const *in, uint8_t *const *out, size_t len,
+                const HostCopies *cb = nullptr) {
   // graph key: the coding parameters the kernel launch reads (the pointers and offsets are the slot's, set below)
   std::vector<uint8_t> key;
   auto put = [&key](const void *p, size_t n) {
@@ -635,7 +713,7 @@ int staged_code(DevCtx *ctx, const CodeArgs &tmpl, const uint8_t *const *in, uin
         for (int r = 0; r < a.rows; ++r) a.out_off[r] = r * out_stride;
         return ozec::launch_code(a, st);
       },
-      &key);
+      &key, true, cb);
 }
 
 }  // namespace
@@ -889,6 +967,83 @@ int ozec_decode(ozec_coder *dec, const uint8_t *const *inputs, const int *erased
   if (int rc = staged_code(ctx, a, in.data(), outputs, len)) return rc;
   // XOR decode: only erasedIndexes[0] is recovered, further outputs stay zero-filled (XORRawDecoder.java:45-61)
   for (int r = a.rows; r < n_erased; ++r) std::memset(outputs[r], 0, len);
+  return OZEC_OK;
+}
+
+// ---- host coding with caller-moved bytes (round 6; the JNI glue's heap arrays) --------------------------------
+
+int ozec_encode_cb(ozec_coder *enc, size_t len, ozec_fill_fn fill, ozec_drain_fn drain, void *user) {
+  ozec::StatScope stat_(OZEC_OP_ENCODE, enc ? static_cast<uint64_t>(enc->k) * len : 0);
+  if (int rc = check_open(enc, "encode")) return rc;
+  if (enc->decoder) return fail(OZEC_EINVAL, "not an encoder");
+  if (!fill || !drain) return fail(OZEC_EINVAL, "null copy callback");
+  if (len == 0) return OZEC_OK;
+  const int k = enc->k, rows = out_rows(enc), p = enc->p;
+  ozec::DeviceScope ds(enc->device);
+  if (!ds.ok()) return fail(OZEC_EDEVICE, "cannot select device " + std::to_string(enc->device));
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  CodeArgs a{};
+  std::vector<uint8_t> coef;
+  encode_rows(enc, coef);
+  fill_coef(a, rows, k, coef.data());
+  // XOR with p > 1: the outputs past the first are zero (XORRawEncoder.java:67-85): drained from a zero block
+  std::vector<uint8_t> zeros;
+  HostCopies cb;
+  cb.fill = [&](size_t off, size_t cl, uint8_t *const *dst) { return fill(user, off, cl, dst); };
+  cb.drain = [&](size_t off, size_t cl, const uint8_t *const *src) {
+    if (rows == p) return drain(user, off, cl, src);
+    if (zeros.size() < cl) zeros.assign(cl, 0);
+    std::vector<const uint8_t *> all(static_cast<size_t>(p), zeros.data());
+    for (int r = 0; r < rows; ++r) all[r] = src[r];
+    return drain(user, off, cl, all.data());
+  };
+  if (int rc = staged_code(ctx, a, nullptr, nullptr, len, &cb)) return rc;
+  return OZEC_OK;
+}
+
+int ozec_decode_cb(ozec_coder *dec, const uint8_t *present_units, const int *erased, int n_erased, size_t len,
+                   ozec_fill_fn fill, ozec_drain_fn drain, void *user) {
+  ozec::StatScope stat_(OZEC_OP_DECODE, dec ? static_cast<uint64_t>(dec->k) * len : 0);
+  if (int rc = check_open(dec, "decode")) return rc;
+  if (!dec->decoder) return fail(OZEC_EINVAL, "not a decoder");
+  if (!present_units) return fail(OZEC_EINVAL, "Invalid inputs length");
+  if (!fill || !drain) return fail(OZEC_EINVAL, "null copy callback");
+  const int n_all = dec->k + dec->p;
+  bool present[256];
+  bool any = false;
+  for (int u = 0; u < n_all; ++u) any |= (present[u] = present_units[u] != 0);
+  if (!any) return fail(OZEC_EINVAL, "Invalid inputs are found, all being null");
+  std::vector<int> units;
+  std::vector<uint8_t> rows;
+  if (int rc = plan_decode(dec, present, erased, n_erased, units, rows)) return rc;
+  if (len == 0 || n_erased == 0) return OZEC_OK;
+  const int nin = static_cast<int>(units.size());
+  ozec::DeviceScope ds(dec->device);
+  if (!ds.ok()) return fail(OZEC_EDEVICE, "cannot select device " + std::to_string(dec->device));
+  DevCtx *ctx;
+  if (int rc = get_ctx(&ctx)) return rc;
+  CodeArgs a{};
+  if (dec->codec == OZEC_CODEC_XOR) fill_coef(a, 1, nin, rows.data());
+  else fill_coef(a, n_erased, nin, rows.data());
+  if (int rc = check_limits(a.k, a.rows)) return rc;
+  std::vector<uint8_t> zeros;
+  HostCopies cb;
+  // fill sees every unit's slot (k + p, null for the units not read), as ozec_decode's inputs
+  cb.fill = [&](size_t off, size_t cl, uint8_t *const *dst) {
+    std::vector<uint8_t *> by_unit(static_cast<size_t>(n_all), nullptr);
+    for (int j = 0; j < nin; ++j) by_unit[units[j]] = dst[j];
+    return fill(user, off, cl, by_unit.data());
+  };
+  // XOR decode: only erasedIndexes[0] is recovered, the other outputs are zero (XORRawDecoder.java:45-61)
+  cb.drain = [&](size_t off, size_t cl, const uint8_t *const *src) {
+    if (a.rows == n_erased) return drain(user, off, cl, src);
+    if (zeros.size() < cl) zeros.assign(cl, 0);
+    std::vector<const uint8_t *> all(static_cast<size_t>(n_erased), zeros.data());
+    for (int r = 0; r < a.rows; ++r) all[r] = src[r];
+    return drain(user, off, cl, all.data());
+  };
+  if (int rc = staged_code(ctx, a, nullptr, nullptr, len, &cb)) return rc;
   return OZEC_OK;
 }
 
@@ -2022,6 +2177,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "host_duplex") {
     if (value < 0) return bad();
     t.host_duplex.store(value);
+  } else if (k == "host_zero_copy") {
+    if (value < 0) return bad();
+    t.host_zero_copy.store(value);
   } else if (k == "host_pitch16") {
     if (value != 0 && value != 1) return bad();
     t.host_pitch16.store(static_cast<int>(value));
@@ -2053,6 +2211,7 @@ int ozec_get_tuning(const char *key, int64_t *value) {
   else if (k == "e2e_rect") *value = t.e2e_rect.load();
   else if (k == "host_graph") *value = t.host_graph.load();
   else if (k == "host_duplex") *value = t.host_duplex.load();
+  else if (k == "host_zero_copy") *value = t.host_zero_copy.load();
   else if (k == "host_pitch16") *value = t.host_pitch16.load();
   else if (k == "fused_min_units") *value = t.fused_min_units.load();
   else if (k == "rec_min_units") *value = t.rec_min_units.load();

@@ -27,6 +27,7 @@
 namespace ozec {
 
 TuneKnobs g_tune;
+thread_local int64_t t_grid_cap = 0;
 
 namespace {
 
@@ -1014,7 +1015,7 @@ hipError_t launch_krv(const CodeArgs &a, hipStream_t st, int64_t default_grid) {
   const int64_t units = a.nstripes * ((nvec + kBlock * VPT - 1) / (kBlock * VPT));
   const TabArgs<K * R> tabs = host_tabs<K * R>(a);
   const int64_t tg = g_tune.grid;
-  int64_t grid = tg > 0 ? tg : default_grid;
+  int64_t grid = tg > 0 ? tg : t_grid_cap > 0 ? std::min(t_grid_cap, default_grid) : default_grid;
   grid = std::max<int64_t>(1, std::min<int64_t>(grid, units));
   hipLaunchKernelGGL((gf_code_vec<K, R, kSreg, VPT, LAUX, SAUX, OPT, WIDE>), dim3(static_cast<unsigned>(grid)), dim3(kBlock),
                      0, st, a, tabs);
@@ -1040,14 +1041,20 @@ hipError_t launch_kr(const CodeArgs &a, hipStream_t st) {
   return launch_krv<K, R, 1, 2, 2>(a, st, kAll);
 }
 
+// grid_for with the thread's zero-copy cap (t_grid_cap) applied
+inline unsigned capped_grid(int64_t units) {
+  const unsigned g = grid_for(units, 1);
+  return t_grid_cap > 0 && static_cast<int64_t>(g) > t_grid_cap ? static_cast<unsigned>(t_grid_cap) : g;
+}
+
 template <int K>
 hipError_t launch_xor(const CodeArgs &a, hipStream_t st, bool buf) {
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
   const int64_t units = a.nstripes * ((nvec + kBlock - 1) / kBlock);
   if (buf) {
-    hipLaunchKernelGGL((xor_vec<K, true>), dim3(grid_for(units, 1)), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL((xor_vec<K, true>), dim3(capped_grid(units)), dim3(kBlock), 0, st, a);
   } else {
-    hipLaunchKernelGGL((xor_vec<K>), dim3(grid_for(units, 1)), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL((xor_vec<K>), dim3(capped_grid(units)), dim3(kBlock), 0, st, a);
   }
   return hipGetLastError();
 }
@@ -1081,7 +1088,7 @@ hipError_t launch_vec(const CodeArgs &a, hipStream_t st) {
 #undef OZEC_KR
   const uint32_t nvec = static_cast<uint32_t>(a.len >> 4);
   const int64_t units = a.nstripes * ((nvec + kBlock - 1) / kBlock);
-  const unsigned grid = grid_for(units, 1);
+  const unsigned grid = capped_grid(units);
   for (int row0 = 0; row0 < a.rows; row0 += 4) {
     const int rr = a.rows - row0 < 4 ? a.rows - row0 : 4;
     if (buf) {

@@ -181,6 +181,12 @@ struct TuneKnobs {
   std::atomic<int64_t> host_graph{256 << 10};  // host-buffer coding calls of one staged chunk up to this many bytes
                                                // per unit replay a cached hipGraph of H2D + kernel + D2H (0: off;
                                                // 64 KiB-cell rs-6-3 stripe from pageable cells 74 -> 64 us)
+  std::atomic<int64_t> host_zero_copy{48};  // host-buffer coding calls (ozec_encode / ozec_decode): the coding kernel
+                                           // reads the pinned caller buffers or libozec's pinned staging and writes
+                                           // the outputs over PCIe itself, in place of H2D + kernel + D2H, on a grid
+                                           // of this many blocks (0: off).  HIP's SDMA copies run at the link rate on
+                                           // some streams and at a third of it on others (profiles/r06/engines/); a
+                                           // 1 MiB-cell rs-6-3 stripe from pinned memory 190-400 -> 150 us
   std::atomic<int64_t> host_duplex{0};  // pinned host-buffer coding calls of at least this many bytes per unit go
                                         // up, through the kernel and back in column chunks, the D2H of chunk c on a
                                         // second stream beside the H2D of chunk c+1 (0: off, the default: 512 KiB
@@ -225,6 +231,16 @@ constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  24,  28,  29,
                                  231, 234};
 
 extern TuneKnobs g_tune;
+
+// Per-thread cap on the coding kernels' grid (0: none), set around a zero-copy launch (capi.cpp staged_pipeline): a
+// kernel streaming over PCIe does best with a few dozen blocks looping over the chunks, so the reads of one chunk
+// overlap the writes of the previous one, rather than every block reading at once and writing at once.
+extern thread_local int64_t t_grid_cap;
+struct GridCap {
+  int64_t prev;
+  explicit GridCap(int64_t cap) : prev(t_grid_cap) { t_grid_cap = cap; }
+  ~GridCap() { t_grid_cap = prev; }
+};
 
 hipError_t launch_code(const CodeArgs &a, hipStream_t stream);
 hipError_t launch_crc_windows(const CrcArgs &a, hipStream_t stream);

@@ -29,6 +29,16 @@ run() {
       step "percall probe"
       { timeout -k 10 120 scripts/percall_probe 1048576 200 && timeout -k 10 120 scripts/percall_probe 65536 500; } \
         > "$OUT/percall.json" 2> "$OUT/percall.err" ;;
+    d2h)
+      step "d2h probe"
+      timeout -k 10 120 scripts/d2h_probe > "$OUT/d2h.json" 2> "$OUT/d2h.err" ;;
+    engines)
+      step "stream engine probe"
+      { timeout -k 10 120 scripts/stream_engine_probe 8 && HSA_ENABLE_SDMA=0 timeout -k 10 120 scripts/stream_engine_probe 8; } \
+        > "$OUT/engines.json" 2> "$OUT/engines.err" ;;
+    jni)
+      step "bench jni rows"
+      timeout -k 10 300 python -u bench.py --workload jni > "$OUT/jni.json" 2> "$OUT/jni.err" ;;
     *)
       step "unknown step $what"
       return 2 ;;

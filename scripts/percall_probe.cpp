@@ -75,6 +75,25 @@ int main(int argc, char **argv) {
     std::printf(", \"enc_pageable_chunk%ldK_us\": %.1f", chunk >> 10, e);
   }
   CHECK(ozec_set_tuning("host_chunk", 4 << 20));
+  // the zero-copy grid and coding-kernel variant of the pinned call
+  for (long g : {16l, 24l, 32l, 64l, 96l, 128l}) {
+    CHECK(ozec_set_tuning("host_zero_copy", g));
+    const double t = time_us(iters, [&] { CHECK(ozec_encode(enc, in_pin, out_pin, cell)); });
+    std::printf(", \"enc_pinned_zc%ld_us\": %.1f", g, t);
+  }
+  CHECK(ozec_set_tuning("host_zero_copy", 48));
+  for (long v : {1l, 5l, 11l}) {
+    CHECK(ozec_set_tuning("gf_variant", v));
+    const double t = time_us(iters, [&] { CHECK(ozec_encode(enc, in_pin, out_pin, cell)); });
+    std::printf(", \"enc_pinned_gfvar%ld_us\": %.1f", v, t);
+  }
+  CHECK(ozec_set_tuning("gf_variant", 0));
+  // the same two calls with the copy path (host_zero_copy = 0: H2D + kernel + D2H on the slot's stream)
+  CHECK(ozec_set_tuning("host_zero_copy", 0));
+  const double epin_copy = time_us(iters, [&] { CHECK(ozec_encode(enc, in_pin, out_pin, cell)); });
+  const double epg_copy = time_us(iters, [&] { CHECK(ozec_encode(enc, in_pg, out_pg, cell)); });
+  CHECK(ozec_set_tuning("host_zero_copy", 48));
+  std::printf(", \"enc_pinned_copy_path_us\": %.1f, \"enc_pageable_copy_path_us\": %.1f", epin_copy, epg_copy);
   // the raw link on the arena
   uint8_t *d = nullptr;
   if (hipMalloc(&d, (k + p) * cell) != hipSuccess) return 1;
@@ -96,6 +115,62 @@ int main(int argc, char **argv) {
     (void)hipStreamSynchronize(s2);
   });
   const double empty = time_us(iters, [&] { (void)hipStreamSynchronize(s1); });
+  // where the arena's pages live, and D2H into its first 3 MiB instead of its parity region
+  int gnode = -9, n0 = -9, n6 = -9, n8 = -9;
+  (void)ozec_device_numa_node(0, &gnode);
+  (void)ozec_host_page_node(arena, &n0);
+  (void)ozec_host_page_node(arena + k * cell, &n6);
+  (void)ozec_host_page_node(arena + (k + p) * cell - 1, &n8);
+  const double d2h_front = time_us(iters, [&] {
+    (void)hipMemcpyAsync(arena, d + k * cell, p * cell, hipMemcpyDeviceToHost, s2);
+    (void)hipStreamSynchronize(s2);
+  });
+  const double d2h_again = time_us(iters, [&] {
+    (void)hipMemcpyAsync(arena + k * cell, d + k * cell, p * cell, hipMemcpyDeviceToHost, s2);
+    (void)hipStreamSynchronize(s2);
+  });
+  const double d2h_dev0 = time_us(iters, [&] {
+    (void)hipMemcpyAsync(arena + k * cell, d, p * cell, hipMemcpyDeviceToHost, s2);
+    (void)hipStreamSynchronize(s2);
+  });
+  const double d2h_s1 = time_us(iters, [&] {
+    (void)hipMemcpyAsync(arena + k * cell, d + k * cell, p * cell, hipMemcpyDeviceToHost, s1);
+    (void)hipStreamSynchronize(s1);
+  });
+  std::printf(", \"gpu_node\": %d, \"page_node_0\": %d, \"page_node_parity\": %d, \"page_node_end\": %d, "
+              "\"d2h_into_front_us\": %.1f, \"d2h_again_us\": %.1f, \"d2h_from_dev_offset0_us\": %.1f, "
+              "\"d2h_on_stream1_us\": %.1f", gnode, n0, n6, n8, d2h_front, d2h_again, d2h_dev0, d2h_s1);
+  // zero copy: the coding kernel reads the arena's data cells and writes its parity cells over PCIe itself (the
+  // arena is registered, so its pages are mapped for the GPU), one launch and no copy operation
+  void *dp = nullptr;
+  (void)hipHostGetDevicePointer(&dp, arena, 0);
+  std::vector<uint8_t> want(p * cell);
+  CHECK(ozec_encode(enc, in_pin, out_pin, cell));  // reference parity through the staged path
+  std::memcpy(want.data(), arena + k * cell, p * cell);
+  std::memset(arena + k * cell, 0xA5, p * cell);
+  uint8_t *dpp = static_cast<uint8_t *>(dp);
+  auto zc = [&](hipStream_t s) {
+    CHECK(ozec_encode_batch(enc, dpp, (k + p) * cell, cell, dpp + k * cell, (k + p) * cell, cell, 1, cell, s));
+    (void)hipStreamSynchronize(s);
+  };
+  zc(s1);
+  const bool zc_ok = std::memcmp(want.data(), arena + k * cell, p * cell) == 0;
+  const double zc1 = time_us(iters, [&] { zc(s1); });
+  const double zc2 = time_us(iters, [&] { zc(s2); });
+  std::printf(", \"dev_ptr_equals_host\": %d, \"zero_copy_ok\": %d, \"zero_copy_encode_us\": %.1f, "
+              "\"zero_copy_encode_stream2_us\": %.1f", dp == arena, zc_ok, zc1, zc2);
+  for (long g : {8l, 16l, 32l, 64l, 128l, 512l}) {  // grid of the coding kernel (blocks of 256 threads, 4 KiB chunks)
+    CHECK(ozec_set_tuning("grid", g));
+    const double t = time_us(iters, [&] { zc(s1); });
+    std::printf(", \"zero_copy_grid%ld_us\": %.1f", g, t);
+  }
+  CHECK(ozec_set_tuning("grid", 0));
+  for (long v : {1l, 5l}) {  // gf_variant 1: cached loads/stores; 5: two vectors per lane
+    CHECK(ozec_set_tuning("gf_variant", v));
+    const double t = time_us(iters, [&] { zc(s1); });
+    std::printf(", \"zero_copy_gfvar%ld_us\": %.1f", v, t);
+  }
+  CHECK(ozec_set_tuning("gf_variant", 0));
   std::printf(", \"h2d_us\": %.1f, \"d2h_us\": %.1f, \"h2d_d2h_concurrent_us\": %.1f, \"empty_sync_us\": %.2f}\n", h2d,
               d2h, dup, empty);
   (void)hipFree(d);

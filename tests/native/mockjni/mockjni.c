@@ -248,6 +248,40 @@ int __wrap_ozec_decode(ozec_coder *c, const uint8_t *const *in, const int *e, in
   at_device_call();
   return __real_ozec_decode(c, in, e, ne, out, len);
 }
+/* the callback forms (round 6): pins outstanding at entry, and -- through trampolines around the glue's fill / drain --
+ * pins still outstanding when a callback hands control back to libozec (which then launches or waits on the device) */
+static int g_pins_after_callback;
+int mock_pins_after_callback(void) { return g_pins_after_callback; }
+typedef struct {
+  ozec_fill_fn fill;
+  ozec_drain_fn drain;
+  void *user;
+} cb_tramp;
+static int tramp_fill(void *u, size_t off, size_t len, uint8_t *const *dst) {
+  cb_tramp *t = (cb_tramp *)u;
+  int rc = t->fill(t->user, off, len, dst);
+  if (__atomic_load_n(&g_pins, __ATOMIC_RELAXED) > 0) __atomic_add_fetch(&g_pins_after_callback, 1, __ATOMIC_RELAXED);
+  return rc;
+}
+static int tramp_drain(void *u, size_t off, size_t len, const uint8_t *const *src) {
+  cb_tramp *t = (cb_tramp *)u;
+  int rc = t->drain(t->user, off, len, src);
+  if (__atomic_load_n(&g_pins, __ATOMIC_RELAXED) > 0) __atomic_add_fetch(&g_pins_after_callback, 1, __ATOMIC_RELAXED);
+  return rc;
+}
+int __real_ozec_encode_cb(ozec_coder *, size_t, ozec_fill_fn, ozec_drain_fn, void *);
+int __wrap_ozec_encode_cb(ozec_coder *c, size_t len, ozec_fill_fn fill, ozec_drain_fn drain, void *user) {
+  at_device_call();
+  cb_tramp t = {fill, drain, user};
+  return __real_ozec_encode_cb(c, len, tramp_fill, tramp_drain, &t);
+}
+int __real_ozec_decode_cb(ozec_coder *, const uint8_t *, const int *, int, size_t, ozec_fill_fn, ozec_drain_fn, void *);
+int __wrap_ozec_decode_cb(ozec_coder *c, const uint8_t *present, const int *e, int ne, size_t len, ozec_fill_fn fill,
+                          ozec_drain_fn drain, void *user) {
+  at_device_call();
+  cb_tramp t = {fill, drain, user};
+  return __real_ozec_decode_cb(c, present, e, ne, len, tramp_fill, tramp_drain, &t);
+}
 int __real_ozec_crc_update(int, uint32_t *, const uint8_t *, size_t);
 int __wrap_ozec_crc_update(int t, uint32_t *s, const uint8_t *d, size_t len) {
   at_device_call();

@@ -31,6 +31,7 @@ def J():
                     os.path.join(ROOT, "tests", "native", "mockjni", "mockjni.c"), "-L", LIBDIR, "-lozec",
                     # device-work entry points wrapped by the mock (pins outstanding at each call)
                     "-Wl,--wrap=ozec_encode,--wrap=ozec_decode,--wrap=ozec_crc_update,--wrap=ozec_checksum_windows,"
+                    "--wrap=ozec_encode_cb,--wrap=ozec_decode_cb,"
                     "--wrap=ozec_host_alloc,--wrap=ozec_host_free",
                     f"-Wl,-rpath,{LIBDIR}", "-o", so], check=True, capture_output=True, timeout=120)
     L = ctypes.CDLL(so)
@@ -43,7 +44,7 @@ def J():
         ("mock_reset_device_calls", None, []), ("mock_region_copies", ctypes.c_int, []),
         ("mock_set_missing_class", None, [ctypes.c_char_p]), ("mock_host_allocs", ctypes.c_int, []),
         ("mock_host_live", ctypes.c_int, []), ("mock_refuse_pin_after", None, [ctypes.c_int]),
-        ("mock_calls_with_pending", ctypes.c_int, []),
+        ("mock_calls_with_pending", ctypes.c_int, []), ("mock_pins_after_callback", ctypes.c_int, []),
         ("mock_take_exception", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
         (P + "deviceCount", i32, [vp, vp]),
         (P + "setDevices", None, [vp, vp, vp]), (P + "getDevices", vp, [vp, vp]),
@@ -439,6 +440,7 @@ def test_heap_arrays_never_pinned_across_device_work(J, java, n):
         assert (~state) & 0xFFFFFFFF == oracle.crc_windows(oracle.CRC32C, d[2], n)[0]
         assert J.mock_device_calls() >= 5
         assert J.mock_pins_at_device_call() == 0, "an array was pinned while libozec did device work"
+        assert J.mock_pins_after_callback() == 0, "a fill / drain callback returned to libozec with an array pinned"
         assert J.mock_region_copies() > copies0
         assert J.mock_pins() == 0
     finally:
@@ -477,14 +479,17 @@ def test_refused_array_pin_leaves_its_exception_and_no_further_jni_call(J, java,
 
 @pytest.mark.gpu
 def test_heap_arenas_are_pooled_across_threads(J, java):
-    """The pinned arenas heap-array calls copy through come from a bounded pool, not one per Java thread: 24 threads
-    calling one after another reuse one arena (no new pinned allocation after the first), and the results stay exact."""
+    """The pinned arenas heap-array checksum calls copy through come from a bounded pool, not one per Java thread: 24
+    threads calling one after another reuse one arena (no new pinned allocation after the first); coder calls copy
+    into libozec's own staging (ozec_encode_cb) and allocate no arena at all; the results stay exact."""
     import threading
-    k, p, n = 6, 3, 50_000
+    k, p, n, bpc = 6, 3, 50_000, 4096
     h = call(J, "coderCreate", 0, 0, k, p)
     try:
         d = cells(SEED, 748000, k, n)
         ref = oracle.rs_encode(k, p, d)
+        nw = (n + bpc - 1) // bpc
+        crc_ref = oracle.crc_windows(oracle.CRC32C, d[0], bpc)
 
         def one():
             outs = [np.zeros(n, np.uint8) for _ in range(p)]
@@ -492,6 +497,9 @@ def test_heap_arenas_are_pooled_across_threads(J, java):
                  java.array([java.bytes(x) for x in outs]), java.ints([0] * p))
             assert java.exception() is None
             assert all((o == r).all() for o, r in zip(outs, ref))
+            c = np.zeros(4 * nw, np.uint8)
+            assert call(J, "checksumWindowsArray", 3, java.bytes(d[0]), 0, n, bpc, java.bytes(c)) == 4 * nw
+            assert (c.view(">u4") == crc_ref).all()
 
         one()  # the first call sizes an arena
         allocs0, live0 = J.mock_host_allocs(), J.mock_host_live()

@@ -20,6 +20,7 @@
  */
 #include <jni.h>
 #include <pthread.h>
+#include <stdatomic.h>
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
@@ -292,12 +293,6 @@ static int copy_regions(JNIEnv *env, const array_set *as, const ozm_buf *bufs, i
   return 0;
 }
 
-
-
-
-
-
-
 /* encode (erased == NULL) or decode of heap arrays already validated by ozm_*_check (round 6): libozec's staged
  * pipeline with the glue moving the bytes (ozec_encode_cb / ozec_decode_cb).  libozec cuts each HEAP_CHUNK piece of the
  * call into column chunks and asks for chunk c's inputs (heap_fill: the arrays held critical for that copy only,
@@ -335,8 +330,8 @@ static int heap_drain(void *user, size_t off, size_t len, const uint8_t *const *
   return copy_regions(j->env, j->ao, j->ob, j->base + (int64_t)off, (int64_t)len, stage, 0) ? -1 : 0;
 }
 
-static int heap_code(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_buf *ib, const array_set *ao,
-                     const ozm_buf *ob, const int *erased, int ne, int64_t len, ozm_status *st) {
+static int heap_code_cb(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_buf *ib, const array_set *ao,
+                        const ozm_buf *ob, const int *erased, int ne, int64_t len, ozm_status *st) {
   heap_job j = {env, ai, ao, ib, ob, 0};
   uint8_t present[MAX_BUFS];
   for (int i = 0; i < ai->n; ++i) present[i] = ai->arr[i] != NULL;
@@ -351,6 +346,91 @@ static int heap_code(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_
     }
   }
   return 0;
+}
+
+/* The arena form: the inputs copied into a leased pinned arena, libozec's in-place DMA + kernel on it, the outputs
+ * copied back -- the copies outside libozec's slot, so concurrent callers' copies and device work interleave freely */
+static int heap_code_arena(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_buf *ib, const array_set *ao,
+                           const ozm_buf *ob, const int *erased, int ne, int64_t len, ozm_status *st) {
+  ozm_buf si[MAX_BUFS], so[MAX_BUFS];
+  int nin = 0;
+  for (int i = 0; i < ai->n; ++i) nin += ai->arr[i] != NULL;
+  arena_lease l;
+  arena_lease_begin(&l);
+  int rc = 0;
+  for (int64_t off = 0; off < len && !rc; off += HEAP_CHUNK) {
+    const int64_t cl = len - off < HEAP_CHUNK ? len - off : HEAP_CHUNK;
+    const int64_t stride = round_up(cl, ARENA_ALIGN);
+    uint8_t *a = arena(&l, (size_t)((int64_t)(nin + ao->n) * stride), st);
+    if (!a) {
+      rc = st->code;
+      break;
+    }
+    int slot = 0;
+    for (int i = 0; i < ai->n; ++i) {  /* present inputs in consecutive arena slots, outputs after them */
+      memset(&si[i], 0, sizeof(si[i]));
+      if (!ai->arr[i]) continue;
+      si[i].present = 1;
+      si[i].base = a + (int64_t)slot++ * stride;
+      si[i].capacity = cl;
+    }
+    for (int r = 0; r < ao->n; ++r) {
+      memset(&so[r], 0, sizeof(so[r]));
+      so[r].present = ao->arr[r] != NULL;
+      so[r].base = a + (int64_t)(nin + r) * stride;
+      so[r].capacity = cl;
+    }
+    if (copy_regions(env, ai, ib, off, cl, si, 1)) {
+      rc = ozm_fail(OZEC_ENOMEM, "a Java array could not be read", st);  /* its exception is pending */
+      break;
+    }
+    rc = erased ? ozm_decode(h, si, ai->n, erased, ne, so, ao->n, cl, st)
+                : ozm_encode(h, si, ai->n, so, ao->n, cl, st);
+    if (!rc && copy_regions(env, ao, ob, off, cl, so, 0))
+      rc = ozm_fail(OZEC_ENOMEM, "a Java array could not be written", st);
+  }
+  arena_lease_end(&l);
+  return rc;
+}
+
+/* Which form a call takes (env OZEC_JNI_HEAP: "cb", "arena", default "auto"): a call alone in the process takes the
+ * callback form (its copies overlap its own device work: rs-6-3 1 MiB cells, one thread, 260 -> ~224 us per stripe);
+ * a call made while another coder call is in flight takes the arena form, whose copies run outside libozec's slots
+ * (4 / 16 threads: the callback form held slots through its copies and lost ~20% aggregate, profiles/r06/zero_copy/) */
+enum { HEAP_AUTO, HEAP_CB, HEAP_ARENA };
+static _Atomic int g_heap_inflight, g_heap_mode = -1;
+static _Atomic unsigned long g_heap_forms[2]; /* calls taken by the callback form, by the arena form */
+
+static int heap_mode(void) {
+  int m = atomic_load(&g_heap_mode);
+  if (m < 0) {
+    const char *e = getenv("OZEC_JNI_HEAP");
+    m = e && !strcmp(e, "cb") ? HEAP_CB : e && !strcmp(e, "arena") ? HEAP_ARENA : HEAP_AUTO;
+    atomic_store(&g_heap_mode, m);
+  }
+  return m;
+}
+
+/* not a native method: the tests' switch between the forms (mode 0 auto, 1 callback, 2 arena; -1 leaves it) and the
+ * count of calls each form took; returns the previous mode */
+JNIEXPORT int ozec_jni_heap_mode(int mode, unsigned long *cb_calls, unsigned long *arena_calls) {
+  const int prev = heap_mode();
+  if (mode >= HEAP_AUTO && mode <= HEAP_ARENA) atomic_store(&g_heap_mode, mode);
+  if (cb_calls) *cb_calls = atomic_load(&g_heap_forms[0]);
+  if (arena_calls) *arena_calls = atomic_load(&g_heap_forms[1]);
+  return prev;
+}
+
+static int heap_code(JNIEnv *env, ozec_coder *h, const array_set *ai, const ozm_buf *ib, const array_set *ao,
+                     const ozm_buf *ob, const int *erased, int ne, int64_t len, ozm_status *st) {
+  const int mode = heap_mode();
+  const int others = atomic_fetch_add(&g_heap_inflight, 1);
+  const int cb = mode == HEAP_CB || (mode == HEAP_AUTO && others == 0);
+  atomic_fetch_add(&g_heap_forms[cb ? 0 : 1], 1);
+  const int rc = cb ? heap_code_cb(env, h, ai, ib, ao, ob, erased, ne, len, st)
+                    : heap_code_arena(env, h, ai, ib, ao, ob, erased, ne, len, st);
+  atomic_fetch_sub(&g_heap_inflight, 1);
+  return rc;
 }
 
 static int int_array(JNIEnv *env, jintArray a, int *out, int max, int *n, ozm_status *st) {

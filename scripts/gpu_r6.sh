@@ -39,6 +39,23 @@ run() {
     jni)
       step "bench jni rows"
       timeout -k 10 300 python -u bench.py --workload jni > "$OUT/jni.json" 2> "$OUT/jni.err" ;;
+    jnisweep)
+      # the JNI heap-array forms (OZEC_JNI_HEAP auto / cb / arena) x libozec's zero-copy grid (0: copy path)
+      step "jni sweep"
+      gcc -O2 -I tests/native/mockjni -I include jni/ozec_jni.c jni/ozec_marshal.c tests/native/mockjni/mockjni.c \
+        tests/native/jni_percall.c -L ozone_amd/lib -lozec -lpthread \
+        -Wl,--wrap=ozec_encode,--wrap=ozec_decode,--wrap=ozec_crc_update,--wrap=ozec_checksum_windows \
+        -Wl,--wrap=ozec_encode_cb,--wrap=ozec_decode_cb,--wrap=ozec_host_alloc,--wrap=ozec_host_free \
+        -Wl,-rpath,"$PWD/ozone_amd/lib" -o "$OUT/jni_percall" || return 1
+      local specs="" m c t
+      for m in encode decode; do for c in 65536 1048576; do for t in 1 4 16; do specs="$specs $m:6:3:$c:$t"; done; done; done
+      for heap in ${JNI_HEAPS:-auto cb arena}; do
+        for zc in ${JNI_ZC:-48 0}; do
+          echo "# heap=$heap zc=$zc" >> "$OUT/jnisweep.json"
+          OZEC_JNI_HEAP=$heap OZEC_TUNE=host_zero_copy=$zc timeout -k 10 120 "$OUT/jni_percall" 0.5 $specs \
+            >> "$OUT/jnisweep.json" 2>> "$OUT/jnisweep.err" || return 1
+        done
+      done ;;
     *)
       step "unknown step $what"
       return 2 ;;

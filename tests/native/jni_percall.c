@@ -26,6 +26,7 @@ jlong P(coderCreate)(JNIEnv *, jclass, jboolean, jint, jint, jint);
 void P(coderRelease)(JNIEnv *, jclass, jlong);
 void P(encodeArrays)(JNIEnv *, jclass, jlong, jobjectArray, jintArray, jint, jobjectArray, jintArray);
 void P(decodeArrays)(JNIEnv *, jclass, jlong, jobjectArray, jintArray, jint, jintArray, jobjectArray, jintArray);
+int ozec_jni_heap_mode(int mode, unsigned long *cb_calls, unsigned long *arena_calls);
 
 JNIEnv *mock_env(void);
 struct mock_object *mock_bytes(void *p, int64_t len);
@@ -155,12 +156,15 @@ static int run_spec(const char *spec) {
   DECODE = mode_decode;
   for (int t = 0; t < T; ++t) call(&ws[t]); /* warm: arenas grown, graphs cached */
   fail_if_exception("warm-up");
+  unsigned long cb0, ar0, cb1, ar1;
+  (void)ozec_jni_heap_mode(-1, &cb0, &ar0);
   pthread_barrier_init(&g_bar, NULL, (unsigned)T);
   pthread_t *th = calloc((size_t)T, sizeof *th);
   for (int t = 0; t < T; ++t) pthread_create(&th[t], NULL, run, &ws[t]);
   for (int t = 0; t < T; ++t) pthread_join(th[t], NULL);
   pthread_barrier_destroy(&g_bar);
   fail_if_exception("timed calls");
+  (void)ozec_jni_heap_mode(-1, &cb1, &ar1);
   long calls = 0;
   double t0 = ws[0].start, t1 = ws[0].stop;
   for (int t = 0; t < T; ++t) {
@@ -171,9 +175,10 @@ static int run_spec(const char *spec) {
   const double el = t1 - t0;
   const double data = (double)calls * K * (double)CELL; /* data bytes, as RawErasureCoderBenchmark counts them */
   printf("{\"mode\": \"%s\", \"k\": %d, \"p\": %d, \"erased\": %d, \"cell_bytes\": %d, \"threads\": %d, \"calls\": %ld, "
-         "\"seconds\": %.4f, \"us_per_stripe\": %.2f, \"GBps\": %.3f, \"round_trip_ok\": %s}\n",
+         "\"seconds\": %.4f, \"us_per_stripe\": %.2f, \"GBps\": %.3f, \"round_trip_ok\": %s, "
+         "\"callback_form_calls\": %lu, \"arena_form_calls\": %lu}\n",
          DECODE ? "decode" : "encode", K, R, DECODE ? g_ne : 0, CELL, T, calls, el, el / ((double)calls / T) * 1e6,
-         data / el / 1e9, ok ? "true" : "false");
+         data / el / 1e9, ok ? "true" : "false", cb1 - cb0, ar1 - ar0);
   fflush(stdout);
   P(coderRelease)(env, NULL, g_enc);
   P(coderRelease)(env, NULL, g_dec);

@@ -46,6 +46,8 @@ def J():
         ("mock_host_live", ctypes.c_int, []), ("mock_refuse_pin_after", None, [ctypes.c_int]),
         ("mock_calls_with_pending", ctypes.c_int, []), ("mock_pins_after_callback", ctypes.c_int, []),
         ("mock_take_exception", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+        ("ozec_jni_heap_mode", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_ulong),
+                                              ctypes.POINTER(ctypes.c_ulong)]),
         (P + "deviceCount", i32, [vp, vp]),
         (P + "setDevices", None, [vp, vp, vp]), (P + "getDevices", vp, [vp, vp]),
         (P + "setDevicePolicy", None, [vp, vp, i32]), (P + "coderDevice", i32, [vp, vp, i64]),
@@ -392,9 +394,31 @@ def test_device_list_natives(J, java):
     assert java.exception()[0] == "java/io/IOException"
 
 
+HEAP_AUTO, HEAP_CB, HEAP_ARENA = 0, 1, 2
+
+
+def heap_forms(J):
+    cb, ar = ctypes.c_ulong(), ctypes.c_ulong()
+    J.ozec_jni_heap_mode(-1, ctypes.byref(cb), ctypes.byref(ar))
+    return cb.value, ar.value
+
+
+@pytest.fixture(params=[HEAP_CB, HEAP_ARENA], ids=["callback", "arena"])
+def heap_form(J, request):
+    """the two forms a heap-array coder call can take (jni/ozec_jni.c heap_code): libozec's staged pipeline with the
+    glue's fill / drain callbacks, or a pinned arena around an in-place call"""
+    prev = J.ozec_jni_heap_mode(request.param, None, None)
+    before = heap_forms(J)
+    yield request.param
+    after = heap_forms(J)
+    J.ozec_jni_heap_mode(prev, None, None)
+    took = after[0] - before[0] if request.param == HEAP_CB else after[1] - before[1]
+    assert took > 0 and sum(after) - sum(before) == took, "a call took the other form"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [1 << 16, (4 << 20) + 4096 + 3])  # one chunk; two chunks of the 4 MiB arena
-def test_heap_arrays_never_pinned_across_device_work(J, java, n):
+def test_heap_arrays_never_pinned_across_device_work(J, java, heap_form, n):
     """byte[] inputs and outputs are copied into a pooled pinned arena (coder calls: the arrays held
     critical for the parallel copy only, ozec_host_copy; checksum calls: Get/SetByteArrayRegion), and no array is
     pinned while libozec works -- the mock records the array pins outstanding at every wrapped ozec_encode /
@@ -450,7 +474,7 @@ def test_heap_arrays_never_pinned_across_device_work(J, java, n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("refuse_after", [0, 2, 3])  # the first input pin, the last one, the first output pin
-def test_refused_array_pin_leaves_its_exception_and_no_further_jni_call(J, java, refuse_after):
+def test_refused_array_pin_leaves_its_exception_and_no_further_jni_call(J, java, heap_form, refuse_after):
     """a JVM that cannot pin an array (GetPrimitiveArrayCritical -> NULL, OutOfMemoryError pending) ends the
     copy: the arrays already pinned are released without write-back, the exception stays the pending one (no JNI call
     but ExceptionCheck / Release / DeleteLocalRef runs while it is pending), outputs stay untouched, and the next call
@@ -511,6 +535,64 @@ def test_heap_arenas_are_pooled_across_threads(J, java):
         assert J.mock_host_live() == live0
     finally:
         call(J, "coderRelease", h)
+
+
+@pytest.mark.gpu
+def test_concurrent_heap_calls_take_either_form_exactly(J, java):
+    """Default (auto) form choice: a call alone takes the callback form, a call made while another coder call is in
+    flight takes the arena form.  Eight threads encoding and decoding at once: every call exact, every call counted
+    under one of the two forms, and a call alone afterwards takes the callback form."""
+    import threading
+    k, p, n = 6, 3, 300_000
+    prev = J.ozec_jni_heap_mode(HEAP_AUTO, None, None)
+    h = call(J, "coderCreate", 0, 0, k, p)
+    hd = call(J, "coderCreate", 1, 0, k, p)
+    errors = []
+    try:
+        d = cells(SEED, 749000, k, n)
+        ref = oracle.rs_encode(k, p, d)
+        units = d + ref
+        # erasure patterns, some listing a parity unit before a data unit: those decode with the reference's ordering
+        # quirk (oracle/ozec_oracle.c oracle_rs_decode_matrix), so the expected outputs are the oracle's
+        patterns = [[t % (k + p), (t + 4) % (k + p)] for t in range(8)]
+        want = [oracle.rs_decode(k, p, [None if u in e else units[u] for u in range(k + p)], e) for e in patterns]
+        before = heap_forms(J)
+
+        def worker(t):
+            try:
+                for i in range(6):
+                    outs = [np.zeros(n, np.uint8) for _ in range(p)]
+                    call(J, "encodeArrays", h, java.array([java.bytes(x) for x in d]), java.ints([0] * k), n,
+                         java.array([java.bytes(x) for x in outs]), java.ints([0] * p))
+                    assert all((o == r).all() for o, r in zip(outs, ref)), f"encode {t}/{i}"
+                    erased = patterns[t]
+                    rec = [np.zeros(n, np.uint8) for _ in erased]
+                    call(J, "decodeArrays", hd, java.array([None if u in erased else java.bytes(units[u])
+                                                            for u in range(k + p)]),
+                         java.ints([0] * (k + p)), n, java.ints(erased), java.array([java.bytes(r) for r in rec]),
+                         java.ints([0, 0]))
+                    assert all((r == w).all() for r, w in zip(rec, want[t])), f"decode {t}/{i}"
+            except Exception as e:  # noqa: BLE001 - reported below
+                errors.append(e)
+
+        ts = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors
+        mid = heap_forms(J)
+        assert sum(mid) - sum(before) == 8 * 6 * 2
+        outs = [np.zeros(n, np.uint8) for _ in range(p)]
+        call(J, "encodeArrays", h, java.array([java.bytes(x) for x in d]), java.ints([0] * k), n,
+             java.array([java.bytes(x) for x in outs]), java.ints([0] * p))
+        assert all((o == r).all() for o, r in zip(outs, ref))
+        after = heap_forms(J)
+        assert after[0] == mid[0] + 1 and after[1] == mid[1], "a call alone did not take the callback form"
+    finally:
+        J.ozec_jni_heap_mode(prev, None, None)
+        call(J, "coderRelease", h)
+        call(J, "coderRelease", hd)
 
 
 @pytest.mark.gpu

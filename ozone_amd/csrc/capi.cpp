@@ -479,10 +479,12 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
   // zero copy for a call alone on the GPU's slots: concurrent callers keep the SDMA copies, which together fill the link
   // (four JNI threads: 52 GB/s through copies, 43 with every call zero-copy, profiles/r06/zero_copy/)
   const int64_t zc_grid = zc && ctx->leased.load() <= 1 ? ozec::g_tune.host_zero_copy.load(std::memory_order_relaxed) : 0;
-  // zero copy, one call in one chunk of at least 2 x 256 KiB per unit: two chunks, so the staging copies of one half
-  // overlap the kernel on the other (1 MiB-cell rs-6-3 stripe from pageable cells 289 -> 239 us; four chunks 360,
-  // profiles/r06/percall/)
-  if (zc_grid > 0 && chunk >= len && len >= 2 * (size_t{256} << 10)) chunk = std::max(gran, round_up((len + 1) / 2, gran));
+  // zero copy, one call in one chunk: host_zc_chunks column chunks (2) of at least 256 KiB per unit, so the staging
+  // copies of one overlap the kernel on another (1 MiB-cell rs-6-3 stripe from pageable cells 289 -> 239 us; four
+  // chunks 360, profiles/r06/percall/)
+  const int64_t zch = ozec::g_tune.host_zc_chunks.load(std::memory_order_relaxed);
+  if (zc_grid > 0 && zch > 1 && chunk >= len && len >= static_cast<size_t>(zch) * (size_t{256} << 10))
+    chunk = std::max(gran, round_up((len + zch - 1) / zch, gran));
   if (chunk >= len) chunk = len;
   const size_t nch = (len + chunk - 1) / chunk;
   const size_t cp = round_up(chunk, kStageAlign), op = round_up(out_bytes(chunk), kStageAlign);
@@ -2180,6 +2182,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "host_zero_copy") {
     if (value < 0) return bad();
     t.host_zero_copy.store(value);
+  } else if (k == "host_zc_chunks") {
+    if (value < 1 || value > 16) return bad();
+    t.host_zc_chunks.store(value);
   } else if (k == "host_pitch16") {
     if (value != 0 && value != 1) return bad();
     t.host_pitch16.store(static_cast<int>(value));
@@ -2212,6 +2217,7 @@ int ozec_get_tuning(const char *key, int64_t *value) {
   else if (k == "host_graph") *value = t.host_graph.load();
   else if (k == "host_duplex") *value = t.host_duplex.load();
   else if (k == "host_zero_copy") *value = t.host_zero_copy.load();
+  else if (k == "host_zc_chunks") *value = t.host_zc_chunks.load();
   else if (k == "host_pitch16") *value = t.host_pitch16.load();
   else if (k == "fused_min_units") *value = t.fused_min_units.load();
   else if (k == "rec_min_units") *value = t.rec_min_units.load();

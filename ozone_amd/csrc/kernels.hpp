@@ -187,6 +187,9 @@ struct TuneKnobs {
                                            // of this many blocks (0: off).  HIP's SDMA copies run at the link rate on
                                            // some streams and at a third of it on others (profiles/r06/engines/); a
                                            // 1 MiB-cell rs-6-3 stripe from pinned memory 190-400 -> 150 us
+  std::atomic<int64_t> host_zc_chunks{2};  // a lone zero-copy call from pageable (or callback-fed) units runs in
+                                           // this many column chunks of at least 256 KiB per unit, the staging
+                                           // copies of one overlapping the kernel on another (1: no overlap)
   std::atomic<int64_t> host_duplex{0};  // pinned host-buffer coding calls of at least this many bytes per unit go
                                         // up, through the kernel and back in column chunks, the D2H of chunk c on a
                                         // second stream beside the H2D of chunk c+1 (0: off, the default: 512 KiB

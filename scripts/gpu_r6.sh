@@ -29,6 +29,9 @@ run() {
       step "percall probe"
       { timeout -k 10 120 scripts/percall_probe 1048576 200 && timeout -k 10 120 scripts/percall_probe 65536 500; } \
         > "$OUT/percall.json" 2> "$OUT/percall.err" ;;
+    pipeline)
+      step "pipeline probe"
+      timeout -k 10 200 scripts/pipeline_probe 1048576 200 > "$OUT/pipeline.json" 2> "$OUT/pipeline.err" ;;
     d2h)
       step "d2h probe"
       timeout -k 10 120 scripts/d2h_probe > "$OUT/d2h.json" 2> "$OUT/d2h.err" ;;
@@ -40,7 +43,7 @@ run() {
       step "bench jni rows"
       timeout -k 10 300 python -u bench.py --workload jni > "$OUT/jni.json" 2> "$OUT/jni.err" ;;
     jnisweep)
-      # the JNI heap-array forms (OZEC_JNI_HEAP auto / cb / arena) x libozec's zero-copy grid (0: copy path)
+      # the JNI heap-array forms (OZEC_JNI_HEAP auto / cb / arena) x libozec tunings (JNI_TUNES, one OZEC_TUNE each)
       step "jni sweep"
       gcc -O2 -I tests/native/mockjni -I include jni/ozec_jni.c jni/ozec_marshal.c tests/native/mockjni/mockjni.c \
         tests/native/jni_percall.c -L ozone_amd/lib -lozec -lpthread \
@@ -50,9 +53,9 @@ run() {
       local specs="" m c t
       for m in encode decode; do for c in 65536 1048576; do for t in 1 4 16; do specs="$specs $m:6:3:$c:$t"; done; done; done
       for heap in ${JNI_HEAPS:-auto cb arena}; do
-        for zc in ${JNI_ZC:-48 0}; do
-          echo "# heap=$heap zc=$zc" >> "$OUT/jnisweep.json"
-          OZEC_JNI_HEAP=$heap OZEC_TUNE=host_zero_copy=$zc timeout -k 10 120 "$OUT/jni_percall" 0.5 $specs \
+        for tune in ${JNI_TUNES:-host_zero_copy=48 host_zero_copy=0}; do
+          echo "# heap=$heap tune=$tune" >> "$OUT/jnisweep.json"
+          OZEC_JNI_HEAP=$heap OZEC_TUNE=$tune timeout -k 10 120 "$OUT/jni_percall" 0.5 ${JNI_SPECS:-$specs} \
             >> "$OUT/jnisweep.json" 2>> "$OUT/jnisweep.err" || return 1
         done
       done ;;

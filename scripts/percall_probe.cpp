@@ -75,6 +75,15 @@ int main(int argc, char **argv) {
     std::printf(", \"enc_pageable_chunk%ldK_us\": %.1f", chunk >> 10, e);
   }
   CHECK(ozec_set_tuning("host_chunk", 4 << 20));
+  // a lone zero-copy call from pageable cells in 1..4 column chunks (copies of one overlapping the kernel on another),
+  // twice over to see the spread
+  for (int rep = 0; rep < 2; ++rep)
+    for (long z : {1l, 2l, 3l, 4l}) {
+      CHECK(ozec_set_tuning("host_zc_chunks", z));
+      const double t = time_us(iters, [&] { CHECK(ozec_encode(enc, in_pg, out_pg, cell)); });
+      std::printf(", \"enc_pageable_zc_chunks%ld_rep%d_us\": %.1f", z, rep, t);
+    }
+  CHECK(ozec_set_tuning("host_zc_chunks", 2));
   // the zero-copy grid and coding-kernel variant of the pinned call
   for (long g : {16l, 24l, 32l, 64l, 96l, 128l}) {
     CHECK(ozec_set_tuning("host_zero_copy", g));

@@ -32,6 +32,9 @@ run() {
     pipeline)
       step "pipeline probe"
       timeout -k 10 200 scripts/pipeline_probe 1048576 200 > "$OUT/pipeline.json" 2> "$OUT/pipeline.err" ;;
+    fusedab)
+      step "fused vs unfused A/B (WIDE, XOR TAIL)"
+      timeout -k 10 400 python -u scripts/fused_ab_r6.py > "$OUT/fused_ab.json" 2> "$OUT/fused_ab.err" ;;
     d2h)
       step "d2h probe"
       timeout -k 10 120 scripts/d2h_probe > "$OUT/d2h.json" 2> "$OUT/d2h.err" ;;

@@ -471,7 +471,7 @@ class Workload:
 # ------------------------------------------------------------------------------------------ C5 end to end
 
 
-_KEEP_MAPPED = []  # host ranges this process registered: mapped until exit (include/ozec.h, ozec_host_unregister)
+_KEEP_MAPPED = []  # host mappings held by ctypes views until the process exits
 
 
 class HostBatch:
@@ -563,9 +563,8 @@ class HostBatch:
         return [page_node(self.base + self.data_off), page_node(self.base + self.data_off + self.data_len - 1)]
 
     def close(self, dist):
-        """Unregister; the mapping itself stays until the process exits (include/ozec.h: a range registered with
-        ozec_host_register stays mapped, DESIGN §4 "GPU faults"); the shared-memory object was unlinked at creation,
-        so its pages go with the last rank."""
+        """Unregister; the mapping itself stays until the process exits (a ctypes view anchors it, and the bench ends
+        right after); the shared-memory object was unlinked at creation, so its pages go with the last rank."""
         from ozone_amd.stripe_queue import host_unregister
         for a in self.registered:
             host_unregister(a)

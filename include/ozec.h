@@ -302,11 +302,12 @@ int ozec_host_copy(void *const *dst, const void *const *src, const size_t *bytes
  * its pages on `device`'s NUMA node first (device < 0: no placement; only pages wholly inside the range move).
  * Placement is best effort: where the kernel refuses it the memory is pinned where it lies, and
  * ozec_host_placement_failures() counts such calls.  ozec_host_unregister undoes the pinning.
- * Keep a range registered here MAPPED until the process exits, even after ozec_host_unregister: caller memory that
- * was registered, unregistered and handed back to the allocator was followed, in the same process, by
- * hipErrorIllegalAddress in HIP's next large pageable copy (one HIP does itself by locking the caller's pages; no
- * libozec code runs in it) -- DESIGN.md 4, "GPU faults".  Memory that comes and goes should come from ozec_host_alloc /
- * ozec_host_free: libozec never returns a range it registered to the kernel (its address range stays reserved). */
+ * After ozec_host_unregister the caller may free or reuse the memory.  (Rounds 4-5 asked callers to keep such ranges
+ * mapped until exit, after hipErrorIllegalAddress aborts in HIP's own pageable copies of a test process; round 6 found
+ * no stale lock or registration left behind by either call -- ROCr's pointer info reports the range unknown right
+ * after the unregister and after every pageable copy -- and the GPU suites run green with their ranges unregistered
+ * and freed: DESIGN.md 4, "GPU faults".)  Memory that comes and goes often is cheaper from ozec_host_alloc /
+ * ozec_host_free, which keep the registration cost off the hot path. */
 int ozec_host_register(void *p, size_t bytes, int device);
 uint64_t ozec_host_placement_failures(void);
 int ozec_host_unregister(void *p);

@@ -42,6 +42,12 @@ run() {
       step "stream engine probe"
       { timeout -k 10 120 scripts/stream_engine_probe 8 && HSA_ENABLE_SDMA=0 timeout -k 10 120 scripts/stream_engine_probe 8; } \
         > "$OUT/engines.json" 2> "$OUT/engines.err" ;;
+    prof)  # rocprofv3 kernel statistics of the headline and of every leg with the bench's own warm-up and steps
+      step "rocprof c2 + legs"
+      (cd /tmp && export TMPDIR=/tmp) && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c2" -o run \
+        --output-format csv -- python3 bench.py --workload c2 --no-cpu --no-pmc --no-e2e --no-legs --no-jni \
+        > "$OUT/prof_c2.log" 2>&1 && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_legs" -o run \
+        --output-format csv -- python3 bench.py --workload legs --no-cpu --no-pmc > "$OUT/prof_legs.log" 2>&1 ;;
     jni)
       step "bench jni rows"
       timeout -k 10 300 python -u bench.py --workload jni > "$OUT/jni.json" 2> "$OUT/jni.err" ;;

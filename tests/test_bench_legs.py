@@ -2,6 +2,7 @@
 default line gets its rocprof average and PMC traffic).  The child runs the legs in order; each leg's set-up starts
 with the synthetic-data fill kernel, and its steps may launch other kernels between the measured ones (the
 reconstruction's mismatch finisher, the runtime's memset of a new WorkQueue slot).  Synthetic trace rows, CPU only."""
+import json
 import os
 import sys
 
@@ -82,3 +83,26 @@ def test_pmc_rows_order_by_dispatch_id():
     assert [int(r["Dispatch_Id"]) for r in second] == [15, 17, 19]
     with pytest.raises(IndexError):
         bench._leg_rows(rows, "Kernel_Name", "Dispatch_Id", "a<", 0, W + K + 1)
+
+
+def test_compact_line_keeps_every_leg_under_the_drivers_tail():
+    """the default run prints one line under the driver's 9 KB stdout tail that still carries the
+    contract keys, the headline roofline, every leg (kernel time, fraction, rocprof average, traffic), both C5 legs, the
+    JNI per-call rows and the CPU baseline -- checked on a full record of this round's default run."""
+    full_path = os.path.join(ROOT, "profiles", "r06", "final_a", "bench_full.json")
+    full = json.load(open(full_path))
+    line = json.dumps(bench.compact_line(full, "gpurun_out/bench_full.json"))
+    assert len(line) < 9000
+    out = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in out, k
+    assert out["value"] == full["value"] and out["roofline"]["frac"] == full["roofline"]["frac"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in out["roofline"], k
+    assert [lg["leg"] for lg in out["legs"]] == [lg["leg"] for lg in full["legs"]]
+    for lg in out["legs"]:
+        assert {"kernel_ms", "frac", "rocprof_avg_ms", "traffic_over_algorithmic"} <= set(lg), lg
+    assert out["e2e"]["value"] == full["e2e"]["value"] and "e2e_in_process" in out
+    assert len(out["jni_percall_us"]) == len(full["jni_percall"]["rows"])
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(out["cpu_baseline"])

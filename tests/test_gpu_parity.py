@@ -1092,8 +1092,9 @@ def test_encode_crc_block_groups_vs_oracle(codec, k, p, n, B, G, bpc):
 def test_host_calls_zero_copy_and_copy_paths(zc, codec, k, p, n):
     """Round 6, host_zero_copy (capi.cpp staged_pipeline): the coding kernel reads pinned caller cells (one pinned pool,
     cells at one stride: the JNI arena's layout) and libozec's pinned staging (pageable cells) in place over PCIe and
-    writes the outputs there, instead of H2D + kernel + D2H; 0 restores the copy path, 5 a small grid.  Encode and a
-    decode of two units, pinned and pageable, vs the oracle, every output byte overwritten."""
+    writes the outputs there, instead of H2D + kernel + D2H; 0 restores the copy path, 5 a small grid.  Encode (pageable
+    cells in 1, 2 and 3 column chunks) and a decode of two units, pinned and pageable, vs the oracle, every output byte
+    overwritten."""
     from ozone_amd.stripe_queue import host_alloc
     lib = L.lib()
     assert lib.ozec_set_tuning(b"host_zero_copy", zc) == 0
@@ -1109,9 +1110,12 @@ def test_host_calls_zero_copy_and_copy_paths(zc, codec, k, p, n):
             v[:] = 0xA5
         enc(codec, k, p).encode(views[:k], views[k:k + p])
         assert all((views[k + r] == ref[r]).all() for r in range(rows)), (codec, k, p, n, zc)
-        par = [np.full(n, 0xA5, np.uint8) for _ in range(p)]  # pageable
-        enc(codec, k, p).encode([d.copy() for d in data], par)
-        assert all((par[r] == ref[r]).all() for r in range(rows)), (codec, k, p, n, zc)
+        for zch in (2, 1, 3):  # pageable, staged in host_zc_chunks column chunks (zero copy needs >= 256 KiB each)
+            assert lib.ozec_set_tuning(b"host_zc_chunks", zch) == 0
+            par = [np.full(n, 0xA5, np.uint8) for _ in range(p)]
+            enc(codec, k, p).encode([d.copy() for d in data], par)
+            assert all((par[r] == ref[r]).all() for r in range(rows)), (codec, k, p, n, zc, zch)
+        assert lib.ozec_set_tuning(b"host_zc_chunks", 2) == 0
         units = list(data) + list(ref) + [np.zeros(n, np.uint8)] * (p - rows)
         erased = [0, k] if codec == "rs" else [1]
         for pinned in (True, False):
@@ -1128,3 +1132,4 @@ def test_host_calls_zero_copy_and_copy_paths(zc, codec, k, p, n):
         pool.free()
     finally:
         lib.ozec_set_tuning(b"host_zero_copy", 48)
+        lib.ozec_set_tuning(b"host_zc_chunks", 2)

@@ -100,13 +100,16 @@ def test_encode_crc_odd_cells_c5_shape():
 def test_fused_min_units_routes_small_batches_unfused(k, p, n):
     """Batches of 16-B cells below fused_min_units (stripe x window units) take the unfused kernels, byte-granular
     ones stay fused: same bytes and CRCs either way."""
+    import ctypes
     lib = L.lib()
+    prev = ctypes.c_int64()
+    assert lib.ozec_get_tuning(b"fused_min_units", ctypes.byref(prev)) == 0
     try:
-        for m in (0, 1 << 40):
+        for m in (0, 1024, 1 << 40):  # fused everywhere, libozec's default routing, unfused everywhere
             assert lib.ozec_set_tuning(b"fused_min_units", m) == 0
             _packed_case(k, p, n, 2, 16384, ck.ChecksumType.CRC32C, 0, [k, n])
     finally:
-        lib.ozec_set_tuning(b"fused_min_units", 1024)
+        lib.ozec_set_tuning(b"fused_min_units", prev.value)
 
 
 @pytest.mark.parametrize("k,p,n", [(6, 3, 700_001), (10, 4, 16384 + 3), (3, 2, 1007), (6, 2, 50_001)])

@@ -477,8 +477,11 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
   chunk = std::max(chunk, (len + kMaxChunks - 1) / kMaxChunks);
   chunk = std::max(gran, chunk / gran * gran);
   // zero copy for a call alone on the GPU's slots: concurrent callers keep the SDMA copies, which together fill the link
-  // (four JNI threads: 52 GB/s through copies, 43 with every call zero-copy, profiles/r06/zero_copy/)
-  const int64_t zc_grid = zc && ctx->leased.load() <= 1 ? ozec::g_tune.host_zero_copy.load(std::memory_order_relaxed) : 0;
+  // (four JNI threads: 52 GB/s through copies, 43 with every call zero-copy, profiles/r06/zero_copy/) -- except small
+  // cells (host_zc_shared_max), whose calls are latency-bound and leave the link half idle
+  const int64_t zc_small = ozec::g_tune.host_zc_shared_max.load(std::memory_order_relaxed);
+  const bool zc_here = ctx->leased.load() <= 1 || (zc_small > 0 && len <= static_cast<size_t>(zc_small));
+  const int64_t zc_grid = zc && zc_here ? ozec::g_tune.host_zero_copy.load(std::memory_order_relaxed) : 0;
   // zero copy, one call in one chunk: host_zc_chunks column chunks (2) of at least 256 KiB per unit, so the staging
   // copies of one overlap the kernel on another (1 MiB-cell rs-6-3 stripe from pageable cells 289 -> 239 us; four
   // chunks 360, profiles/r06/percall/)
@@ -2182,6 +2185,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "host_zero_copy") {
     if (value < 0) return bad();
     t.host_zero_copy.store(value);
+  } else if (k == "host_zc_shared_max") {
+    if (value < 0) return bad();
+    t.host_zc_shared_max.store(value);
   } else if (k == "host_zc_chunks") {
     if (value < 1 || value > 16) return bad();
     t.host_zc_chunks.store(value);
@@ -2218,6 +2224,7 @@ int ozec_get_tuning(const char *key, int64_t *value) {
   else if (k == "host_duplex") *value = t.host_duplex.load();
   else if (k == "host_zero_copy") *value = t.host_zero_copy.load();
   else if (k == "host_zc_chunks") *value = t.host_zc_chunks.load();
+  else if (k == "host_zc_shared_max") *value = t.host_zc_shared_max.load();
   else if (k == "host_pitch16") *value = t.host_pitch16.load();
   else if (k == "fused_min_units") *value = t.fused_min_units.load();
   else if (k == "rec_min_units") *value = t.rec_min_units.load();

@@ -190,6 +190,11 @@ struct TuneKnobs {
   std::atomic<int64_t> host_zc_chunks{2};  // a lone zero-copy call from pageable (or callback-fed) units runs in
                                            // this many column chunks of at least 256 KiB per unit, the staging
                                            // copies of one overlapping the kernel on another (1: no overlap)
+  std::atomic<int64_t> host_zc_shared_max{64 << 10};  // host coding calls of at most this many bytes per unit take
+                                                     // zero copy even beside other calls in flight (0: only a lone
+                                                     // call does).  JNI 64 KiB cells, 16 threads: 238 -> 174-177 us
+                                                     // per stripe; 256 KiB cells at 4 threads lose (145 -> 212-245
+                                                     // us), profiles/r06/jni_forms/jnisweep_r6r.json
   std::atomic<int64_t> host_duplex{0};  // pinned host-buffer coding calls of at least this many bytes per unit go
                                         // up, through the kernel and back in column chunks, the D2H of chunk c on a
                                         // second stream beside the H2D of chunk c+1 (0: off, the default: 512 KiB

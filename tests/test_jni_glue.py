@@ -538,12 +538,14 @@ def test_heap_arenas_are_pooled_across_threads(J, java):
 
 
 @pytest.mark.gpu
-def test_concurrent_heap_calls_take_either_form_exactly(J, java):
+@pytest.mark.parametrize("n", [300_000, 65536 - 3])  # copy path beside other calls; zero copy (host_zc_shared_max)
+def test_concurrent_heap_calls_take_either_form_exactly(J, java, n):
     """Default (auto) form choice: a call alone takes the callback form, a call made while another coder call is in
-    flight takes the arena form.  Eight threads encoding and decoding at once: every call exact, every call counted
-    under one of the two forms, and a call alone afterwards takes the callback form."""
+    flight takes the arena form (whose libozec call codes the arena in place: by DMA for large cells, zero copy for cells
+    up to host_zc_shared_max).  Eight threads encoding and decoding at once: every call exact, every call counted under
+    one of the two forms, and a call alone afterwards takes the callback form."""
     import threading
-    k, p, n = 6, 3, 300_000
+    k, p = 6, 3
     prev = J.ozec_jni_heap_mode(HEAP_AUTO, None, None)
     h = call(J, "coderCreate", 0, 0, k, p)
     hd = call(J, "coderCreate", 1, 0, k, p)

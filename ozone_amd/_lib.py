@@ -57,7 +57,14 @@ c_intp = ctypes.POINTER(ctypes.c_int)
 c_i64 = ctypes.c_int64
 c_size = ctypes.c_size_t
 
+# ozec_fill_fn / ozec_drain_fn (include/ozec.h): (user, off, len, unit pointers) -> status
+FILL_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_voidp, c_size, c_size, ctypes.POINTER(ctypes.c_void_p))
+DRAIN_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_voidp, c_size, c_size, ctypes.POINTER(ctypes.c_void_p))
+
 _SIGS = {
+    "ozec_encode_cb": (ctypes.c_int, [c_voidp, c_size, FILL_FN, DRAIN_FN, c_voidp]),
+    "ozec_decode_cb": (ctypes.c_int, [c_voidp, ctypes.POINTER(ctypes.c_uint8), c_intp, ctypes.c_int, c_size, FILL_FN,
+                                      DRAIN_FN, c_voidp]),
     "ozec_last_error": (ctypes.c_char_p, []),
     "ozec_version": (ctypes.c_int, []),
     "ozec_device_count": (ctypes.c_int, []),

@@ -2170,6 +2170,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
     ozec::set_copy_threads(static_cast<int>(value));
   } else if (k == "copy_stream") {
     if (!ozec::set_copy_stream(static_cast<int>(value))) return bad();
+  } else if (k == "copy_spin_us") {
+    if (value < 0 || value > 100000) return bad();
+    ozec::set_copy_spin_us(value);
   } else if (k == "e2e_chunk") {
     if (value <= 0) return bad();
     t.e2e_chunk.store(value);
@@ -2224,6 +2227,7 @@ int ozec_get_tuning(const char *key, int64_t *value) {
   else if (k == "host_duplex") *value = t.host_duplex.load();
   else if (k == "host_zero_copy") *value = t.host_zero_copy.load();
   else if (k == "host_zc_chunks") *value = t.host_zc_chunks.load();
+  else if (k == "copy_spin_us") *value = ozec::copy_spin_us();
   else if (k == "host_zc_shared_max") *value = t.host_zc_shared_max.load();
   else if (k == "host_pitch16") *value = t.host_pitch16.load();
   else if (k == "fused_min_units") *value = t.fused_min_units.load();

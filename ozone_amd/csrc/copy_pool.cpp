@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <condition_variable>
 #include <cstdlib>
@@ -88,6 +89,21 @@ struct Job {
   }
 };
 
+// copy_spin (ozec_set_tuning "copy_spin_us"): how long a pool worker, and a caller waiting for its job's last pieces,
+// poll before sleeping on a condition variable (0: sleep at once)
+std::atomic<int64_t> g_spin_ns{0};
+
+template <class Pred>
+void spin_until(Pred done) {
+  const int64_t ns = g_spin_ns.load(std::memory_order_relaxed);
+  if (ns <= 0) return;
+  const auto end = std::chrono::steady_clock::now() + std::chrono::nanoseconds(ns);
+  while (!done()) {
+    for (int i = 0; i < 64; ++i) _mm_pause();
+    if (std::chrono::steady_clock::now() >= end) return;
+  }
+}
+
 // One pool per host NUMA node: a GPU's staging buffers live on its node (numa.hpp), and the copies into and out of
 // them run on that node's CPUs -- a process driving GPUs on both sockets (devices.hpp) keeps every staging copy local.
 int g_default_threads = -1;  // -1: min(8, hardware threads / 2) - 1, or OZEC_COPY_THREADS
@@ -117,9 +133,11 @@ class Pool {
     {
       std::lock_guard<std::mutex> lk(mu_);
       jobs_.push_back(job);
+      epoch_.fetch_add(1);
     }
     cv_.notify_all();
     job->work();
+    spin_until([&] { return job->done.load() == job->pieces.size(); });
     std::unique_lock<std::mutex> lk(job->mu);
     job->cv.wait(lk, [&] { return job->done.load() == job->pieces.size(); });
   }
@@ -147,11 +165,16 @@ class Pool {
   }
 
   void loop() {
+    uint64_t seen = epoch_.load();
     for (;;) {
+      // a worker that just finished keeps polling for copy_spin before it sleeps: the staging copies of a pipelined
+      // call come every few tens of microseconds, and a futex wake-up costs about as much as a 256 KiB piece
+      spin_until([&] { return epoch_.load() != seen || stop_.load(); });
       std::shared_ptr<Job> job;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
+        seen = epoch_.load();
         if (stop_) return;
         job = jobs_.front();
         if (job->next.load() >= job->pieces.size()) {  // fully claimed: retire it
@@ -167,7 +190,8 @@ class Pool {
   std::condition_variable cv_;
   std::deque<std::shared_ptr<Job>> jobs_;
   std::vector<std::thread> workers_;
-  bool stop_ = false;
+  std::atomic<uint64_t> epoch_{0};  // jobs queued so far (the spinning workers' signal)
+  std::atomic<bool> stop_{false};
   int nthreads_ = 0;
   int node_ = -1;
 };
@@ -189,6 +213,10 @@ void set_copy_threads(int n) {
   g_default_threads = std::max(0, n);
   for (auto &kv : g_pools) kv.second->resize(g_default_threads);
 }
+
+void set_copy_spin_us(int64_t us) { g_spin_ns.store(std::max<int64_t>(0, us) * 1000); }
+
+int64_t copy_spin_us() { return g_spin_ns.load() / 1000; }
 
 bool set_copy_stream(int mode) {
   if (mode < -1 || mode > 3) return false;

@@ -3,6 +3,7 @@
 // >= 256 KiB pieces over a small process-wide worker pool, the calling thread taking part.
 #pragma once
 #include <cstddef>
+#include <cstdint>
 #include <vector>
 
 namespace ozec {
@@ -21,6 +22,9 @@ enum class CopyDir { kToStaging, kFromStaging };
 void parallel_copy(const std::vector<CopyTask> &tasks, CopyDir dir, bool shared = true, int node = -1);
 // threads used besides the caller by every node's pool (0 = copy inline); set by ozec_set_tuning("copy_threads", n)
 void set_copy_threads(int n);
+// how long pool workers and waiting callers poll before sleeping (0: not at all)
+void set_copy_spin_us(int64_t us);
+int64_t copy_spin_us();
 // pieces copied with streaming (non-temporal) stores: 1 both directions, 2 into staging only, 3 only for copies that
 // share DRAM with other transfers, 0 plain memcpy, -1 auto (1 where AVX2 exists); set by
 // ozec_set_tuning("copy_stream", n); false (nothing changed) outside -1..3

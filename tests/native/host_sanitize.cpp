@@ -158,12 +158,14 @@ static void check_copy() {
   for (int stream : {1, 2, 3, 0})  // streaming stores both ways / into staging only / when shared, plain memcpy
     for (int threads : {4, 0, 2}) {
       ozec::set_copy_stream(stream);
+      ozec::set_copy_spin_us(stream == 2 ? 50 : 0);  // workers and callers polling before they sleep, or not
       ozec::set_copy_threads(threads);  // resize the pool between rounds of concurrent callers
       std::vector<std::thread> ts;
       for (int c = 0; c < 4; ++c) ts.emplace_back(caller, c);
       for (auto &t : ts) t.join();
     }
   ozec::set_copy_stream(-1);
+  ozec::set_copy_spin_us(0);
   CHECK(bad.load() == 0, "%d parallel copies differ", bad.load());
 }
 

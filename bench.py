@@ -1200,6 +1200,8 @@ def jni_rows(args, threads=(1, 4, 16), cells=(64 << 10, MIB), seconds=0.5):
     SetByteArrayRegion back.  rs-6-3, T threads sharing one coder (RawErasureCoderBenchmark.java:201-206), beside
     the CPU doing one stripe per call on one thread (oracle/cpu_baseline.c percall_encode: the RSUtil table loop)."""
     specs = [f"{mode}:6:3:{c}:{t}" for mode in ("encode", "decode") for c in cells for t in threads]
+    # a writer whose buffer pool is pinned (OzecNative.allocatePinned): encodeDirect on pinned direct buffers
+    specs += [f"encodedirect:6:3:{c}:{t}" for c in cells for t in threads]
     rows = jni_percall(specs, seconds)
     cpu = {}
     for c in cells:
@@ -1207,8 +1209,8 @@ def jni_rows(args, threads=(1, 4, 16), cells=(64 << 10, MIB), seconds=0.5):
     for r in rows:
         if r["mode"] == "encode":
             r["cpu_1thread_us_per_stripe"] = round(cpu[r["cell_bytes"]], 1)
-    return {"path": "jni/ozec_jni.c encodeArrays / decodeArrays (heap byte[]) via the JNI test double, rs-6-3, decode "
-                    "of 3 erased {0,1,2}", "rows": rows,
+    return {"path": "jni/ozec_jni.c encodeArrays / decodeArrays (heap byte[]) and encodeDirect (pinned direct buffers, "
+                    "encodedirect rows) via the JNI test double, rs-6-3, decode of 3 erased {0,1,2}", "rows": rows,
             "cpu": f"oracle/cpu_baseline.c percall_encode (1 thread, one stripe per call), {flags}"}
 
 

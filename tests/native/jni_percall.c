@@ -8,6 +8,8 @@
  *
  *   jni_percall SECONDS SPEC...        SPEC = encode|decode:K:P:CELL_BYTES:THREADS
  *
+ * SPEC modes encodedirect / decodedirect call encodeDirect / decodeDirect on pinned direct buffers instead (every
+ * cell in one ozec_host_alloc block, what OzecNative.allocatePinned hands a writer's buffer pool).
  * prints one JSON object per SPEC: calls, seconds, us per stripe (wall / calls per thread), GB/s of data bytes.  Before
  * timing, one encode + decode round trip of every thread's stripe is checked (the decoded units equal the originals).
  */
@@ -26,24 +28,28 @@ jlong P(coderCreate)(JNIEnv *, jclass, jboolean, jint, jint, jint);
 void P(coderRelease)(JNIEnv *, jclass, jlong);
 void P(encodeArrays)(JNIEnv *, jclass, jlong, jobjectArray, jintArray, jint, jobjectArray, jintArray);
 void P(decodeArrays)(JNIEnv *, jclass, jlong, jobjectArray, jintArray, jint, jintArray, jobjectArray, jintArray);
+void P(encodeDirect)(JNIEnv *, jclass, jlong, jobjectArray, jintArray, jint, jobjectArray, jintArray);
+void P(decodeDirect)(JNIEnv *, jclass, jlong, jobjectArray, jintArray, jint, jintArray, jobjectArray, jintArray);
 int ozec_jni_heap_mode(int mode, unsigned long *cb_calls, unsigned long *arena_calls);
 
 JNIEnv *mock_env(void);
 struct mock_object *mock_bytes(void *p, int64_t len);
+struct mock_object *mock_direct(void *p, int64_t cap);
 struct mock_object *mock_ints(int32_t *p, int64_t n);
 struct mock_object *mock_objects(int64_t n);
 void mock_set(struct mock_object *arr, int64_t i, struct mock_object *v);
 int mock_take_exception(char *cls, int cls_cap, char *msg, int msg_cap);
 
 enum { MAXU = 32 };
-static int K, R, CELL, DECODE;
+static int K, R, CELL, DECODE, DIRECT;
 static double SECONDS;
 static jlong g_enc, g_dec;
 static int g_erased[4] = {0, 1, 2, 3}; /* rs-6-3 decode: 3 erased {0, 1, 2}; rs-10-4: {0, 1, 2, 3} */
 static int g_ne;
 
 typedef struct {
-  uint8_t *unit[MAXU]; /* k data + p parity cells, each a byte[] */
+  uint8_t *unit[MAXU]; /* k data + p parity cells, each a byte[] (DIRECT: cells of one pinned block) */
+  uint8_t *block;      /* DIRECT: the ozec_host_alloc block holding every cell and the decode outputs */
   uint8_t *rec[4];     /* decode outputs */
   struct mock_object *enc_in, *enc_out, *dec_in, *dec_out, *zeros_in, *zeros_out, *zeros_dec, *erased;
   int32_t zeros[MAXU], er[4];
@@ -68,8 +74,14 @@ static void fail_if_exception(const char *what) {
 static void setup(worker_t *w, unsigned seed) {
   JNIEnv *env = mock_env();
   (void)env;
+  w->block = NULL;
+  if (DIRECT && ozec_host_alloc((size_t)(K + R + g_ne) * (size_t)CELL, (void **)&w->block) != 0) {
+    fprintf(stderr, "ozec_host_alloc failed: %s\n", ozec_last_error());
+    exit(2);
+  }
+  struct mock_object *(*wrap)(void *, int64_t) = DIRECT ? mock_direct : mock_bytes;
   for (int u = 0; u < K + R; ++u) {
-    w->unit[u] = malloc((size_t)CELL);
+    w->unit[u] = DIRECT ? w->block + (size_t)u * (size_t)CELL : malloc((size_t)CELL);
     if (u < K)
       for (int i = 0; i < CELL; ++i) w->unit[u][i] = (uint8_t)((seed = seed * 1103515245u + 12345u) >> 16);
     else
@@ -77,8 +89,8 @@ static void setup(worker_t *w, unsigned seed) {
   }
   w->enc_in = mock_objects(K);
   w->enc_out = mock_objects(R);
-  for (int u = 0; u < K; ++u) mock_set(w->enc_in, u, mock_bytes(w->unit[u], CELL));
-  for (int r = 0; r < R; ++r) mock_set(w->enc_out, r, mock_bytes(w->unit[K + r], CELL));
+  for (int u = 0; u < K; ++u) mock_set(w->enc_in, u, wrap(w->unit[u], CELL));
+  for (int r = 0; r < R; ++r) mock_set(w->enc_out, r, wrap(w->unit[K + r], CELL));
   memset(w->zeros, 0, sizeof w->zeros);
   w->zeros_in = mock_ints(w->zeros, K + R);
   w->zeros_out = mock_ints(w->zeros, R);
@@ -86,12 +98,12 @@ static void setup(worker_t *w, unsigned seed) {
   for (int u = 0; u < K + R; ++u) {
     int gone = 0;
     for (int e = 0; e < g_ne; ++e) gone |= g_erased[e] == u;
-    mock_set(w->dec_in, u, gone ? NULL : mock_bytes(w->unit[u], CELL));
+    mock_set(w->dec_in, u, gone ? NULL : wrap(w->unit[u], CELL));
   }
   w->dec_out = mock_objects(g_ne);
   for (int e = 0; e < g_ne; ++e) {
-    w->rec[e] = calloc(1, (size_t)CELL);
-    mock_set(w->dec_out, e, mock_bytes(w->rec[e], CELL));
+    w->rec[e] = DIRECT ? w->block + (size_t)(K + R + e) * (size_t)CELL : calloc(1, (size_t)CELL);
+    mock_set(w->dec_out, e, wrap(w->rec[e], CELL));
     w->er[e] = g_erased[e];
   }
   w->zeros_dec = mock_ints(w->zeros, g_ne);
@@ -101,11 +113,12 @@ static void setup(worker_t *w, unsigned seed) {
 static void call(worker_t *w) {
   JNIEnv *env = mock_env();
   if (DECODE)
-    P(decodeArrays)(env, NULL, g_dec, (jobjectArray)w->dec_in, (jintArray)w->zeros_in, CELL, (jintArray)w->erased,
-                    (jobjectArray)w->dec_out, (jintArray)w->zeros_dec);
+    (DIRECT ? P(decodeDirect) : P(decodeArrays))(env, NULL, g_dec, (jobjectArray)w->dec_in, (jintArray)w->zeros_in,
+                                                 CELL, (jintArray)w->erased, (jobjectArray)w->dec_out,
+                                                 (jintArray)w->zeros_dec);
   else
-    P(encodeArrays)(env, NULL, g_enc, (jobjectArray)w->enc_in, (jintArray)w->zeros_in, CELL, (jobjectArray)w->enc_out,
-                    (jintArray)w->zeros_out);
+    (DIRECT ? P(encodeDirect) : P(encodeArrays))(env, NULL, g_enc, (jobjectArray)w->enc_in, (jintArray)w->zeros_in,
+                                                 CELL, (jobjectArray)w->enc_out, (jintArray)w->zeros_out);
 }
 
 static pthread_barrier_t g_bar;
@@ -133,7 +146,8 @@ static int run_spec(const char *spec) {
     fprintf(stderr, "bad spec %s\n", spec);
     return 1;
   }
-  DECODE = !strcmp(mode, "decode");
+  DECODE = !strncmp(mode, "decode", 6);
+  DIRECT = strstr(mode, "direct") != NULL;  /* encodedirect / decodedirect: pinned direct buffers (allocatePinned) */
   g_ne = R < 4 ? R : 4;
   JNIEnv *env = mock_env();
   g_enc = P(coderCreate)(env, NULL, 0, 0, K, R);
@@ -177,12 +191,17 @@ static int run_spec(const char *spec) {
   printf("{\"mode\": \"%s\", \"k\": %d, \"p\": %d, \"erased\": %d, \"cell_bytes\": %d, \"threads\": %d, \"calls\": %ld, "
          "\"seconds\": %.4f, \"us_per_stripe\": %.2f, \"GBps\": %.3f, \"round_trip_ok\": %s, "
          "\"callback_form_calls\": %lu, \"arena_form_calls\": %lu}\n",
-         DECODE ? "decode" : "encode", K, R, DECODE ? g_ne : 0, CELL, T, calls, el, el / ((double)calls / T) * 1e6,
+         DECODE ? (DIRECT ? "decodedirect" : "decode") : (DIRECT ? "encodedirect" : "encode"), K, R, DECODE ? g_ne : 0,
+         CELL, T, calls, el, el / ((double)calls / T) * 1e6,
          data / el / 1e9, ok ? "true" : "false", cb1 - cb0, ar1 - ar0);
   fflush(stdout);
   P(coderRelease)(env, NULL, g_enc);
   P(coderRelease)(env, NULL, g_dec);
   for (int t = 0; t < T; ++t) {
+    if (DIRECT) {
+      (void)ozec_host_free(ws[t].block);
+      continue;
+    }
     for (int u = 0; u < K + R; ++u) free(ws[t].unit[u]);
     for (int e = 0; e < g_ne; ++e) free(ws[t].rec[e]);
   }

@@ -48,6 +48,11 @@ run() {
         --output-format csv -- python3 bench.py --workload c2 --no-cpu --no-pmc --no-e2e --no-legs --no-jni \
         > "$OUT/prof_c2.log" 2>&1 && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_legs" -o run \
         --output-format csv -- python3 bench.py --workload legs --no-cpu --no-pmc > "$OUT/prof_legs.log" 2>&1 ;;
+    rehearse)  # the driver's N = 2 launch (torchrun, two ranks) on one GPU: two gloo ranks on device 0, default line
+      step "rehearse N=2"
+      OZEC_BENCH_SAME_DEVICE=1 OZEC_DIST_BACKEND=gloo OZEC_BENCH_FULL=$OUT/bench_2rank_full.json timeout -k 10 900 \
+        python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 \
+        bench.py --gpus 2 --steps 5 --warmup 3 > "$OUT/bench_2rank.json" 2> "$OUT/bench_2rank.err" ;;
     jni)
       step "bench jni rows"
       timeout -k 10 300 python -u bench.py --workload jni > "$OUT/jni.json" 2> "$OUT/jni.err" ;;

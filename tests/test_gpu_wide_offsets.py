@@ -104,3 +104,50 @@ def test_units_more_than_2gib_apart(codec, k, p, shift, n):
         for u in range(k + p):
             assert torch.equal(base[s * ss + u * US + n:s * ss + u * US + n + 16], guard_after[i]), (codec, s, u)
             i += 1
+
+
+@pytest.mark.parametrize("codec,k,p", [("rs", 6, 3), ("xor", 2, 1)])
+def test_wide_fused_at_bench_cell_size(codec, k, p):
+    """The WIDE fused forms at the bench's cell size (profiles/r06/fused_ab/): 24 stripes of 1 MiB cells, units 768 MiB
+    apart, at an odd base -- one fused launch (past the small-batch threshold under libozec's own routing too), every
+    stripe's parity and all units' CRC32C windows vs the oracle, and a fused reconstruction of two units (one) whose
+    rebuilt units and CRCs match and whose verification of the stored CRCs passes."""
+    S, n, bpc, shift = 24, 1 << 20, 16384, 3
+    ss = n
+    buf = torch.empty(shift + (k + p - 1) * US + S * ss + 64, dtype=torch.uint8, device=DEV)
+    base = buf[shift:]
+    rng = np.random.default_rng([k, p, 24])
+    data = rng.integers(0, 256, (S, k, n), dtype=np.uint8)
+    for u in range(k):
+        base[u * US:u * US + S * ss].copy_(to_dev(data[:, u].reshape(-1)))
+    conf = rc.ECReplicationConfig(k, p, codec)
+    nwin = n // bpc
+    crcs = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    r0 = _routes()
+    rc.RawErasureEncoder(conf).encode_crc_batch(base, ss, US, base[k * US:], ss, US, S, n, ck.ChecksumType.CRC32C,
+                                                bpc, crcs)
+    r1 = _routes()
+    assert (r1[0] - r0[0], r1[1] - r0[1]) == (1, 0), (r0, r1)
+    erased = [0] if codec == "xor" else [1, k + 1]
+    present = [u for u in range(k + p) if u not in erased][:k]
+    rout = torch.zeros((S, len(erased), n), dtype=torch.uint8, device=DEV)
+    rcrc = torch.zeros((S, len(erased), nwin), dtype=torch.int32, device=DEV)
+    mism = torch.zeros(S, dtype=torch.int32, device=DEV)
+    rc.RawErasureDecoder(conf).reconstruct_crc_batch(base, ss, US, present, erased, rout, len(erased) * n, n, S, n,
+                                                     ck.ChecksumType.CRC32C, bpc, rcrc, d_expected=crcs,
+                                                     d_mismatch=mism)
+    torch.cuda.synchronize()
+    c = to_host(crcs).view(np.uint32)
+    par = [to_host(base[(k + q) * US:(k + q) * US + S * ss]).reshape(S, n) for q in range(p)]
+    ro, rcc, m = to_host(rout), to_host(rcrc).view(np.uint32), to_host(mism)
+    for s in range(S):
+        ref = [oracle.xor_encode(list(data[s]))] if codec == "xor" else oracle.rs_encode(k, p, list(data[s]))
+        units = list(data[s]) + list(ref)
+        for q in range(p):
+            assert (par[q][s] == ref[q]).all(), (codec, s, q)
+        for u in range(k + p):
+            assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, units[u], bpc)).all(), (codec, s, u)
+        for i, e in enumerate(erased):
+            assert (ro[s, i] == units[e]).all() and (rcc[s, i] == c[s, e]).all(), (codec, s, e)
+        assert m[s] == -1, (codec, s, m)
+    del buf, base

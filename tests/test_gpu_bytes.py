@@ -253,3 +253,32 @@ def test_xor_fused_any_length_and_offset(k, n, shift):
             assert m[s] == -1
         assert (oc[s, 0] == oracle.crc_windows(oracle.CRC32C, rebuilt, bpc)).all(), (k, n, shift, s)
     assert m[1] == present[-1] * nwin + pos // bpc
+
+
+@pytest.mark.parametrize("k,n", [(6, (1 << 20) + 5), (2, 700_001)])
+def test_xor_fused_tail_at_bench_cell_size(k, n):
+    """The XOR TAIL fused form at the A/B's cell sizes (profiles/r06/fused_ab/): 48 packed stripes of xor-k-1 whose
+    cells are not a multiple of 16 B (every unit at an odd offset), at an odd base: one fused launch (past the
+    small-batch threshold under libozec's own routing too), parity and every unit's CRC32C windows vs the oracle."""
+    p, S, bpc, shift = 1, 48, 16384, 3
+    rng = np.random.default_rng([k, n, 48])
+    data = rng.integers(0, 256, (S, k, n), dtype=np.uint8)
+    flat = np.full(GUARD + shift + S * (k + p) * n + GUARD, 0xA5, np.uint8)
+    flat[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)[:, :k] = data
+    d = to_dev(flat)
+    base = d[GUARD + shift:]
+    nwin = -(-n // bpc)
+    crcs = torch.zeros((S, k + p, nwin), dtype=torch.int32, device=DEV)
+    f0, u0 = _routes()
+    rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, "xor")).encode_crc_batch(
+        base, (k + p) * n, n, base[k * n:], (k + p) * n, n, S, n, ck.ChecksumType.CRC32C, bpc, crcs)
+    f1, u1 = _routes()
+    assert (f1 - f0, u1 - u0) == (1, 0), "the encode did not take the fused kernel"
+    got, c = to_host(d), to_host(crcs).view(np.uint32)
+    assert (got[:GUARD + shift] == 0xA5).all() and (got[GUARD + shift + S * (k + p) * n:] == 0xA5).all()
+    units = got[GUARD + shift:GUARD + shift + S * (k + p) * n].reshape(S, k + p, n)
+    for s in range(S):
+        ref = oracle.xor_encode(list(data[s]))
+        assert (units[s, k] == ref).all(), (k, n, s)
+        for u in range(k + 1):
+            assert (c[s, u] == oracle.crc_windows(oracle.CRC32C, units[s, u], bpc)).all(), (k, n, s, u)

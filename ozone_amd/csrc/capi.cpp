@@ -208,7 +208,7 @@ struct DevCtx {
     if (free_slots.empty()) {
       auto s = std::make_unique<Slot>();
       s->device = device;
-      OZEC_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+      OZEC_HIP(ozec::make_stream(&s->stream));
       free_slots.push_back(s.get());
       slots.push_back(std::move(s));
     }
@@ -553,7 +553,7 @@ int staged_pipeline(DevCtx *ctx, int nin, const uint8_t *const *in, size_t len, 
     if (duplex > 0 && len >= static_cast<size_t>(duplex) && obytes == len && out_pos(0) == 0) {
       const size_t cw = std::max<size_t>(256u << 10, round_up((len + 7) / 8, 4096));
       const size_t nc = (len + cw - 1) / cw;
-      if (!s->stream2) OZEC_HIP(hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking));
+      if (!s->stream2) OZEC_HIP(ozec::make_stream(&s->stream2));
       if (int rc = s->ensure_events(nc)) return rc;
       for (size_t c = 0; c < nc; ++c) {
         const size_t off = c * cw, cl = std::min(cw, len - off);
@@ -1441,9 +1441,9 @@ static int encode_crc_host_batch_dev(ozec_coder *enc, const uint8_t *h_in, int64
   const bool crc_pinned = !with_crc || range_pinned(h_crcs, num_stripes * ncrc * sizeof(uint32_t));
   const bool staged = !in_pinned || !out_pinned || !crc_pinned;
   if (!P.h2d) {
-    OZEC_HIP(hipStreamCreateWithFlags(&P.h2d, hipStreamNonBlocking));
-    OZEC_HIP(hipStreamCreateWithFlags(&P.comp, hipStreamNonBlocking));
-    OZEC_HIP(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
+    OZEC_HIP(ozec::make_stream(&P.h2d));
+    OZEC_HIP(ozec::make_stream(&P.comp));
+    OZEC_HIP(ozec::make_stream(&P.d2h));
     for (int b = 0; b < E2E::NB; ++b) {
       OZEC_HIP(hipEventCreateWithFlags(&P.h2d_done[b], hipEventDisableTiming));
       OZEC_HIP(hipEventCreateWithFlags(&P.comp_done[b], hipEventDisableTiming));
@@ -1806,9 +1806,9 @@ static int reconstruct_crc_host_batch_dev(ozec_coder *dec, const uint8_t *h_in, 
   const bool mis_pinned = !h_expected || range_pinned(h_mismatch, num_stripes * sizeof(int32_t));
   const bool staged = !in_pinned || !out_pinned || !exp_pinned || !ocrc_pinned || !mis_pinned;
   if (!P.h2d) {
-    OZEC_HIP(hipStreamCreateWithFlags(&P.h2d, hipStreamNonBlocking));
-    OZEC_HIP(hipStreamCreateWithFlags(&P.comp, hipStreamNonBlocking));
-    OZEC_HIP(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
+    OZEC_HIP(ozec::make_stream(&P.h2d));
+    OZEC_HIP(ozec::make_stream(&P.comp));
+    OZEC_HIP(ozec::make_stream(&P.d2h));
     for (int b = 0; b < E2E::NB; ++b) {
       OZEC_HIP(hipEventCreateWithFlags(&P.h2d_done[b], hipEventDisableTiming));
       OZEC_HIP(hipEventCreateWithFlags(&P.comp_done[b], hipEventDisableTiming));
@@ -2191,6 +2191,9 @@ int ozec_set_tuning(const char *key, int64_t value) {
   } else if (k == "host_zc_shared_max") {
     if (value < 0) return bad();
     t.host_zc_shared_max.store(value);
+  } else if (k == "stream_priority") {
+    if (value != 0 && value != 1) return bad();
+    t.stream_priority.store(static_cast<int>(value));
   } else if (k == "host_zc_chunks") {
     if (value < 1 || value > 16) return bad();
     t.host_zc_chunks.store(value);
@@ -2227,6 +2230,7 @@ int ozec_get_tuning(const char *key, int64_t *value) {
   else if (k == "host_duplex") *value = t.host_duplex.load();
   else if (k == "host_zero_copy") *value = t.host_zero_copy.load();
   else if (k == "host_zc_chunks") *value = t.host_zc_chunks.load();
+  else if (k == "stream_priority") *value = t.stream_priority.load();
   else if (k == "copy_spin_us") *value = ozec::copy_spin_us();
   else if (k == "host_zc_shared_max") *value = t.host_zc_shared_max.load();
   else if (k == "host_pitch16") *value = t.host_pitch16.load();

@@ -195,6 +195,14 @@ struct TuneKnobs {
                                                      // call does).  JNI 64 KiB cells, 16 threads: 238 -> 174-177 us
                                                      // per stripe; 256 KiB cells at 4 threads lose (145 -> 212-245
                                                      // us), profiles/r06/jni_forms/jnisweep_r6r.json
+  std::atomic<int> stream_priority{0};  // libozec's streams made by hipStreamCreateWithFlags (0) or by
+                                        // hipStreamCreateWithPriority at the default priority (1), read when a stream
+                                        // is made.  In a probe the first plain stream's 1-D copies run at the link
+                                        // rate and every later one's at half (H2D) to a third (D2H) of it, while
+                                        // streams made with a priority all run at the link rate
+                                        // (profiles/r06/engines/engines_how*.json); libozec's own copy patterns (2-D
+                                        // rect copies, concurrent slots, the host-batch pipelines) measured the same
+                                        // either way (profiles/r06/engines/ab_stream_priority/), so the default stays
   std::atomic<int64_t> host_duplex{0};  // pinned host-buffer coding calls of at least this many bytes per unit go
                                         // up, through the kernel and back in column chunks, the D2H of chunk c on a
                                         // second stream beside the H2D of chunk c+1 (0: off, the default: 512 KiB
@@ -239,6 +247,14 @@ constexpr int kCrcVariants[] = {2,   3,   4,   5,   20,  21,  22,  24,  28,  29,
                                  231, 234};
 
 extern TuneKnobs g_tune;
+
+// a non-blocking stream for libozec's copies and launches (TuneKnobs::stream_priority)
+inline hipError_t make_stream(hipStream_t *s) {
+  if (g_tune.stream_priority.load(std::memory_order_relaxed) == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+}
 
 // Per-thread cap on the coding kernels' grid (0: none), set around a zero-copy launch (capi.cpp staged_pipeline): a
 // kernel streaming over PCIe does best with a few dozen blocks looping over the chunks, so the reads of one chunk

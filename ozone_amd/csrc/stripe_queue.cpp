@@ -355,8 +355,8 @@ int ozec_stripe_queue_create(ozec_coder *enc, size_t cell_len, size_t stripes_pe
   q->batches.resize(qb >= 2 ? static_cast<size_t>(qb) : kDefaultBatches);
   for (Batch &b : q->batches) {
     b.pend.resize(q->S);
-    hipError_t e = q->h2d ? hipSuccess : hipStreamCreateWithFlags(&q->h2d, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking);
+    hipError_t e = q->h2d ? hipSuccess : ozec::make_stream(&q->h2d);
+    if (e == hipSuccess) e = ozec::make_stream(&b.stream);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&b.copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&b.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&b.d_units), q->S * q->stripe_bytes());

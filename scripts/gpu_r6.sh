@@ -40,7 +40,8 @@ run() {
       timeout -k 10 120 scripts/d2h_probe > "$OUT/d2h.json" 2> "$OUT/d2h.err" ;;
     engines)
       step "stream engine probe"
-      { timeout -k 10 120 scripts/stream_engine_probe 8 && HSA_ENABLE_SDMA=0 timeout -k 10 120 scripts/stream_engine_probe 8; } \
+      { timeout -k 10 120 scripts/stream_engine_probe ${ENGINE_STREAMS:-8} ${ENGINE_HOW:-0} && HSA_ENABLE_SDMA=0 \
+          timeout -k 10 120 scripts/stream_engine_probe ${ENGINE_STREAMS:-8} ${ENGINE_HOW:-0}; } \
         > "$OUT/engines.json" 2> "$OUT/engines.err" ;;
     prof)  # rocprofv3 kernel statistics of the headline and of every leg with the bench's own warm-up and steps
       step "rocprof c2 + legs"

@@ -22,10 +22,20 @@ int main(int argc, char **argv) {
   uint8_t *h = nullptr, *d = nullptr;
   if (hipHostMalloc(reinterpret_cast<void **>(&h), hb + db, hipHostMallocDefault) != hipSuccess) return 1;
   if (hipMalloc(&d, hb + db) != hipSuccess) return 1;
-  hipStream_t st[32];
-  for (int i = 0; i < n; ++i) (void)hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
+  // argv[2]: how the streams are made -- 0 hipStreamCreateWithFlags (non-blocking), 1 blocking hipStreamCreate,
+  // 2 hipStreamCreateWithPriority at the highest priority, 3 at the lowest
+  const int how = argc > 2 ? std::atoi(argv[2]) : 0;
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  hipStream_t st[64];
+  for (int i = 0; i < n && i < 64; ++i) {
+    if (how == 1) (void)hipStreamCreate(&st[i]);
+    else if (how == 2) (void)hipStreamCreateWithPriority(&st[i], hipStreamNonBlocking, prio_hi);
+    else if (how == 3) (void)hipStreamCreateWithPriority(&st[i], hipStreamNonBlocking, prio_lo);
+    else (void)hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
+  }
   std::printf("[");
-  for (int i = -1; i < n; ++i) {
+  for (int i = -1; i < n && i < 64; ++i) {
     hipStream_t s = i < 0 ? nullptr : st[i];
     const double h2d = time_us(40, [&] {
       (void)hipMemcpyAsync(d, h, hb, hipMemcpyHostToDevice, s);
@@ -36,7 +46,7 @@ int main(int argc, char **argv) {
       (void)hipStreamSynchronize(s);
     });
     double both = 0;
-    if (i >= 0 && i + 1 < n) {
+    if (i >= 0 && i + 1 < n && i + 1 < 64) {
       hipStream_t s2 = st[i + 1];
       both = time_us(40, [&] {
         (void)hipMemcpyAsync(d, h, hb, hipMemcpyHostToDevice, s);

@@ -39,8 +39,19 @@ class Mover:
         self.inputs, self.outputs = inputs, outputs
         self.fills, self.drains, self.fill_slots = [], [], []
         self.fail_fill_at, self.fail_drain_at = fail_fill_at, fail_drain_at
-        self.fill = L.FILL_FN(self._fill)
-        self.drain = L.DRAIN_FN(self._drain)
+        self.errors = []  # exceptions inside a callback (ctypes would only print them): reported by check()
+        self.fill = L.FILL_FN(lambda *a: self._guard(self._fill, *a))
+        self.drain = L.DRAIN_FN(lambda *a: self._guard(self._drain, *a))
+
+    def _guard(self, fn, *args):
+        try:
+            return fn(*args)
+        except Exception as e:  # noqa: BLE001 - surfaced by check()
+            self.errors.append(e)
+            return -99
+
+    def check(self):
+        assert not self.errors, self.errors
 
     def _fill(self, user, off, n, dst):
         if self.fail_fill_at is not None and len(self.fills) == self.fail_fill_at:
@@ -89,7 +100,8 @@ def test_encode_cb_vs_oracle(codec, k, p, n, zc):
             [np.zeros(n, np.uint8)] * (p - 1)
         outs = [np.full(n, 0xA5, np.uint8) for _ in range(p)]
         m = Mover(data, outs)
-        assert lib.ozec_encode_cb(h, n, m.fill, m.drain, None) == 0, L.last_error()
+        assert lib.ozec_encode_cb(h, n, m.fill, m.drain, None) == 0, (L.last_error(), m.errors)
+        m.check()
         assert all((o == r).all() for o, r in zip(outs, ref)), (codec, k, p, n, zc)
         _tiles(m.fills, n)
         _tiles(m.drains, n)
@@ -123,7 +135,8 @@ def test_decode_cb_vs_oracle(codec, k, p, n, erased, absent):
         m = Mover(inputs, outs)
         present = (ctypes.c_uint8 * (k + p))(*[x is not None for x in inputs])
         er = (ctypes.c_int * len(erased))(*erased)
-        assert lib.ozec_decode_cb(h, present, er, len(erased), n, m.fill, m.drain, None) == 0, L.last_error()
+        assert lib.ozec_decode_cb(h, present, er, len(erased), n, m.fill, m.drain, None) == 0, (L.last_error(), m.errors)
+        m.check()
         assert all((o == w).all() for o, w in zip(outs, want)), (codec, k, p, erased)
         _tiles(m.fills, n)
         _tiles(m.drains, n)
@@ -150,11 +163,13 @@ def test_callback_failure_ends_the_call_and_the_next_works(where):
         m = Mover(data, outs, fail_fill_at=at if kind == "fill" else None,
                   fail_drain_at=at if kind == "drain" else None)
         rc = lib.ozec_encode_cb(h, n, m.fill, m.drain, None)
+        m.check()
         assert rc == (-77 if kind == "fill" else -78), (rc, m.fills, m.drains)
         assert len(m.fills if kind == "fill" else m.drains) == at
         outs2 = [np.zeros(n, np.uint8) for _ in range(p)]
         m2 = Mover(data, outs2)
-        assert lib.ozec_encode_cb(h, n, m2.fill, m2.drain, None) == 0, L.last_error()
+        assert lib.ozec_encode_cb(h, n, m2.fill, m2.drain, None) == 0, (L.last_error(), m2.errors)
+        m2.check()
         assert all((o == r).all() for o, r in zip(outs2, ref))
     finally:
         _free(h)

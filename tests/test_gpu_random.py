@@ -321,3 +321,103 @@ def test_random_stripe_queue(i):
             got = crcs.reshape(k + rows, -1)
             for u, x in enumerate(d + ref[:rows]):
                 assert (got[u] == oracle.crc_windows(_otype(ctype), x, bpc)).all(), (codec, k, p, t, n, u)
+
+
+@pytest.mark.parametrize("i", range(N_CASES // 2))
+def test_random_host_zero_copy_and_callbacks(i):
+    """Round 6's host paths under random knobs: zero copy on / off / at a tiny grid (host_zero_copy), 1-3 column chunks
+    (host_zc_chunks), cells pinned in one pool at a stride (the JNI arena's layout) or pageable, and the
+    caller-moves-the-bytes entry points (ozec_encode_cb / ozec_decode_cb, the JNI heap-array form) -- encode and a
+    decode of the drawn erasure pattern vs the oracle."""
+    import ctypes
+    from ozone_amd import _lib as L
+    from ozone_amd.stripe_queue import host_alloc
+    lib = L.lib()
+    r = _rng(9, i)
+    codec, k, p = _codec(r)
+    n = int(r.integers(1, 2_600_000))
+    zc, zch = int(r.choice([0, 5, 48])), int(r.integers(1, 4))
+    pinned = bool(r.random() < 0.5)
+    data = _cells(r, k, n)
+    ref = _parity(codec, k, p, data)
+    units = data + ref
+    erased, present = _erasure(r, codec, k, p)
+    assert lib.ozec_set_tuning(b"host_zero_copy", zc) == 0 and lib.ozec_set_tuning(b"host_zc_chunks", zch) == 0
+    pool = None
+    try:
+        # the ozone_amd API, pinned or pageable cells
+        if pinned:
+            pool = host_alloc((k + p + len(erased)) * n + 64)
+            cell = [pool.array[u * n:(u + 1) * n] for u in range(k + p + len(erased))]
+            ins, outs = cell[:k], cell[k:k + p]
+            for a, d in zip(ins, data):
+                a[:] = d
+            for o in outs:
+                o[:] = 0xA5
+        else:
+            ins, outs = [d.copy() for d in data], [np.full(n, 0xA5, np.uint8) for _ in range(p)]
+        rc.RawErasureEncoder(rc.ECReplicationConfig(k, p, codec)).encode(ins, outs)
+        assert all((o == x).all() for o, x in zip(outs, ref)), (codec, k, p, n, zc, zch, pinned)
+        slots = [(cell[u] if pinned else units[u].copy()) if u in present else None for u in range(k + p)]
+        if pinned:
+            for u in range(k, k + p):
+                cell[u][:] = units[u]
+        got = cell[k + p:] if pinned else [np.zeros(n, np.uint8) for _ in erased]
+        for g in got:
+            g[:] = 0x5A
+        rc.RawErasureDecoder(rc.ECReplicationConfig(k, p, codec)).decode(slots, erased, got)
+        assert all((g == units[e]).all() for g, e in zip(got, erased)), (codec, k, p, n, erased, zc, zch, pinned)
+        if pinned:
+            del cell, ins, outs, slots, got
+        # the callback entry points
+        errors = []
+
+        def fill_from(src_units):
+            def fill(user, off, ln, dst):
+                try:
+                    for j, x in enumerate(src_units):
+                        if dst[j]:
+                            ctypes.memmove(dst[j], x[off:off + ln].ctypes.data, ln)
+                    return 0
+                except Exception as e:  # noqa: BLE001
+                    errors.append(e)
+                    return -99
+            return L.FILL_FN(fill)
+
+        def drain_to(dst_units):
+            def drain(user, off, ln, src):
+                try:
+                    for q, o in enumerate(dst_units):
+                        ctypes.memmove(o[off:off + ln].ctypes.data, src[q], ln)
+                    return 0
+                except Exception as e:  # noqa: BLE001
+                    errors.append(e)
+                    return -99
+            return L.DRAIN_FN(drain)
+
+        cid = L.OZEC_CODEC_RS if codec == "rs" else L.OZEC_CODEC_XOR
+        he, hd = ctypes.c_void_p(), ctypes.c_void_p()
+        assert lib.ozec_encoder_create(cid, k, p, ctypes.byref(he)) == 0
+        assert lib.ozec_decoder_create(cid, k, p, ctypes.byref(hd)) == 0
+        try:
+            cb_out = [np.full(n, 0xA5, np.uint8) for _ in range(p)]
+            f, d = fill_from(data), drain_to(cb_out)
+            assert lib.ozec_encode_cb(he, n, f, d, None) == 0, (L.last_error(), errors)
+            assert not errors and all((o == x).all() for o, x in zip(cb_out, ref)), (codec, k, p, n, zc, zch)
+            cb_got = [np.zeros(n, np.uint8) for _ in erased]
+            have = [units[u] if u in present else None for u in range(k + p)]
+            f, d = fill_from(have), drain_to(cb_got)
+            pres = (ctypes.c_uint8 * (k + p))(*[u in present for u in range(k + p)])
+            er = (ctypes.c_int * len(erased))(*erased)
+            assert lib.ozec_decode_cb(hd, pres, er, len(erased), n, f, d, None) == 0, (L.last_error(), errors)
+            assert not errors and all((g == units[e]).all() for g, e in zip(cb_got, erased)), \
+                (codec, k, p, n, erased, zc, zch)
+        finally:
+            for h in (he, hd):
+                lib.ozec_coder_release(h)
+                lib.ozec_coder_free(h)
+    finally:
+        lib.ozec_set_tuning(b"host_zero_copy", 48)
+        lib.ozec_set_tuning(b"host_zc_chunks", 2)
+        if pool is not None:
+            pool.free()

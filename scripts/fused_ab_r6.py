@@ -5,7 +5,8 @@
 Per case the route is forced through libozec's own routing knobs (fused: fused_min_units = rec_min_units = 0;
 unfused: both 2^62), checked with ozec_fused_routes, the outputs of the two routes compared byte for byte, and the
 call timed with HIP events on the launch stream (median of 5 rounds of 10 calls, the routes interleaved).  One JSON
-line per case.  usage: python scripts/fused_ab_r6.py"""
+line per case.  `full`: the WIDE form against the compact layout at a full 1,024-stripe batch instead.
+usage: python scripts/fused_ab_r6.py [full]"""
 import ctypes
 import json
 import os
@@ -136,6 +137,44 @@ def tail_cases():
             torch.cuda.empty_cache()
 
 
+def wide_vs_compact(S=1024):
+    """The WIDE form's own cost at a full batch: rs-6-3 encode + CRC32C of S stripes of 1 MiB cells with units 1.25 GiB
+    apart (WIDE: one buffer descriptor per unit) against the same stripes with units 1 MiB apart inside each stripe
+    (the C5dev layout), both on the fused route, median of 5 rounds of 10 calls, routes interleaved."""
+    k, p, n = 6, 3, 1 << 20
+    set_route(True)
+    us_wide = (5 << 30) // 4
+    nwin = n // BPC
+    res = {}
+    for name, unit_stride, stripe_stride, span in (("wide", us_wide, n, (k + p - 1) * us_wide + S * n),
+                                                   ("compact", n, (k + p) * n, S * (k + p) * n)):
+        buf = torch.empty(span + 64, dtype=torch.uint8, device="cuda")
+        buf.random_(0, 256)
+        enc = rc.RawErasureEncoder(rc.ECReplicationConfig(k, p))
+        crcs = torch.zeros((S, k + p, nwin), dtype=torch.int32, device="cuda")
+
+        def call(enc=enc, buf=buf, crcs=crcs, us=unit_stride, ss=stripe_stride):
+            enc.encode_crc_batch(buf, ss, us, buf[k * us:], ss, us, S, n, ck.ChecksumType.CRC32C, BPC, crcs)
+        r0 = routes()
+        call()
+        torch.cuda.synchronize()
+        assert routes()[0] > r0[0], name
+        res[name] = (call, buf, crcs)
+    times = {"wide": [], "compact": []}
+    for _ in range(5):
+        for name in ("wide", "compact"):
+            times[name].append(timed(res[name][0]))
+    moved = S * ((k + p) * n + (k + p) * nwin * 4)
+    out = {"case": f"WIDE vs compact, rs-6-3 encode + CRC32C, {S} stripes of 1 MiB, fused"}
+    for name in ("wide", "compact"):
+        ms = statistics.median(times[name])
+        out[name] = {"ms": round(ms, 4), "frac_of_8TBps": round(moved / (ms * 1e-3) / 8e12, 4)}
+    print(json.dumps(out), flush=True)
+
+
 if __name__ == "__main__":
-    wide_cases()
-    tail_cases()
+    if len(sys.argv) > 1 and sys.argv[1] == "full":
+        wide_vs_compact()
+    else:
+        wide_cases()
+        tail_cases()
